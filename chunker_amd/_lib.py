@@ -1,0 +1,100 @@
+"""ctypes binding of libchunker_amd.so (the C ABI in include/chunker_gpu.h).
+
+The shared library is built in-tree (chunker_amd/libchunker_amd.so, see
+chunker_amd/build.py).  If it is missing this module raises at import: the
+package has no CPU fallback path.
+"""
+from __future__ import annotations
+
+import ctypes
+from pathlib import Path
+
+import numpy as np
+
+LIB_PATH = Path(__file__).resolve().parent / "libchunker_amd.so"
+
+CG_OK = 0
+CG_E_BOUNDS = 1
+CG_E_IO = 2
+CG_E_ZERO_LENGTH_CHUNK = 3
+CG_E_INVALID_OPTIONS = 4
+CG_E_BUFFER_LIMIT = 5
+CG_E_CAPACITY = 6
+CG_E_NO_DEVICE = 7
+
+# cg_desc (48 bytes): ChunkDescriptor {offset, length, hash[32]}
+DESC_DTYPE = np.dtype([("offset", "<u8"), ("length", "<u8"), ("hash", "u1", (32,))])
+assert DESC_DTYPE.itemsize == 48
+
+# every exported symbol declared in include/chunker_gpu.h
+EXPORTS = (
+    "cg_abi_version", "cg_last_error_message", "cg_validate", "cg_capacity", "cg_chunk_descriptors",
+    "cg_chunk_batch", "cg_chunk_batch_device", "cg_push_new", "cg_push_push", "cg_push_finish",
+    "cg_push_bytes_consumed", "cg_push_out_capacity", "cg_push_free", "cg_hash_spans_device",
+    "cg_set_gear_table", "cg_get_gear_table", "cg_gear_is_placeholder", "cg_set_profiling",
+    "cg_last_stage_times", "cg_synth_nars",
+)
+
+
+def _load() -> ctypes.CDLL:
+    # PyTorch-ROCm ships its own libamdhip64 (SONAME libamdhip64.so.7) and links it as
+    # "libamdhip64.so".  Loading torch first makes our DT_NEEDED libamdhip64.so.7
+    # resolve to that same copy, so one process never holds two HIP runtimes.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    if not LIB_PATH.exists():
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(hipcc --offload-arch=gfx950). chunker_amd has no CPU fallback.")
+    L = ctypes.CDLL(str(LIB_PATH))
+    u64, sz, p, i = ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int
+    psz = ctypes.POINTER(sz)
+    L.cg_abi_version.restype = ctypes.c_uint32
+    L.cg_last_error_message.restype = ctypes.c_char_p
+    L.cg_validate.argtypes = [u64, u64, u64, ctypes.c_char_p, sz]
+    L.cg_validate.restype = i
+    L.cg_capacity.argtypes = [u64, u64]
+    L.cg_capacity.restype = sz
+    L.cg_chunk_descriptors.argtypes = [p, u64, u64, u64, u64, i, p, sz, psz]
+    L.cg_chunk_descriptors.restype = i
+    L.cg_chunk_batch.argtypes = [p, p, sz, u64, u64, u64, i, p, sz, p]
+    L.cg_chunk_batch.restype = i
+    L.cg_chunk_batch_device.argtypes = [p, p, sz, u64, u64, u64, i, p, sz, p, p]
+    L.cg_chunk_batch_device.restype = i
+    L.cg_push_new.argtypes = [u64, u64, u64, i, ctypes.POINTER(i)]
+    L.cg_push_new.restype = p
+    L.cg_push_push.argtypes = [p, p, u64, p, sz, psz]
+    L.cg_push_push.restype = i
+    L.cg_push_finish.argtypes = [p, p, sz, psz]
+    L.cg_push_finish.restype = i
+    L.cg_push_bytes_consumed.argtypes = [p]
+    L.cg_push_bytes_consumed.restype = u64
+    L.cg_push_out_capacity.argtypes = [p, u64]
+    L.cg_push_out_capacity.restype = sz
+    L.cg_push_free.argtypes = [p]
+    L.cg_push_free.restype = None
+    L.cg_hash_spans_device.argtypes = [p, p, p, sz, i, p, p]
+    L.cg_hash_spans_device.restype = i
+    L.cg_set_gear_table.argtypes = [p]
+    L.cg_set_gear_table.restype = i
+    L.cg_get_gear_table.argtypes = [p]
+    L.cg_get_gear_table.restype = None
+    L.cg_gear_is_placeholder.restype = i
+    L.cg_set_profiling.argtypes = [i]
+    L.cg_set_profiling.restype = None
+    L.cg_last_stage_times.argtypes = [p, sz]
+    L.cg_last_stage_times.restype = sz
+    L.cg_synth_nars.argtypes = [p, p, sz, i, u64]
+    L.cg_synth_nars.restype = None
+    return L
+
+
+lib = _load()
+assert lib.cg_abi_version() == 1
+
+
+def last_error() -> str:
+    msg = lib.cg_last_error_message()
+    return msg.decode() if msg else ""

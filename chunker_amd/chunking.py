@@ -1,0 +1,400 @@
+"""Host-side mirror of FlakeCache/chunker's chunking API (src/chunking.rs), backed by
+the gfx950 engine through the C ABI.
+
+Names, argument meaning and error behaviour follow the reference so its tests read
+the same here:
+
+=====================================  ======================================================
+this module                            reference (src/chunking.rs)
+=====================================  ======================================================
+ChunkingError and subclasses           ChunkingError :33-51 (same Display strings)
+HashAlgorithm                          :53-58
+ChunkMetadata / ChunkDescriptor        :76-155 (equality ignores payload, :120-134)
+ChunkingOptions.resolve                :157-231
+chunk_data / chunk_data_with_hash      :241-297
+chunk_descriptors[_with_hash]          :299-374
+ChunkStream                            :382-740 (read-slice sizing :713-716, env cap :427-433)
+PushChunker                            :742-829
+chunk_stream / chunk_stream_with_hash  :1132-1166
+=====================================  ======================================================
+
+Plus batch entry points the reference has no equivalent for (many NARs per call,
+device-resident inputs): chunk_batch, chunk_batch_device.
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+import os
+from dataclasses import dataclass, field
+from typing import BinaryIO, Iterator, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import DESC_DTYPE, lib
+
+DEFAULT_MIN = 256 * 1024
+DEFAULT_AVG = 1024 * 1024
+DEFAULT_MAX = 4 * 1024 * 1024
+
+# fastcdc::v2020 ranges [ext] (pinned by src/chunking.rs:1401-1415)
+MINIMUM_MIN, MINIMUM_MAX = 64, 1_048_576
+AVERAGE_MIN, AVERAGE_MAX = 256, 4_194_304
+MAXIMUM_MIN, MAXIMUM_MAX = 1024, 16_777_216
+
+DEFAULT_READ_SLICE_CAP = 8 * 1024 * 1024
+MAX_READ_SLICE_CAP = 256 * 1024 * 1024
+MIN_READ_SLICE_CAP = 4096
+
+
+# ---------------------------------------------------------------------------
+# errors (src/chunking.rs:33-51)
+# ---------------------------------------------------------------------------
+class ChunkingError(Exception):
+    """Base of the ChunkingError variants."""
+
+
+class BoundsError(ChunkingError):
+    def __init__(self, data_len: int, offset: int, length: int):
+        self.data_len, self.offset, self.length = data_len, offset, length
+        super().__init__(
+            f"bounds_check_failed: offset {offset} + length {length} exceeds data length {data_len}")
+
+
+class IoError(ChunkingError):
+    def __init__(self, msg: str):
+        super().__init__(f"io_error: {msg}")
+
+
+class ZeroLengthChunkError(ChunkingError):
+    def __init__(self):
+        super().__init__("zero_length_chunk: FastCDC returned a chunk with length 0")
+
+
+class InvalidOptionsError(ChunkingError):
+    def __init__(self, msg: str):
+        self.detail = msg
+        super().__init__(f"invalid_chunking_options: {msg}")
+
+
+class BufferLimitExceededError(ChunkingError):
+    def __init__(self, attempted: int, limit: int):
+        self.attempted, self.limit = attempted, limit
+        super().__init__(f"buffer_limit_exceeded: attempted {attempted} bytes, limit {limit} bytes")
+
+
+class DeviceUnavailableError(IoError):
+    """No gfx950 device: the engine has no CPU fallback (ABI status CG_E_NO_DEVICE)."""
+
+
+def _raise(status: int, data_len: int = 0) -> None:
+    msg = _lib.last_error()
+    if status == _lib.CG_E_INVALID_OPTIONS:
+        raise InvalidOptionsError(msg)
+    if status == _lib.CG_E_BOUNDS:
+        raise BoundsError(data_len, 0, 0)
+    if status == _lib.CG_E_ZERO_LENGTH_CHUNK:
+        raise ZeroLengthChunkError()
+    if status == _lib.CG_E_BUFFER_LIMIT:
+        raise BufferLimitExceededError(0, 0)
+    if status == _lib.CG_E_NO_DEVICE:
+        raise DeviceUnavailableError(msg)
+    raise IoError(msg or f"engine status {status}")
+
+
+def _check(status: int, data_len: int = 0) -> None:
+    if status != _lib.CG_OK:
+        _raise(status, data_len)
+
+
+# ---------------------------------------------------------------------------
+# value types
+# ---------------------------------------------------------------------------
+class HashAlgorithm(enum.IntEnum):
+    """HashAlgorithm (src/chunking.rs:53-58); values are the ABI's cg_hash_algo."""
+    Blake3 = 0
+    Sha256 = 1
+
+
+@dataclass(frozen=True)
+class ChunkDescriptor:
+    """ChunkDescriptor (src/chunking.rs:100-118)."""
+    hash: bytes
+    offset: int
+    length: int
+
+    def hash_hex(self) -> str:
+        return self.hash.hex()
+
+
+@dataclass(eq=False)
+class ChunkMetadata:
+    """ChunkMetadata (src/chunking.rs:76-98); equality/hash ignore payload (:120-134)."""
+    hash: bytes
+    offset: int
+    length: int
+    payload: bytes = field(default=b"", repr=False)
+
+    def hash_hex(self) -> str:
+        return self.hash.hex()
+
+    def __eq__(self, other) -> bool:
+        if not isinstance(other, ChunkMetadata):
+            return NotImplemented
+        return (self.hash, self.offset, self.length) == (other.hash, other.offset, other.length)
+
+    def __hash__(self) -> int:
+        return hash((self.hash, self.offset, self.length))
+
+
+@dataclass(frozen=True)
+class ChunkingOptions:
+    """ChunkingOptions (src/chunking.rs:157-231)."""
+    min_size: int
+    avg_size: int
+    max_size: int
+
+    @classmethod
+    def resolve(cls, min_size=None, avg_size=None, max_size=None) -> "ChunkingOptions":
+        o = cls(DEFAULT_MIN if min_size is None else int(min_size),
+                DEFAULT_AVG if avg_size is None else int(avg_size),
+                DEFAULT_MAX if max_size is None else int(max_size))
+        o.validate()
+        return o
+
+    def validate(self) -> None:
+        """src/chunking.rs:190-231, same order and messages (the ABI re-checks)."""
+        for name, v, lo, hi in (("min_size", self.min_size, MINIMUM_MIN, MINIMUM_MAX),
+                                ("avg_size", self.avg_size, AVERAGE_MIN, AVERAGE_MAX),
+                                ("max_size", self.max_size, MAXIMUM_MIN, MAXIMUM_MAX)):
+            if not lo <= v <= hi:
+                raise InvalidOptionsError(f"{name} must be in {lo}..={hi}, got {v}")
+        if self.min_size > self.avg_size:
+            raise InvalidOptionsError("min_size must be <= avg_size")
+        if self.avg_size > self.max_size:
+            raise InvalidOptionsError("avg_size must be <= max_size")
+
+
+# ---------------------------------------------------------------------------
+# helpers
+# ---------------------------------------------------------------------------
+def _as_u8(data) -> np.ndarray:
+    if isinstance(data, np.ndarray):
+        a = data.reshape(-1)
+        if a.dtype != np.uint8:
+            a = a.view(np.uint8)
+        return np.ascontiguousarray(a)
+    return np.frombuffer(memoryview(data).cast("B"), dtype=np.uint8)
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data if a.size else None
+
+
+def descriptors_to_list(arr: np.ndarray) -> list[ChunkDescriptor]:
+    return [ChunkDescriptor(bytes(r["hash"]), int(r["offset"]), int(r["length"])) for r in arr]
+
+
+# ---------------------------------------------------------------------------
+# eager API
+# ---------------------------------------------------------------------------
+def chunk_descriptors_array(data, min_size=None, avg_size=None, max_size=None,
+                            hash: HashAlgorithm = HashAlgorithm.Sha256) -> np.ndarray:
+    """chunk_descriptors_with_hash as a structured numpy array (DESC_DTYPE)."""
+    o = ChunkingOptions.resolve(min_size, avg_size, max_size)
+    a = _as_u8(data)
+    cap = max(lib.cg_capacity(len(a), o.min_size), 1)
+    out = np.zeros(cap, DESC_DTYPE)
+    n = ctypes.c_size_t(0)
+    _check(lib.cg_chunk_descriptors(_ptr(a), len(a), o.min_size, o.avg_size, o.max_size, int(hash),
+                                    out.ctypes.data, cap, ctypes.byref(n)), len(a))
+    return out[: n.value]
+
+
+def chunk_descriptors_with_hash(data, min_size=None, avg_size=None, max_size=None,
+                                hash: HashAlgorithm = HashAlgorithm.Sha256) -> list[ChunkDescriptor]:
+    """src/chunking.rs:323-374."""
+    return descriptors_to_list(chunk_descriptors_array(data, min_size, avg_size, max_size, hash))
+
+
+def chunk_descriptors(data, min_size=None, avg_size=None, max_size=None) -> list[ChunkDescriptor]:
+    """src/chunking.rs:308-315 (SHA-256)."""
+    return chunk_descriptors_with_hash(data, min_size, avg_size, max_size, HashAlgorithm.Sha256)
+
+
+def chunk_data_with_hash(data, min_size=None, avg_size=None, max_size=None,
+                         hash: HashAlgorithm = HashAlgorithm.Sha256) -> list[ChunkMetadata]:
+    """src/chunking.rs:256-297: descriptors plus an owned payload copy per chunk."""
+    a = _as_u8(data)
+    out = []
+    for d in chunk_descriptors_array(a, min_size, avg_size, max_size, hash):
+        off, ln = int(d["offset"]), int(d["length"])
+        if off + ln > len(a):  # bounds check (:268-287)
+            raise BoundsError(len(a), off, ln)
+        out.append(ChunkMetadata(bytes(d["hash"]), off, ln, a[off:off + ln].tobytes()))
+    return out
+
+
+def chunk_data(data, min_size=None, avg_size=None, max_size=None) -> list[ChunkMetadata]:
+    """src/chunking.rs:241-249 (SHA-256)."""
+    return chunk_data_with_hash(data, min_size, avg_size, max_size, HashAlgorithm.Sha256)
+
+
+# ---------------------------------------------------------------------------
+# batch API (one engine call for many independent NARs)
+# ---------------------------------------------------------------------------
+def chunk_batch(nars: Sequence, min_size=None, avg_size=None, max_size=None,
+                hash: HashAlgorithm = HashAlgorithm.Sha256) -> list[np.ndarray]:
+    """Chunk every NAR of `nars` independently (== one chunk_descriptors_with_hash
+    per NAR) in a single device pass; returns one descriptor array per NAR."""
+    o = ChunkingOptions.resolve(min_size, avg_size, max_size)
+    arrs = [_as_u8(x) for x in nars]
+    offs = np.zeros(len(arrs) + 1, np.uint64)
+    np.cumsum([len(x) for x in arrs], out=offs[1:])
+    flat = np.concatenate(arrs) if arrs else np.zeros(0, np.uint8)
+    cap = max(sum(lib.cg_capacity(len(x), o.min_size) for x in arrs), 1)
+    out = np.zeros(cap, DESC_DTYPE)
+    first = np.zeros(len(arrs) + 1, np.uint64)
+    _check(lib.cg_chunk_batch(_ptr(flat), offs.ctypes.data, len(arrs), o.min_size, o.avg_size, o.max_size,
+                              int(hash), out.ctypes.data, cap, first.ctypes.data), len(flat))
+    return [out[int(first[i]):int(first[i + 1])] for i in range(len(arrs))]
+
+
+def chunk_batch_device(d_data_ptr: int, nar_offsets: np.ndarray, d_out_ptr: int, out_cap: int,
+                       min_size=None, avg_size=None, max_size=None,
+                       hash: HashAlgorithm = HashAlgorithm.Sha256, stream: int = 0) -> np.ndarray:
+    """Device-resident batch: pointers are HIP device addresses (e.g. torch
+    tensor.data_ptr()); returns nar_first (n+1) with the per-NAR descriptor starts."""
+    o = ChunkingOptions.resolve(min_size, avg_size, max_size)
+    offs = np.ascontiguousarray(nar_offsets, dtype=np.uint64)
+    n = len(offs) - 1
+    first = np.zeros(n + 1, np.uint64)
+    _check(lib.cg_chunk_batch_device(ctypes.c_void_p(d_data_ptr), offs.ctypes.data, n, o.min_size,
+                                     o.avg_size, o.max_size, int(hash), ctypes.c_void_p(d_out_ptr), out_cap,
+                                     first.ctypes.data, ctypes.c_void_p(stream or None)))
+    return first
+
+
+def batch_capacity(nar_offsets: np.ndarray, min_size=None) -> int:
+    m = DEFAULT_MIN if min_size is None else int(min_size)
+    lens = np.diff(np.asarray(nar_offsets, dtype=np.uint64))
+    return int(sum(lib.cg_capacity(int(x), m) for x in lens))
+
+
+# ---------------------------------------------------------------------------
+# streaming
+# ---------------------------------------------------------------------------
+class PushChunker:
+    """PushChunker (src/chunking.rs:753-829): feed slices, get the chunks whose
+    content-defined boundaries are now final (with payloads)."""
+
+    def __init__(self, min_size=None, avg_size=None, max_size=None,
+                 hash: HashAlgorithm = HashAlgorithm.Sha256):
+        self.options = ChunkingOptions.resolve(min_size, avg_size, max_size)
+        self.hash = HashAlgorithm(hash)
+        st = ctypes.c_int(0)
+        o = self.options
+        self._h = lib.cg_push_new(o.min_size, o.avg_size, o.max_size, int(self.hash), ctypes.byref(st))
+        if not self._h:
+            _raise(st.value)
+        # payload bookkeeping (the engine returns descriptors; payloads are sliced here)
+        self._pending = bytearray()
+        self._pending_pos = 0
+
+    def _collect(self, arr: np.ndarray) -> list[ChunkMetadata]:
+        out = []
+        for d in arr:
+            off, ln = int(d["offset"]), int(d["length"])
+            rel = off - self._pending_pos
+            out.append(ChunkMetadata(bytes(d["hash"]), off, ln, bytes(self._pending[rel:rel + ln])))
+        if len(arr):
+            consumed = int(arr[-1]["offset"] + arr[-1]["length"]) - self._pending_pos
+            del self._pending[:consumed]
+            self._pending_pos += consumed
+        return out
+
+    def push(self, data) -> list[ChunkMetadata]:
+        a = _as_u8(data)
+        cap = lib.cg_push_out_capacity(self._h, len(a))
+        out = np.zeros(max(cap, 1), DESC_DTYPE)
+        n = ctypes.c_size_t(0)
+        st = lib.cg_push_push(self._h, _ptr(a), len(a), out.ctypes.data, len(out), ctypes.byref(n))
+        _check(st)
+        self._pending += a.tobytes()
+        return self._collect(out[: n.value])
+
+    def finish(self) -> list[ChunkMetadata]:
+        cap = lib.cg_push_out_capacity(self._h, 0)
+        out = np.zeros(max(cap, 1), DESC_DTYPE)
+        n = ctypes.c_size_t(0)
+        _check(lib.cg_push_finish(self._h, out.ctypes.data, len(out), ctypes.byref(n)))
+        return self._collect(out[: n.value])
+
+    def bytes_consumed(self) -> int:
+        return int(lib.cg_push_bytes_consumed(self._h))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib.cg_push_free(h)
+            self._h = None
+
+
+def effective_read_slice_cap() -> int:
+    """src/chunking.rs:427-433."""
+    try:
+        v = int(os.environ.get("CHUNKER_READ_SLICE_CAP_BYTES", ""))
+        if MIN_READ_SLICE_CAP <= v <= MAX_READ_SLICE_CAP:
+            return v
+    except ValueError:
+        pass
+    return DEFAULT_READ_SLICE_CAP
+
+
+class ChunkStream:
+    """ChunkStream (src/chunking.rs:382-740): pull chunks from a binary reader."""
+
+    def __init__(self, reader: BinaryIO, min_size=None, avg_size=None, max_size=None,
+                 hash: HashAlgorithm = HashAlgorithm.Sha256):
+        self._reader = reader
+        self._push = PushChunker(min_size, avg_size, max_size, hash)
+        self._max = self._push.options.max_size
+        self._pending: list[ChunkMetadata] = []
+        self._eof = False
+
+    @classmethod
+    def new_with_hash(cls, reader, min_size, avg_size, max_size, hash):
+        return cls(reader, min_size, avg_size, max_size, hash)
+
+    def __iter__(self) -> Iterator[ChunkMetadata]:
+        return self
+
+    def __next__(self) -> ChunkMetadata:
+        while True:
+            if self._pending:
+                return self._pending.pop(0)
+            if self._eof:
+                raise StopIteration
+            target = max(self._max * 8, 4 * 1024 * 1024)  # :713-716
+            read_size = max(min(target, effective_read_slice_cap()), MIN_READ_SLICE_CAP)
+            try:
+                buf = self._reader.read(read_size)
+            except OSError as e:
+                raise IoError(str(e)) from e
+            if not buf:
+                self._eof = True
+                self._pending.extend(self._push.finish())
+            else:
+                self._pending.extend(self._push.push(buf))
+
+
+def chunk_stream_with_hash(reader, min_size=None, avg_size=None, max_size=None,
+                           hash: HashAlgorithm = HashAlgorithm.Sha256) -> list[ChunkMetadata]:
+    """src/chunking.rs:1153-1166."""
+    return list(ChunkStream(reader, min_size, avg_size, max_size, hash))
+
+
+def chunk_stream(reader, min_size=None, avg_size=None, max_size=None) -> list[ChunkMetadata]:
+    """src/chunking.rs:1139-1146."""
+    return chunk_stream_with_hash(reader, min_size, avg_size, max_size, HashAlgorithm.Sha256)

@@ -1,0 +1,67 @@
+// common.h -- shared definitions of the gfx950 FastCDC + digest engine.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// One lane of the candidate scan owns SEG consecutive bytes of the flat batch
+// buffer, after a HALO-byte warm-up.  Every FastCDC v2020 mask lives in bits <= 47,
+// so 48 bytes of history make the rolling Gear hash's tested bits exact
+// (SURVEY.md Appendix A.3).
+#define CG_SEG 4096u
+#define CG_HALO 48u
+#define CG_SCAN_BLOCK 256u
+
+// Compacted candidate entry: (absolute position << 2) | flags.  flags bit1 = the
+// position passes mask_s, bit0 = it passes mask_l, 0 = "dense segment" marker
+// (the segment had more candidates than the per-segment capacity; the walker
+// rescans it exactly).
+#define CG_FLAG_S 2u
+#define CG_FLAG_L 1u
+
+// Device view of cg_desc (include/chunker_gpu.h): 48 bytes.
+struct DescRaw {
+    uint64_t offset, length;
+    uint8_t hash[32];
+};
+
+struct CdcParams {
+    uint64_t min, avg, max;
+    uint64_t mask_s, mask_l;
+};
+
+// Kernel launch wrappers (defined next to their kernels).
+namespace cg {
+
+void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint64_t mask_s, uint64_t mask_l,
+                 uint32_t cap, uint32_t *d_seg_count, uint32_t *d_seg_cand, uint64_t nseg, hipStream_t st);
+
+// Exclusive prefix sum of per-segment entry counts; writes d_out[0..n] (d_out[n] = total).
+// `cap` > 0 applies the entry transform (count <= cap ? count : 1).
+void launch_exclusive_scan_u32(const uint32_t *d_in, uint64_t *d_out, uint64_t n, uint32_t cap, uint64_t *d_tmp,
+                               hipStream_t st);
+size_t exclusive_scan_tmp_elems(uint64_t n);
+
+void launch_compact(const uint32_t *d_seg_count, const uint32_t *d_seg_cand, const uint64_t *d_eoff, uint32_t cap,
+                    uint64_t nseg, uint64_t *d_entries, hipStream_t st);
+
+void launch_walk(const uint8_t *d_data, const uint64_t *d_gear, const uint64_t *d_entries, const uint64_t *d_eoff,
+                 uint64_t nseg, const uint64_t *d_nar_off, const uint64_t *d_cap_base, uint64_t n_nars,
+                 CdcParams p, uint64_t *d_wchunk, uint32_t *d_nar_nchunks, hipStream_t st);
+
+void launch_assemble(const uint64_t *d_nar_off, const uint64_t *d_cap_base, const uint64_t *d_wchunk,
+                     const uint64_t *d_nar_first, uint64_t n_nars, void *d_out, uint64_t out_cap,
+                     uint64_t *d_chunk_abs, hipStream_t st);
+
+void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
+                   uint64_t max_chunks, uint8_t *d_hash_base, size_t hash_stride, hipStream_t st);
+
+void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
+                   uint64_t max_chunks, uint64_t total_bytes, uint8_t *d_hash_base, size_t hash_stride,
+                   uint64_t *d_group_count_tmp, uint64_t *d_group_base, uint32_t *d_gcount_u32,
+                   uint64_t *d_scan_tmp, uint32_t *d_gcv, hipStream_t st);
+size_t blake3_group_bound(uint64_t total_bytes, uint64_t max_chunks);
+
+void launch_spans_to_desc(const uint64_t *d_off, const uint64_t *d_len, uint64_t n, uint64_t *d_abs, void *d_desc,
+                          uint64_t *d_total, hipStream_t st);
+
+}  // namespace cg

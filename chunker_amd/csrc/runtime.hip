@@ -1,0 +1,700 @@
+// runtime.hip -- host runtime behind the C ABI (include/chunker_gpu.h).
+//
+// Per device: a pool of workspaces (device scratch grown on demand, a pinned
+// staging area, an own stream, timing events), the uploaded GEAR table, and lazy
+// once-only initialisation.  Every call takes a workspace from the pool, so the ABI
+// is re-entrant for the reference's concurrent callers (HTTP thread per
+// connection, BEAM dirty schedulers, rayon).  There is no CPU fallback: without a
+// usable gfx950 device every compute entry point returns CG_E_NO_DEVICE.
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/chunker_gpu.h"
+#include "common.h"
+#include "gear_table.h"
+
+namespace {
+
+static_assert(sizeof(cg_desc) == 48, "cg_desc must be 48 bytes");
+
+// reference defaults, src/chunking.rs:179-181
+constexpr uint64_t DEF_MIN = 256 * 1024, DEF_AVG = 1024 * 1024, DEF_MAX = 4 * 1024 * 1024;
+// fastcdc::v2020 ranges [ext], pinned by src/chunking.rs:1401-1415
+constexpr uint64_t MINIMUM_MIN = 64, MINIMUM_MAX = 1048576, AVERAGE_MIN = 256, AVERAGE_MAX = 4194304,
+                   MAXIMUM_MIN = 1024, MAXIMUM_MAX = 16777216;
+
+thread_local std::string t_err;
+thread_local std::vector<double> t_stage_ms;
+std::atomic<int> g_profiling{0};
+
+std::mutex g_gear_mu;
+uint64_t g_gear[256];
+bool g_gear_init = false;
+std::atomic<uint64_t> g_gear_epoch{1};
+std::atomic<int> g_gear_placeholder{CG_GEAR_IS_PLACEHOLDER};
+
+int fail(int code, const std::string &msg) {
+    t_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char *what) {
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation)
+        return fail(CG_E_BUFFER_LIMIT, std::string("device allocation failed: ") + what);
+    if (e == hipErrorNoDevice || e == hipErrorNoBinaryForGpu || e == hipErrorInvalidDevice)
+        return fail(CG_E_NO_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+    return fail(CG_E_IO, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr)                                   \
+    do {                                                \
+        hipError_t _e = (expr);                         \
+        if (_e != hipSuccess) return hip_fail(_e, #expr); \
+    } while (0)
+
+void gear_snapshot(uint64_t out[256]) {
+    std::lock_guard<std::mutex> g(g_gear_mu);
+    if (!g_gear_init) {
+        memcpy(g_gear, CG_DEFAULT_GEAR, sizeof g_gear);
+        g_gear_init = true;
+    }
+    memcpy(out, g_gear, sizeof g_gear);
+}
+
+uint32_t logarithm2(uint32_t v) { return (uint32_t)std::round(std::log2((double)v)); }
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes, const char *name) {
+        if (bytes <= cap) return CG_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = bytes + bytes / 4 + 256;
+        hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return hip_fail(e, name);
+        }
+        cap = want;
+        return CG_OK;
+    }
+    template <class T>
+    T *as() const { return static_cast<T *>(p); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+struct PinBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return CG_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = bytes + bytes / 4 + 256;
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return hip_fail(e, "hipHostMalloc");
+        }
+        cap = want;
+        return CG_OK;
+    }
+    template <class T>
+    T *as() const { return static_cast<T *>(p); }
+};
+
+enum { EV_START, EV_SCAN, EV_COMPACT, EV_WALK, EV_ASSEMBLE, EV_DIGEST, EV_N };
+
+struct Workspace {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    uint64_t gear_epoch = 0;
+    DevBuf gear, seg_count, seg_cand, eoff, scan_tmp, entries, nar_off, cap_base, wchunk, nar_nchunks, nar_first,
+        chunk_abs, b3_gcount, b3_gbase, b3_gcv, in, out, span_off, span_len;
+    PinBuf stage;
+    hipEvent_t ev[EV_N] = {};
+    int init(int dev) {
+        device = dev;
+        HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        for (auto &e : ev) HIP_TRY(hipEventCreate(&e));
+        return CG_OK;
+    }
+};
+
+struct DevicePool {
+    std::mutex mu;
+    std::vector<Workspace *> free_list;
+};
+constexpr int MAX_DEV = 64;
+DevicePool g_pools[MAX_DEV];
+
+int current_device(int *dev) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0)
+        return fail(CG_E_NO_DEVICE, "no HIP device visible: the chunker engine has no CPU fallback");
+    HIP_TRY(hipGetDevice(dev));
+    if (*dev < 0 || *dev >= MAX_DEV) return fail(CG_E_NO_DEVICE, "device index out of range");
+    return CG_OK;
+}
+
+int acquire(Workspace **out) {
+    int dev = 0, st = current_device(&dev);
+    if (st) return st;
+    DevicePool &pool = g_pools[dev];
+    {
+        std::lock_guard<std::mutex> g(pool.mu);
+        if (!pool.free_list.empty()) {
+            *out = pool.free_list.back();
+            pool.free_list.pop_back();
+            return CG_OK;
+        }
+    }
+    Workspace *ws = new Workspace();
+    st = ws->init(dev);
+    if (st) {
+        delete ws;
+        return st;
+    }
+    *out = ws;
+    return CG_OK;
+}
+
+void release(Workspace *ws) {
+    DevicePool &pool = g_pools[ws->device];
+    std::lock_guard<std::mutex> g(pool.mu);
+    pool.free_list.push_back(ws);
+}
+
+struct WsGuard {
+    Workspace *ws;
+    ~WsGuard() {
+        if (ws) release(ws);
+    }
+};
+
+int ensure_gear(Workspace *ws) {
+    const uint64_t epoch = g_gear_epoch.load();
+    if (ws->gear_epoch == epoch && ws->gear.p) return CG_OK;
+    int st = ws->gear.ensure(256 * sizeof(uint64_t), "gear");
+    if (st) return st;
+    uint64_t g[256];
+    gear_snapshot(g);
+    HIP_TRY(hipMemcpy(ws->gear.p, g, sizeof g, hipMemcpyHostToDevice));
+    ws->gear_epoch = epoch;
+    return CG_OK;
+}
+
+struct Opts {
+    uint64_t min, avg, max;
+};
+
+int resolve(uint64_t mn, uint64_t avg, uint64_t mx, Opts *o, char *msg, size_t cap) {
+    o->min = mn ? mn : DEF_MIN;
+    o->avg = avg ? avg : DEF_AVG;
+    o->max = mx ? mx : DEF_MAX;
+    char buf[160];
+    buf[0] = 0;
+    int st = CG_OK;
+    if (o->min < MINIMUM_MIN || o->min > MINIMUM_MAX) {
+        snprintf(buf, sizeof buf, "min_size must be in %llu..=%llu, got %llu", (unsigned long long)MINIMUM_MIN,
+                 (unsigned long long)MINIMUM_MAX, (unsigned long long)o->min);
+        st = CG_E_INVALID_OPTIONS;
+    } else if (o->avg < AVERAGE_MIN || o->avg > AVERAGE_MAX) {
+        snprintf(buf, sizeof buf, "avg_size must be in %llu..=%llu, got %llu", (unsigned long long)AVERAGE_MIN,
+                 (unsigned long long)AVERAGE_MAX, (unsigned long long)o->avg);
+        st = CG_E_INVALID_OPTIONS;
+    } else if (o->max < MAXIMUM_MIN || o->max > MAXIMUM_MAX) {
+        snprintf(buf, sizeof buf, "max_size must be in %llu..=%llu, got %llu", (unsigned long long)MAXIMUM_MIN,
+                 (unsigned long long)MAXIMUM_MAX, (unsigned long long)o->max);
+        st = CG_E_INVALID_OPTIONS;
+    } else if (o->min > o->avg) {
+        snprintf(buf, sizeof buf, "min_size must be <= avg_size");
+        st = CG_E_INVALID_OPTIONS;
+    } else if (o->avg > o->max) {
+        snprintf(buf, sizeof buf, "avg_size must be <= max_size");
+        st = CG_E_INVALID_OPTIONS;
+    }
+    if (msg && cap) {
+        strncpy(msg, buf, cap - 1);
+        msg[cap - 1] = 0;
+    }
+    if (st) return fail(st, buf);
+    return CG_OK;
+}
+
+uint64_t capacity_of(uint64_t len, uint64_t mn) {
+    if (len == 0) return 0;
+    const uint64_t step = std::max<uint64_t>(2 * (mn / 2), 1);
+    return len / step + 1;
+}
+
+// Per-segment candidate slots: ~2x the expected candidates per segment + 8,
+// rounded to a power of two, at most 64 (denser segments become markers).
+uint32_t seg_slots(const CdcParams &p) {
+    const double lam = CG_SEG * (std::ldexp(1.0, -__builtin_popcountll(p.mask_s)) +
+                                 std::ldexp(1.0, -__builtin_popcountll(p.mask_l)));
+    uint32_t c = 8;
+    while (c < 64 && c < 2 * lam + 8) c <<= 1;
+    return c;
+}
+
+// The whole device pipeline for one batch.  d_out receives descriptors; the
+// digest of descriptor g is written in place at d_out[g].hash.
+int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, size_t n_nars, const Opts &o,
+              int algo, cg_desc *d_out, size_t out_cap, uint64_t *h_nar_first, hipStream_t st) {
+    if (algo != CG_BLAKE3 && algo != CG_SHA256) return fail(CG_E_INVALID_OPTIONS, "unknown hash algorithm");
+    if (((uintptr_t)d_data & 15u) != 0) return fail(CG_E_IO, "device input must be 16-byte aligned");
+    int rc;
+    const uint64_t base0 = n_nars ? h_nar_off[0] : 0;
+    const uint64_t total_len = n_nars ? h_nar_off[n_nars] : 0;
+    for (size_t i = 0; i < n_nars; ++i)
+        if (h_nar_off[i + 1] < h_nar_off[i]) return fail(CG_E_BOUNDS, "nar offsets must be non-decreasing");
+    (void)base0;
+
+    CdcParams P;
+    const uint32_t bits = logarithm2((uint32_t)o.avg);
+    P.min = o.min;
+    P.avg = o.avg;
+    P.max = o.max;
+    P.mask_s = CG_MASKS[bits + 1];
+    P.mask_l = CG_MASKS[bits - 1];
+
+    // host staging: nar_off (n+1), cap_base (n+1), nar_first (n+1)
+    if ((rc = ws->stage.ensure(3 * (n_nars + 1) * sizeof(uint64_t)))) return rc;
+    uint64_t *s_off = ws->stage.as<uint64_t>();
+    uint64_t *s_cap = s_off + (n_nars + 1);
+    uint64_t *s_first = s_cap + (n_nars + 1);
+    memcpy(s_off, h_nar_off, (n_nars + 1) * sizeof(uint64_t));
+    uint64_t total_cap = 0;
+    for (size_t i = 0; i < n_nars; ++i) {
+        s_cap[i] = total_cap;
+        total_cap += capacity_of(h_nar_off[i + 1] - h_nar_off[i], o.min);
+    }
+    s_cap[n_nars] = total_cap;
+
+    const uint64_t nseg = (total_len + CG_SEG - 1) / CG_SEG;
+    const uint32_t slots = seg_slots(P);
+    const uint64_t chunk_bound = std::min<uint64_t>(total_cap, out_cap);
+    if ((rc = ensure_gear(ws))) return rc;
+    if ((rc = ws->seg_count.ensure((nseg + 1) * 4, "seg_count"))) return rc;
+    if ((rc = ws->seg_cand.ensure((nseg * slots + 1) * 4, "seg_cand"))) return rc;
+    if ((rc = ws->eoff.ensure((nseg + 1) * 8, "eoff"))) return rc;
+    const uint64_t scan_n = std::max<uint64_t>({nseg, (uint64_t)n_nars, total_cap, 1});
+    if ((rc = ws->scan_tmp.ensure(cg::exclusive_scan_tmp_elems(scan_n) * 8 + 64, "scan_tmp"))) return rc;
+    if ((rc = ws->entries.ensure((nseg * slots + 1) * 8, "entries"))) return rc;
+    if ((rc = ws->nar_off.ensure((n_nars + 1) * 8, "nar_off"))) return rc;
+    if ((rc = ws->cap_base.ensure((n_nars + 1) * 8, "cap_base"))) return rc;
+    if ((rc = ws->wchunk.ensure((total_cap + 1) * 16, "wchunk"))) return rc;
+    if ((rc = ws->nar_nchunks.ensure((n_nars + 1) * 4, "nar_nchunks"))) return rc;
+    if ((rc = ws->nar_first.ensure((n_nars + 1) * 8, "nar_first"))) return rc;
+    if ((rc = ws->chunk_abs.ensure((total_cap + 1) * 8, "chunk_abs"))) return rc;
+    if (algo == CG_BLAKE3) {
+        if ((rc = ws->b3_gcount.ensure((chunk_bound + 1) * 4, "b3_gcount"))) return rc;
+        if ((rc = ws->b3_gbase.ensure((chunk_bound + 1) * 8, "b3_gbase"))) return rc;
+        if ((rc = ws->b3_gcv.ensure((cg::blake3_group_bound(total_len, chunk_bound) + 1) * 32, "b3_gcv"))) return rc;
+    }
+
+    const bool prof = g_profiling.load() != 0;
+    if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_START], st));
+    HIP_TRY(hipMemcpyAsync(ws->nar_off.p, s_off, (n_nars + 1) * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ws->cap_base.p, s_cap, (n_nars + 1) * 8, hipMemcpyHostToDevice, st));
+
+    cg::launch_scan(d_data, total_len, ws->gear.as<uint64_t>(), P.mask_s, P.mask_l, slots,
+                    ws->seg_count.as<uint32_t>(), ws->seg_cand.as<uint32_t>(), nseg, st);
+    if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_SCAN], st));
+    cg::launch_exclusive_scan_u32(ws->seg_count.as<uint32_t>(), ws->eoff.as<uint64_t>(), nseg, slots,
+                                  ws->scan_tmp.as<uint64_t>(), st);
+    cg::launch_compact(ws->seg_count.as<uint32_t>(), ws->seg_cand.as<uint32_t>(), ws->eoff.as<uint64_t>(), slots,
+                       nseg, ws->entries.as<uint64_t>(), st);
+    if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_COMPACT], st));
+    cg::launch_walk(d_data, ws->gear.as<uint64_t>(), ws->entries.as<uint64_t>(), ws->eoff.as<uint64_t>(), nseg,
+                    ws->nar_off.as<uint64_t>(), ws->cap_base.as<uint64_t>(), n_nars, P, ws->wchunk.as<uint64_t>(),
+                    ws->nar_nchunks.as<uint32_t>(), st);
+    if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_WALK], st));
+    cg::launch_exclusive_scan_u32(ws->nar_nchunks.as<uint32_t>(), ws->nar_first.as<uint64_t>(), n_nars, 0,
+                                  ws->scan_tmp.as<uint64_t>(), st);
+    cg::launch_assemble(ws->nar_off.as<uint64_t>(), ws->cap_base.as<uint64_t>(), ws->wchunk.as<uint64_t>(),
+                        ws->nar_first.as<uint64_t>(), n_nars, d_out, out_cap, ws->chunk_abs.as<uint64_t>(), st);
+    if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_ASSEMBLE], st));
+    const uint64_t *d_total = ws->nar_first.as<uint64_t>() + n_nars;
+    uint8_t *hash_base = reinterpret_cast<uint8_t *>(d_out) + offsetof(cg_desc, hash);
+    if (algo == CG_SHA256) {
+        cg::launch_sha256(d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, hash_base,
+                          sizeof(cg_desc), st);
+    } else {
+        cg::launch_blake3(d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, total_len, hash_base,
+                          sizeof(cg_desc), nullptr, ws->b3_gbase.as<uint64_t>(), ws->b3_gcount.as<uint32_t>(),
+                          ws->scan_tmp.as<uint64_t>(), ws->b3_gcv.as<uint32_t>(), st);
+    }
+    if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_DIGEST], st));
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(s_first, ws->nar_first.p, (n_nars + 1) * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (prof) {
+        t_stage_ms.assign(EV_N - 1, 0.0);
+        for (int k = 1; k < EV_N; ++k) {
+            float ms = 0;
+            HIP_TRY(hipEventElapsedTime(&ms, ws->ev[k - 1], ws->ev[k]));
+            t_stage_ms[k - 1] = ms;
+        }
+    }
+    if (h_nar_first) memcpy(h_nar_first, s_first, (n_nars + 1) * 8);
+    if (s_first[n_nars] > out_cap) return fail(CG_E_CAPACITY, "descriptor output array too small");
+    return CG_OK;
+}
+
+int batch_host(const uint8_t *data, const uint64_t *nar_offsets, size_t n_nars, uint64_t mn, uint64_t avg,
+               uint64_t mx, int algo, cg_desc *out, size_t out_cap, uint64_t *nar_first) {
+    Opts o;
+    int rc = resolve(mn, avg, mx, &o, nullptr, 0);
+    if (rc) return rc;
+    Workspace *ws = nullptr;
+    if ((rc = acquire(&ws))) return rc;
+    WsGuard guard{ws};
+    const uint64_t lo = n_nars ? nar_offsets[0] : 0, hi = n_nars ? nar_offsets[n_nars] : 0;
+    const uint64_t bytes = hi - lo;
+    // device copy starts at nar_offsets[0]; offsets are rebased so the flat buffer starts at 0
+    std::vector<uint64_t> off(n_nars + 1);
+    for (size_t i = 0; i <= n_nars; ++i) off[i] = nar_offsets[i] - lo;
+    uint64_t total_cap = 0;
+    for (size_t i = 0; i < n_nars; ++i) total_cap += capacity_of(off[i + 1] - off[i], o.min);
+    if ((rc = ws->in.ensure(bytes + 256, "input"))) return rc;
+    if ((rc = ws->out.ensure((total_cap + 1) * sizeof(cg_desc), "descriptors"))) return rc;
+    if (bytes) HIP_TRY(hipMemcpyAsync(ws->in.p, data + lo, bytes, hipMemcpyHostToDevice, ws->stream));
+    std::vector<uint64_t> first(n_nars + 1);
+    rc = run_batch(ws, ws->in.as<uint8_t>(), off.data(), n_nars, o, algo, ws->out.as<cg_desc>(), total_cap,
+                   first.data(), ws->stream);
+    if (rc) return rc;
+    const uint64_t total = first[n_nars];
+    if (nar_first) memcpy(nar_first, first.data(), (n_nars + 1) * 8);
+    if (total > out_cap) return fail(CG_E_CAPACITY, "descriptor output array too small");
+    if (total) {
+        HIP_TRY(hipMemcpyAsync(out, ws->out.p, total * sizeof(cg_desc), hipMemcpyDeviceToHost, ws->stream));
+        HIP_TRY(hipStreamSynchronize(ws->stream));
+    }
+    return CG_OK;
+}
+
+// Digest-only pipeline over n device spans on `st` (shared by cg_hash_spans_device and cg_hash).
+int hash_spans(Workspace *ws, const uint8_t *d_data, const uint64_t *d_offsets, const uint64_t *d_lengths, size_t n,
+               int algo, uint8_t *d_digests, hipStream_t st) {
+    int rc;
+    if ((rc = ws->chunk_abs.ensure((n + 1) * 8, "chunk_abs"))) return rc;
+    if ((rc = ws->out.ensure((n + 1) * sizeof(cg_desc), "descriptors"))) return rc;
+    if ((rc = ws->nar_first.ensure(16, "total"))) return rc;
+    if ((rc = ws->scan_tmp.ensure(cg::exclusive_scan_tmp_elems(n) * 8 + 64, "scan_tmp"))) return rc;
+    uint64_t *d_total = ws->nar_first.as<uint64_t>();
+    cg::launch_spans_to_desc(d_offsets, d_lengths, n, ws->chunk_abs.as<uint64_t>(), ws->out.p, d_total, st);
+    uint8_t *hb = ws->out.as<uint8_t>() + offsetof(cg_desc, hash);
+    if (algo == CG_SHA256) {
+        cg::launch_sha256(d_data, ws->chunk_abs.as<uint64_t>(), ws->out.p, d_total, n, hb, sizeof(cg_desc), st);
+    } else {
+        // group-grid bound without reading lengths back: spans are capped at 16 MiB each
+        const uint64_t tb = (uint64_t)n * MAXIMUM_MAX;
+        const uint64_t gb = cg::blake3_group_bound(tb, n);
+        if ((rc = ws->b3_gcount.ensure((n + 1) * 4, "b3_gcount"))) return rc;
+        if ((rc = ws->b3_gbase.ensure((n + 1) * 8, "b3_gbase"))) return rc;
+        if ((rc = ws->b3_gcv.ensure((gb + 1) * 32, "b3_gcv"))) return rc;
+        cg::launch_blake3(d_data, ws->chunk_abs.as<uint64_t>(), ws->out.p, d_total, n, tb, hb, sizeof(cg_desc),
+                          nullptr, ws->b3_gbase.as<uint64_t>(), ws->b3_gcount.as<uint32_t>(),
+                          ws->scan_tmp.as<uint64_t>(), ws->b3_gcv.as<uint32_t>(), st);
+    }
+    HIP_TRY(hipMemcpy2DAsync(d_digests, 32, hb, sizeof(cg_desc), 32, n, hipMemcpyDeviceToDevice, st));
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(st));
+    return CG_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// PushChunker (src/chunking.rs:753-829) over drain_finalized_chunks (:541-673)
+// ---------------------------------------------------------------------------
+struct cg_push {
+    Opts o;
+    int algo;
+    std::vector<uint8_t> buf;
+    uint64_t position = 0;
+    bool finished = false;
+};
+
+namespace {
+
+int push_drain(cg_push *h, bool eof, cg_desc *out, size_t out_cap, size_t *n_out) {
+    *n_out = 0;
+    size_t n = 0;
+    uint64_t total = 0;
+    if (!h->buf.empty() && (h->buf.size() >= h->o.min || eof)) {
+        const uint64_t len = h->buf.size();
+        const uint64_t cap = capacity_of(len, h->o.min);
+        std::vector<cg_desc> tmp(cap);
+        uint64_t offs[2] = {0, len};
+        uint64_t first[2];
+        int rc = batch_host(h->buf.data(), offs, 1, h->o.min, h->o.avg, h->o.max, h->algo, tmp.data(), cap, first);
+        if (rc) return rc;
+        for (uint64_t k = 0; k < first[1]; ++k) {
+            const cg_desc &d = tmp[k];
+            if (d.length == 0) return fail(CG_E_ZERO_LENGTH_CHUNK, "FastCDC returned a chunk with length 0");
+            const bool touches_end = d.offset + d.length == len;
+            if (touches_end && !eof && d.length < h->o.max) break;  // retained tail (:579-584)
+            if (n >= out_cap) return fail(CG_E_CAPACITY, "push output array too small");
+            out[n] = d;
+            out[n].offset += h->position;
+            ++n;
+            total += d.length;
+        }
+        h->buf.erase(h->buf.begin(), h->buf.begin() + (ptrdiff_t)total);
+        h->position += total;
+    }
+    if (eof && !h->buf.empty()) {  // defensive EOF remainder (:651-670)
+        if (n >= out_cap) return fail(CG_E_CAPACITY, "push output array too small");
+        uint64_t offs[2] = {0, h->buf.size()};
+        // a buffer below min is one chunk by FastCDC's first rule; digest it through the same path
+        cg_desc d;
+        uint64_t first[2];
+        int rc = batch_host(h->buf.data(), offs, 1, h->o.min, h->o.avg, h->o.max, h->algo, &d, 1, first);
+        if (rc) return rc;
+        d.offset = h->position;
+        d.length = h->buf.size();
+        out[n++] = d;
+        h->position += h->buf.size();
+        h->buf.clear();
+    }
+    *n_out = n;
+    return CG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t cg_abi_version(void) { return CG_ABI_VERSION; }
+
+const char *cg_last_error_message(void) { return t_err.c_str(); }
+
+int cg_validate(uint64_t min_size, uint64_t avg_size, uint64_t max_size, char *msg, size_t msg_cap) {
+    Opts o;
+    return resolve(min_size, avg_size, max_size, &o, msg, msg_cap);
+}
+
+size_t cg_capacity(uint64_t len, uint64_t min_size) { return capacity_of(len, min_size ? min_size : DEF_MIN); }
+
+int cg_chunk_batch(const uint8_t *data, const uint64_t *nar_offsets, size_t n_nars, uint64_t min_size,
+                   uint64_t avg_size, uint64_t max_size, int algo, cg_desc *out, size_t out_cap,
+                   uint64_t *nar_first) {
+    t_err.clear();
+    return batch_host(data, nar_offsets, n_nars, min_size, avg_size, max_size, algo, out, out_cap, nar_first);
+}
+
+int cg_chunk_descriptors(const uint8_t *data, uint64_t len, uint64_t min_size, uint64_t avg_size,
+                         uint64_t max_size, int algo, cg_desc *out, size_t out_cap, size_t *n_out) {
+    t_err.clear();
+    uint64_t offs[2] = {0, len};
+    uint64_t first[2] = {0, 0};
+    int rc = batch_host(data, offs, 1, min_size, avg_size, max_size, algo, out, out_cap, first);
+    if (n_out) *n_out = rc == CG_OK ? first[1] : 0;
+    return rc;
+}
+
+int cg_chunk_batch_device(const uint8_t *d_data, const uint64_t *nar_offsets, size_t n_nars, uint64_t min_size,
+                          uint64_t avg_size, uint64_t max_size, int algo, cg_desc *d_out, size_t out_cap,
+                          uint64_t *nar_first, void *stream) {
+    t_err.clear();
+    Opts o;
+    int rc = resolve(min_size, avg_size, max_size, &o, nullptr, 0);
+    if (rc) return rc;
+    if (n_nars && nar_offsets[0] != 0) return fail(CG_E_BOUNDS, "device batch offsets must start at 0");
+    Workspace *ws = nullptr;
+    if ((rc = acquire(&ws))) return rc;
+    WsGuard guard{ws};
+    return run_batch(ws, d_data, nar_offsets, n_nars, o, algo, d_out, out_cap, nar_first,
+                     static_cast<hipStream_t>(stream));
+}
+
+int cg_hash_spans_device(const uint8_t *d_data, const uint64_t *d_offsets, const uint64_t *d_lengths, size_t n,
+                         int algo, uint8_t *d_digests, void *stream) {
+    t_err.clear();
+    if (algo != CG_BLAKE3 && algo != CG_SHA256) return fail(CG_E_INVALID_OPTIONS, "unknown hash algorithm");
+    if (n == 0) return CG_OK;
+    Workspace *ws = nullptr;
+    int rc = acquire(&ws);
+    if (rc) return rc;
+    WsGuard guard{ws};
+    return hash_spans(ws, d_data, d_offsets, d_lengths, n, algo, d_digests, static_cast<hipStream_t>(stream));
+}
+
+int cg_hash(const uint8_t *data, uint64_t len, int algo, uint8_t out[32]) {
+    t_err.clear();
+    if (algo != CG_BLAKE3 && algo != CG_SHA256) return fail(CG_E_INVALID_OPTIONS, "unknown hash algorithm");
+    if (algo == CG_BLAKE3 && len > MAXIMUM_MAX) return fail(CG_E_BOUNDS, "cg_hash: BLAKE3 input above 16 MiB");
+    Workspace *ws = nullptr;
+    int rc = acquire(&ws);
+    if (rc) return rc;
+    WsGuard guard{ws};
+    if ((rc = ws->in.ensure(len + 256, "input"))) return rc;
+    if ((rc = ws->span_off.ensure(64, "span"))) return rc;
+    if ((rc = ws->stage.ensure(64))) return rc;
+    uint64_t *s = ws->stage.as<uint64_t>();
+    s[0] = 0;
+    s[1] = len;
+    if (len) HIP_TRY(hipMemcpyAsync(ws->in.p, data, len, hipMemcpyHostToDevice, ws->stream));
+    HIP_TRY(hipMemcpyAsync(ws->span_off.p, s, 16, hipMemcpyHostToDevice, ws->stream));
+    const uint64_t *d_off = ws->span_off.as<uint64_t>();
+    uint8_t *d_dig = reinterpret_cast<uint8_t *>(ws->span_off.as<uint64_t>() + 2);
+    if ((rc = hash_spans(ws, ws->in.as<uint8_t>(), d_off, d_off + 1, 1, algo, d_dig, ws->stream))) return rc;
+    HIP_TRY(hipMemcpyAsync(s + 2, d_dig, 32, hipMemcpyDeviceToHost, ws->stream));
+    HIP_TRY(hipStreamSynchronize(ws->stream));
+    memcpy(out, s + 2, 32);
+    return CG_OK;
+}
+
+cg_push *cg_push_new(uint64_t min_size, uint64_t avg_size, uint64_t max_size, int algo, int *status) {
+    t_err.clear();
+    Opts o;
+    int rc = resolve(min_size, avg_size, max_size, &o, nullptr, 0);
+    if (!rc && algo != CG_BLAKE3 && algo != CG_SHA256) rc = fail(CG_E_INVALID_OPTIONS, "unknown hash algorithm");
+    if (status) *status = rc;
+    if (rc) return nullptr;
+    cg_push *h = new cg_push();
+    h->o = o;
+    h->algo = algo;
+    return h;
+}
+
+int cg_push_push(cg_push *h, const uint8_t *data, uint64_t len, cg_desc *out, size_t out_cap, size_t *n_out) {
+    t_err.clear();
+    if (n_out) *n_out = 0;
+    if (!h) return fail(CG_E_IO, "null push handle");
+    if (h->finished) return fail(CG_E_INVALID_OPTIONS, "push called after finish");
+    if (len == 0) return CG_OK;
+    h->buf.insert(h->buf.end(), data, data + len);
+    size_t n = 0;
+    int rc = push_drain(h, false, out, out_cap, &n);
+    if (n_out) *n_out = n;
+    return rc;
+}
+
+int cg_push_finish(cg_push *h, cg_desc *out, size_t out_cap, size_t *n_out) {
+    t_err.clear();
+    if (n_out) *n_out = 0;
+    if (!h) return fail(CG_E_IO, "null push handle");
+    h->finished = true;
+    size_t n = 0;
+    int rc = push_drain(h, true, out, out_cap, &n);
+    if (n_out) *n_out = n;
+    return rc;
+}
+
+uint64_t cg_push_bytes_consumed(const cg_push *h) { return h ? h->position + h->buf.size() : 0; }
+
+size_t cg_push_out_capacity(const cg_push *h, uint64_t next_len) {
+    return h ? capacity_of(h->buf.size() + next_len, h->o.min) + 1 : 0;
+}
+
+void cg_push_free(cg_push *h) { delete h; }
+
+int cg_set_gear_table(const uint64_t gear[256]) {
+    {
+        std::lock_guard<std::mutex> g(g_gear_mu);
+        memcpy(g_gear, gear, sizeof g_gear);
+        g_gear_init = true;
+    }
+    g_gear_placeholder.store(memcmp(gear, CG_DEFAULT_GEAR, sizeof g_gear) == 0 ? CG_GEAR_IS_PLACEHOLDER : 0);
+    g_gear_epoch.fetch_add(1);
+    return CG_OK;
+}
+
+void cg_get_gear_table(uint64_t gear[256]) { gear_snapshot(gear); }
+
+int cg_gear_is_placeholder(void) { return g_gear_placeholder.load(); }
+
+void cg_set_profiling(int on) { g_profiling.store(on ? 1 : 0); }
+
+size_t cg_last_stage_times(double *ms, size_t n) {
+    const size_t k = std::min(n, t_stage_ms.size());
+    for (size_t i = 0; i < k; ++i) ms[i] = t_stage_ms[i];
+    return k;
+}
+
+void cg_synth_nars(uint8_t *out, const uint64_t *nar_sizes, size_t n, int zeros, uint64_t first_index) {
+    std::vector<uint64_t> off(n + 1, 0);
+    for (size_t i = 0; i < n; ++i) off[i + 1] = off[i] + nar_sizes[i];
+    auto one = [&](size_t i) {
+        uint8_t *p = out + off[i];
+        const uint64_t S = nar_sizes[i];
+        const uint64_t L = S >= 112 ? S - 112 : 0;  // payload; framing is 112 bytes for a regular file
+        uint64_t at = 0;
+        auto put_u64 = [&](uint64_t v) {
+            memcpy(p + at, &v, 8);
+            at += 8;
+        };
+        auto put_str = [&](const char *s) {
+            const uint64_t l = strlen(s);
+            put_u64(l);
+            memset(p + at, 0, (l + 7) / 8 * 8);
+            memcpy(p + at, s, l);
+            at += (l + 7) / 8 * 8;
+        };
+        put_str("nix-archive-1");
+        put_str("(");
+        put_str("type");
+        put_str("regular");
+        put_str("contents");
+        put_u64(L);
+        if (zeros) {
+            memset(p + at, 0, L);
+        } else {  // xorshift64, crates/node/src/lib.rs:192-203
+            uint64_t state = (0x9E3779B97F4A7C15ull ^ (first_index + i)) | 1ull;
+            uint64_t k = 0;
+            for (; k + 8 <= L; k += 8) {
+                state ^= state << 13;
+                state ^= state >> 7;
+                state ^= state << 17;
+                memcpy(p + at + k, &state, 8);
+            }
+            if (k < L) {
+                state ^= state << 13;
+                state ^= state >> 7;
+                state ^= state << 17;
+                memcpy(p + at + k, &state, L - k);
+            }
+        }
+        at += L;
+        // payload padded to 8 (L may be unaligned only if S is not a multiple of 8)
+        const uint64_t pad = (8 - (L & 7)) & 7;
+        memset(p + at, 0, std::min<uint64_t>(pad, S - std::min(S, at)));
+        at += pad;
+        if (at + 16 <= S) {
+            put_str(")");
+        }
+    };
+    const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    if (n <= 1 || nt == 1) {
+        for (size_t i = 0; i < n; ++i) one(i);
+        return;
+    }
+    std::atomic<size_t> next{0};
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t)
+        th.emplace_back([&]() {
+            for (size_t i; (i = next.fetch_add(1)) < n;) one(i);
+        });
+    for (auto &t : th) t.join();
+}
+
+}  // extern "C"

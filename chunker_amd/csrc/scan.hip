@@ -1,0 +1,210 @@
+// scan.hip -- K1: data-parallel FastCDC v2020 boundary-candidate scan, and the
+// device prefix sum + compaction that turn per-segment candidates into one sorted
+// candidate list for the cut walk (K2, walk.hip).
+//
+// Replaces the serial Gear loop inside fastcdc's `cut_gear` [ext], called from
+// chunk_descriptors_with_hash (src/chunking.rs:334-336).  The rolling hash
+// h = (h << 1) + GEAR[b] is evaluated for every byte of the flat batch buffer with
+// a 48-byte warm-up per lane segment; because every mask lives in bits <= 47,
+// the tested bits equal those of the crate's per-chunk hash for every position at
+// least 47 bytes past the chunk's hash start.  The 47
+// positions before that are recomputed exactly by the walker.
+#include "common.h"
+
+namespace cg {
+
+// One Gear step + both mask tests for one byte.  Returns the 2-bit flag set.
+__device__ __forceinline__ uint32_t gear_step(uint64_t &h, uint32_t byte, const uint64_t *__restrict__ gear,
+                                              uint64_t mask_s, uint64_t mask_l) {
+    h = (h << 1) + gear[byte];
+    return (((h & mask_s) == 0) ? CG_FLAG_S : 0u) | (((h & mask_l) == 0) ? CG_FLAG_L : 0u);
+}
+
+__global__ __launch_bounds__(CG_SCAN_BLOCK) void k_scan(const uint8_t *__restrict__ data, uint64_t n,
+                                                         const uint64_t *__restrict__ gear_g, uint64_t mask_s,
+                                                         uint64_t mask_l, uint32_t cap,
+                                                         uint32_t *__restrict__ seg_count,
+                                                         uint32_t *__restrict__ seg_cand, uint64_t nseg) {
+    __shared__ uint64_t gear[256];
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) gear[i] = gear_g[i];
+    __syncthreads();
+
+    const uint64_t seg = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (seg >= nseg) return;
+    const uint64_t start = seg * CG_SEG;
+    const uint64_t end = start + CG_SEG < n ? start + CG_SEG : n;
+
+    uint64_t h = 0;
+    if (start >= CG_HALO) {  // warm-up: the 48 bytes before the segment (16-B aligned)
+        const uint4 *hp = reinterpret_cast<const uint4 *>(data + start - CG_HALO);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const uint4 v = hp[k];
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) h = (h << 1) + gear[(w[j] >> (8 * b)) & 0xffu];
+        }
+    }
+
+    uint32_t count = 0;
+    uint32_t *cand = seg_cand + seg * cap;
+    uint64_t p = start;
+    for (; p + 16 <= end; p += 16) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(data + p);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const uint32_t f = gear_step(h, (w[j] >> (8 * b)) & 0xffu, gear, mask_s, mask_l);
+                if (f) {
+                    if (count < cap) cand[count] = ((uint32_t)(p - start + 4 * j + b) << 2) | f;
+                    ++count;
+                }
+            }
+        }
+    }
+    for (; p < end; ++p) {  // ragged tail of the last segment
+        const uint32_t f = gear_step(h, data[p], gear, mask_s, mask_l);
+        if (f) {
+            if (count < cap) cand[count] = ((uint32_t)(p - start) << 2) | f;
+            ++count;
+        }
+    }
+    seg_count[seg] = count;
+}
+
+void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint64_t mask_s, uint64_t mask_l,
+                 uint32_t cap, uint32_t *d_seg_count, uint32_t *d_seg_cand, uint64_t nseg, hipStream_t st) {
+    if (nseg == 0) return;
+    const uint64_t blocks = (nseg + CG_SCAN_BLOCK - 1) / CG_SCAN_BLOCK;
+    hipLaunchKernelGGL(k_scan, dim3((uint32_t)blocks), dim3(CG_SCAN_BLOCK), 0, st, d_data, n, d_gear, mask_s,
+                       mask_l, cap, d_seg_count, d_seg_cand, nseg);
+}
+
+// ---------------------------------------------------------------------------
+// Exclusive prefix sum u32 -> u64 (three launches: tile sums, top scan, apply).
+// ---------------------------------------------------------------------------
+#define SCAN_T 256u
+#define SCAN_ITEMS 8u
+#define SCAN_TILE (SCAN_T * SCAN_ITEMS)
+
+__device__ __forceinline__ uint64_t xform(uint32_t v, uint32_t cap) { return cap ? (v <= cap ? v : 1u) : v; }
+
+// Block-wide inclusive scan of one u64 per thread (wave64 shuffles + LDS).
+__device__ __forceinline__ uint64_t block_inclusive_scan(uint64_t v, uint64_t *s_wave) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint64_t t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    if (lane == 63) s_wave[wave] = v;
+    __syncthreads();
+    uint64_t add = 0;
+    for (uint32_t w = 0; w < wave; ++w) add += s_wave[w];
+    __syncthreads();
+    return v + add;
+}
+
+__global__ __launch_bounds__(SCAN_T) void k_tile_sums(const uint32_t *__restrict__ in, uint64_t n, uint32_t cap,
+                                                      uint64_t *__restrict__ tile_sum) {
+    __shared__ uint64_t s_wave[SCAN_T / 64];
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_ITEMS;
+    uint64_t s = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_ITEMS; ++k)
+        if (base + k < n) s += xform(in[base + k], cap);
+    const uint64_t inc = block_inclusive_scan(s, s_wave);
+    if (threadIdx.x == SCAN_T - 1) tile_sum[blockIdx.x] = inc;
+}
+
+// Single block: exclusive scan of tile sums in place; total to tile_sum[ntiles].
+__global__ __launch_bounds__(1024) void k_top_scan(uint64_t *__restrict__ tile_sum, uint64_t ntiles) {
+    __shared__ uint64_t s_wave[16];
+    __shared__ uint64_t s_carry;
+    if (threadIdx.x == 0) s_carry = 0;
+    __syncthreads();
+    for (uint64_t b = 0; b < ntiles; b += 1024) {
+        const uint64_t i = b + threadIdx.x;
+        const uint64_t v = i < ntiles ? tile_sum[i] : 0;
+        const uint64_t inc = block_inclusive_scan(v, s_wave);
+        const uint64_t carry = s_carry;
+        if (i < ntiles) tile_sum[i] = carry + inc - v;
+        __syncthreads();
+        if (threadIdx.x == 1023) s_carry = carry + inc;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) tile_sum[ntiles] = s_carry;
+}
+
+__global__ __launch_bounds__(SCAN_T) void k_scan_apply(const uint32_t *__restrict__ in, uint64_t n, uint32_t cap,
+                                                       const uint64_t *__restrict__ tile_sum,
+                                                       uint64_t *__restrict__ out, uint64_t ntiles) {
+    __shared__ uint64_t s_wave[SCAN_T / 64];
+    const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_ITEMS;
+    uint64_t v[SCAN_ITEMS];
+    uint64_t s = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_ITEMS; ++k) {
+        v[k] = base + k < n ? xform(in[base + k], cap) : 0;
+        s += v[k];
+    }
+    const uint64_t inc = block_inclusive_scan(s, s_wave);
+    uint64_t run = tile_sum[blockIdx.x] + inc - s;
+#pragma unroll
+    for (uint32_t k = 0; k < SCAN_ITEMS; ++k) {
+        if (base + k < n) out[base + k] = run;
+        run += v[k];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = tile_sum[ntiles];
+}
+
+size_t exclusive_scan_tmp_elems(uint64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE + 1; }
+
+void launch_exclusive_scan_u32(const uint32_t *d_in, uint64_t *d_out, uint64_t n, uint32_t cap, uint64_t *d_tmp,
+                               hipStream_t st) {
+    const uint64_t ntiles = n ? (n + SCAN_TILE - 1) / SCAN_TILE : 0;
+    if (ntiles == 0) {
+        (void)hipMemsetAsync(d_out, 0, sizeof(uint64_t), st);
+        return;
+    }
+    hipLaunchKernelGGL(k_tile_sums, dim3((uint32_t)ntiles), dim3(SCAN_T), 0, st, d_in, n, cap, d_tmp);
+    hipLaunchKernelGGL(k_top_scan, dim3(1), dim3(1024), 0, st, d_tmp, ntiles);
+    hipLaunchKernelGGL(k_scan_apply, dim3((uint32_t)ntiles), dim3(SCAN_T), 0, st, d_in, n, cap, d_tmp, d_out,
+                       ntiles);
+}
+
+// ---------------------------------------------------------------------------
+// Compaction: per-segment candidate slots -> one sorted entry list.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_compact(const uint32_t *__restrict__ seg_count,
+                                                 const uint32_t *__restrict__ seg_cand,
+                                                 const uint64_t *__restrict__ eoff, uint32_t cap, uint64_t nseg,
+                                                 uint64_t *__restrict__ entries) {
+    const uint64_t seg = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (seg >= nseg) return;
+    const uint32_t count = seg_count[seg];
+    if (count == 0) return;
+    const uint64_t base = eoff[seg];
+    const uint64_t start = seg * CG_SEG;
+    if (count <= cap) {
+        for (uint32_t k = 0; k < count; ++k) {
+            const uint32_t e = seg_cand[seg * cap + k];
+            entries[base + k] = ((start + (e >> 2)) << 2) | (e & 3u);
+        }
+    } else {
+        entries[base] = start << 2;  // dense-segment marker
+    }
+}
+
+void launch_compact(const uint32_t *d_seg_count, const uint32_t *d_seg_cand, const uint64_t *d_eoff, uint32_t cap,
+                    uint64_t nseg, uint64_t *d_entries, hipStream_t st) {
+    if (nseg == 0) return;
+    hipLaunchKernelGGL(k_compact, dim3((uint32_t)((nseg + 255) / 256)), dim3(256), 0, st, d_seg_count, d_seg_cand,
+                       d_eoff, cap, nseg, d_entries);
+}
+
+}  // namespace cg

@@ -1,0 +1,133 @@
+/*
+ * chunker_gpu.h -- C ABI of the MI355X (gfx950) FastCDC + per-chunk digest engine.
+ *
+ * This is the drop-in boundary for FlakeCache/chunker's hot path.  Each entry point
+ * names the reference interface it replaces (paths are into the FlakeCache/chunker
+ * tree).  The ABI uses plain pointers and sizes only; no HIP, torch or Rust types.
+ * A Rust binding for it is given in INTEGRATION.md (the `chunker-hip` shim crate
+ * that `chunker`'s `chunk_descriptors_with_hash` / `PushChunker` dispatch to behind
+ * a cargo feature, since the reference crate is `unsafe_code = "forbid"`,
+ * Cargo.toml:120).
+ *
+ * Threading: every entry point is re-entrant.  Device state is initialised once per
+ * device, lazily; each call takes a workspace from a per-device pool.  A cg_push
+ * handle is single-owner (the NIF already serialises it, src/nif.rs:285-297).
+ * No entry point panics or aborts: failures are status codes plus a thread-local
+ * message (cg_last_error_message).
+ */
+#ifndef CHUNKER_GPU_H
+#define CHUNKER_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CG_ABI_VERSION 1u
+
+/* Status codes.  1..5 map 1:1 onto ChunkingError (src/chunking.rs:33-51) so the
+ * host shim can rebuild the exact Display strings. */
+typedef enum {
+    CG_OK = 0,
+    CG_E_BOUNDS = 1,             /* ChunkingError::Bounds */
+    CG_E_IO = 2,                 /* ChunkingError::Io (HIP runtime errors map here) */
+    CG_E_ZERO_LENGTH_CHUNK = 3,  /* ChunkingError::ZeroLengthChunk */
+    CG_E_INVALID_OPTIONS = 4,    /* ChunkingError::InvalidOptions(msg) */
+    CG_E_BUFFER_LIMIT = 5,       /* ChunkingError::BufferLimitExceeded (device OOM) */
+    CG_E_CAPACITY = 6,           /* ABI only: caller's output array too small */
+    CG_E_NO_DEVICE = 7,          /* ABI only: no gfx950 device; there is no CPU fallback */
+} cg_status;
+
+/* HashAlgorithm (src/chunking.rs:53-58), same declaration order. */
+typedef enum { CG_BLAKE3 = 0, CG_SHA256 = 1 } cg_hash_algo;
+
+/* ChunkDescriptor (src/chunking.rs:100-110): 48 bytes, offsets relative to the NAR. */
+typedef struct {
+    uint64_t offset;
+    uint64_t length;
+    uint8_t hash[32];
+} cg_desc;
+
+uint32_t cg_abi_version(void);
+
+/* Thread-local message of the last failing call on this thread ("" if none).  For
+ * CG_E_INVALID_OPTIONS it is exactly the InvalidOptions payload of
+ * ChunkingOptions::validate (src/chunking.rs:190-231). */
+const char *cg_last_error_message(void);
+
+/* ChunkingOptions::resolve/validate (src/chunking.rs:173-231).  Pass 0 for a size to
+ * take the reference default (256 KiB / 1 MiB / 4 MiB, :179-181).  `msg` may be NULL. */
+int cg_validate(uint64_t min_size, uint64_t avg_size, uint64_t max_size, char *msg, size_t msg_cap);
+
+/* Upper bound on the descriptors one input of `len` bytes can produce:
+ * floor(len / (2*floor(min/2))) + 1 (every non-final cut is >= 2*floor(min/2)). */
+size_t cg_capacity(uint64_t len, uint64_t min_size);
+
+/* chunk_descriptors_with_hash (src/chunking.rs:323-374) on one host buffer.
+ * Replaces `FastCDC::new(..).collect()` + the rayon `compute_hash` pass.  `data` is
+ * borrowed (pageable is fine; the library stages it).  Writes *n_out descriptors. */
+int cg_chunk_descriptors(const uint8_t *data, uint64_t len, uint64_t min_size, uint64_t avg_size,
+                         uint64_t max_size, int algo, cg_desc *out, size_t out_cap, size_t *n_out);
+
+/* Batch of independent NARs in one host buffer: NAR i is
+ * data[nar_offsets[i] .. nar_offsets[i+1]).  Descriptors are written NAR after NAR;
+ * nar_first[i] = index of NAR i's first descriptor, nar_first[n_nars] = total.
+ * Equivalent to one chunk_descriptors_with_hash call per NAR. */
+int cg_chunk_batch(const uint8_t *data, const uint64_t *nar_offsets, size_t n_nars, uint64_t min_size,
+                   uint64_t avg_size, uint64_t max_size, int algo, cg_desc *out, size_t out_cap,
+                   uint64_t *nar_first);
+
+/* Device-resident batch: `d_data` and `d_out` are device pointers on the current
+ * HIP device, `nar_offsets`/`nar_first` are host arrays, `stream` is a hipStream_t
+ * (NULL = the null stream).  Returns after the descriptors are in HBM (the call
+ * synchronises `stream` once to learn the count). */
+int cg_chunk_batch_device(const uint8_t *d_data, const uint64_t *nar_offsets, size_t n_nars,
+                          uint64_t min_size, uint64_t avg_size, uint64_t max_size, int algo,
+                          cg_desc *d_out, size_t out_cap, uint64_t *nar_first, void *stream);
+
+/* PushChunker (src/chunking.rs:753-829) over drain_finalized_chunks (:541-673).
+ * push/finish write the chunks that became final; `out_cap` must be at least
+ * cg_push_out_capacity(h, len).  push after finish -> CG_E_INVALID_OPTIONS
+ * ("push called after finish"). */
+typedef struct cg_push cg_push;
+cg_push *cg_push_new(uint64_t min_size, uint64_t avg_size, uint64_t max_size, int algo, int *status);
+int cg_push_push(cg_push *h, const uint8_t *data, uint64_t len, cg_desc *out, size_t out_cap, size_t *n_out);
+int cg_push_finish(cg_push *h, cg_desc *out, size_t out_cap, size_t *n_out);
+uint64_t cg_push_bytes_consumed(const cg_push *h); /* PushChunker::bytes_consumed */
+size_t cg_push_out_capacity(const cg_push *h, uint64_t next_len);
+void cg_push_free(cg_push *h);
+
+/* Digest-only entry (sha256_hash_raw src/hashing.rs:36-44 / blake3::hash) over n
+ * device-resident spans; d_digests receives n*32 bytes. */
+int cg_hash_spans_device(const uint8_t *d_data, const uint64_t *d_offsets, const uint64_t *d_lengths, size_t n,
+                         int algo, uint8_t *d_digests, void *stream);
+
+/* Host convenience over the same kernels: digest of one host buffer (sha256_hash_raw /
+ * blake3::hash, src/hashing.rs:36-53) into out[32].  len <= 16 MiB for BLAKE3. */
+int cg_hash(const uint8_t *data, uint64_t len, int algo, uint8_t out[32]);
+
+/* FastCDC v2020 GEAR table plumbing.  The compiled-in table comes from
+ * tables/fastcdc_v2020_gear.txt; cg_set_gear_table replaces it process-wide
+ * (all devices) for later calls. */
+int cg_set_gear_table(const uint64_t gear[256]);
+void cg_get_gear_table(uint64_t gear[256]);
+int cg_gear_is_placeholder(void);
+
+/* Per-stage device times (ms) of the last batch call on this thread, measured with
+ * HIP events on the stream the kernels ran on.  Order: scan, compact, walk,
+ * assemble, digest.  Returns the number of stages written; 0 if profiling is off. */
+void cg_set_profiling(int on);
+size_t cg_last_stage_times(double *ms, size_t n);
+
+/* Synthetic NAR writer: nix-archive-1 framing around an
+ * xorshift64 payload (crates/node/src/lib.rs:192-203) with seed
+ * 0x9E3779B97F4A7C15 ^ (first_index + i), or zeros.  NAR i is nar_sizes[i] bytes
+ * (a multiple of 8, >= 120) written back to back into `out`. */
+void cg_synth_nars(uint8_t *out, const uint64_t *nar_sizes, size_t n, int zeros, uint64_t first_index);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,292 @@
+"""GPU parity: the gfx950 engine (through the C ABI) vs the CPU oracle.
+
+Bit-exact on every (offset, length) and every digest.  Cases follow the
+reference's own tests (src/chunking.rs:1168-1443, tests/streaming_chunking.rs,
+tests/proptest_suite.rs, fuzz/fuzz_targets/chunking.rs) plus edge cases of the
+GPU design (segment/halo seams, dense candidate segments, unaligned chunk
+starts, empty and ragged NARs, digest padding boundaries).
+"""
+import hashlib
+import io
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SHA, B3 = 1, 0
+D = (256 * 1024, 1024 * 1024, 4 * 1024 * 1024)
+S = (64 * 1024, 256 * 1024, 1024 * 1024)
+FIX = (1024, 6000, 16 * 1024)
+TINY = (64, 256, 1024)
+ODD = (65, 300, 1025)
+ODD2 = (4097, 10000, 70001)
+
+
+@pytest.fixture(scope="module")
+def ca(gpu):
+    import chunker_amd
+
+    return chunker_amd
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import oracle
+
+    return oracle
+
+
+def rand_bytes(n, seed):
+    return np.random.default_rng(seed).integers(0, 256, n, dtype=np.uint8)
+
+
+def fixture_bytes(n):
+    i = np.arange(n, dtype=np.int64)
+    return ((i * 31 + i // 7) % 251).astype(np.uint8)
+
+
+def assert_same(got, ref, ctx=""):
+    assert len(got) == len(ref), f"{ctx}: {len(got)} chunks vs oracle {len(ref)}"
+    assert np.array_equal(got["offset"], ref["offset"]), ctx
+    assert np.array_equal(got["length"], ref["length"]), ctx
+    bad = np.nonzero(~np.all(got["hash"] == ref["hash"], axis=1))[0]
+    assert len(bad) == 0, f"{ctx}: digest mismatch at chunks {bad[:8]}"
+
+
+CASES = [
+    ("empty", lambda: np.zeros(0, np.uint8), D),
+    ("one", lambda: rand_bytes(1, 1), D),
+    ("small_data", lambda: np.frombuffer(b"small data", np.uint8), D),
+    ("63", lambda: rand_bytes(63, 2), TINY),
+    ("min-1", lambda: rand_bytes(FIX[0] - 1, 3), FIX),
+    ("min", lambda: rand_bytes(FIX[0], 4), FIX),
+    ("min+1", lambda: rand_bytes(FIX[0] + 1, 5), FIX),
+    ("fixture", lambda: fixture_bytes(64 * 1024 + 123), FIX),
+    ("rand_fix_200k", lambda: rand_bytes(200_000, 6), FIX),
+    ("rand_tiny_100k", lambda: rand_bytes(100_003, 7), TINY),
+    ("rand_odd_300k", lambda: rand_bytes(300_001, 8), ODD),
+    ("rand_odd2_3m", lambda: rand_bytes(3_000_017, 9), ODD2),
+    ("zeros_10m", lambda: np.zeros(10 * 1024 * 1024, np.uint8), D),
+    ("ff_1m", lambda: np.full(1 << 20, 0xFF, np.uint8), FIX),
+    ("rand_D_10m", lambda: rand_bytes(10 * 1024 * 1024, 10), D),
+    ("rand_S_5m", lambda: rand_bytes(5 * 1024 * 1024 + 77, 11), S),
+    ("lowentropy_tiny", lambda: (rand_bytes(400_000, 12) & 3).astype(np.uint8), TINY),
+    ("periodic_fix_S", lambda: fixture_bytes(3 * 1024 * 1024), S),
+    ("repeat_phrase", lambda: np.frombuffer(b"descriptor parity test payload" * 8192, np.uint8), (1024, 4096, 8192)),
+    ("max_sizes", lambda: rand_bytes(40 * 1024 * 1024 + 5, 13), (1 << 20, 4 << 20, 16 << 20)),
+    ("all_min_sizes", lambda: rand_bytes(50_000, 14), (64, 256, 1024)),
+]
+
+
+@pytest.mark.parametrize("algo", [SHA, B3], ids=["sha256", "blake3"])
+@pytest.mark.parametrize("name,make,params", CASES, ids=[c[0] for c in CASES])
+def test_descriptors_match_oracle(ca, O, name, make, params, algo):
+    data = make()
+    got = ca.chunk_descriptors_array(data, *params, hash=algo)
+    ref = O.chunk_descriptors(data, *params, algo=algo)
+    assert_same(got, ref, name)
+    # invariants of the reference tests: contiguity, full coverage, sizes
+    if len(got):
+        ends = got["offset"] + got["length"]
+        assert got["offset"][0] == 0 and ends[-1] == len(data)
+        assert np.array_equal(got["offset"][1:], ends[:-1])
+        assert np.all(got["length"][:-1] >= 2 * (params[0] // 2)) and np.all(got["length"] <= params[2])
+    else:
+        assert len(data) == 0
+
+
+@pytest.mark.parametrize("algo", [SHA, B3], ids=["sha256", "blake3"])
+def test_batch_ragged_unaligned(ca, O, algo):
+    rng = np.random.default_rng(99)
+    lens = [0, 1, 7, 1023, 1024, 1025, 65_535, 100_001, 0, 333_333, 1_048_577, 2_000_003, 5, 4_194_305]
+    nars = [rng.integers(0, 256, n, dtype=np.uint8) for n in lens]
+    params = (4096, 16384, 65536)
+    got = ca.chunk_batch(nars, *params, hash=algo)
+    for i, nar in enumerate(nars):
+        assert_same(got[i], O.chunk_descriptors(nar, *params, algo=algo), f"nar{i} len={lens[i]}")
+
+
+@pytest.mark.parametrize("params", [D, S], ids=["D", "S"])
+def test_batch_synthetic_nars(ca, O, params):
+    from chunker_amd.nar import synth_nars
+
+    sizes = [4 * 1024 * 1024] * 24 + [1024 * 1024 + 8 * k for k in range(8)]
+    data, offs = synth_nars(sizes)
+    nars = [data[offs[i]:offs[i + 1]] for i in range(len(sizes))]
+    got = ca.chunk_batch(nars, *params)
+    for i, nar in enumerate(nars):
+        assert_same(got[i], O.chunk_descriptors(nar, *params, algo=SHA), f"nar{i}")
+
+
+def test_device_batch_matches_host(ca, O):
+    import torch
+
+    from chunker_amd.nar import synth_nars
+
+    sizes = [2 * 1024 * 1024 + 8 * k for k in range(16)]
+    data, offs = synth_nars(sizes, first_index=7)
+    d = torch.from_numpy(data).cuda()
+    cap = ca.chunking.batch_capacity(offs, D[0])
+    out = torch.zeros(cap * 48, dtype=torch.uint8, device="cuda")
+    first = ca.chunk_batch_device(d.data_ptr(), offs, out.data_ptr(), cap, *D,
+                                  stream=torch.cuda.current_stream().cuda_stream)
+    descs = out.cpu().numpy().view(ca.DESC_DTYPE)
+    for i in range(len(sizes)):
+        ref = O.chunk_descriptors(data[offs[i]:offs[i + 1]], *D, algo=SHA)
+        assert_same(descs[int(first[i]):int(first[i + 1])], ref, f"nar{i}")
+
+
+# --- streaming: tests/streaming_chunking.rs -----------------------------------
+@pytest.mark.parametrize("slice_size", [512, 8_192, 65_536, 400_000, 1_500_000])
+def test_push_matches_in_memory_across_slice_sizes(ca, slice_size):
+    data = rand_bytes(1_500_000, 1234).tobytes()
+    params = (8_192, 32_768, 131_072)
+    expected = ca.chunk_data_with_hash(data, *params, hash=ca.HashAlgorithm.Blake3)
+    pc = ca.PushChunker(*params, hash=ca.HashAlgorithm.Blake3)
+    got, re = [], bytearray()
+    for k in range(0, len(data), slice_size):
+        for c in pc.push(data[k:k + slice_size]):
+            re += c.payload
+            got.append(c)
+    for c in pc.finish():
+        re += c.payload
+        got.append(c)
+    assert got == expected
+    assert bytes(re) == data
+    for c in got:
+        assert len(c.payload) == c.length <= 131_072
+        assert c.payload == data[c.offset:c.offset + c.length]
+
+
+def test_push_nonuniform_with_empties(ca, O):
+    data = rand_bytes(800_000, 99).tobytes()
+    params = (8_192, 32_768, 131_072)
+    expected = ca.chunk_data_with_hash(data, *params)
+    pc = ca.PushChunker(*params)
+    steps = [1, 7, 33, 1, 60_000, 3, 131_073, 500, 250_000, 9]
+    got, pos, i = [], 0, 0
+    while pos < len(data):
+        assert pc.push(b"") == []
+        step = min(steps[i % len(steps)], len(data) - pos)
+        i += 1
+        got += pc.push(data[pos:pos + step])
+        pos += step
+    got += pc.finish()
+    assert got == expected
+    # and the oracle's PushChunker restatement agrees chunk for chunk
+    op = O.Push(*params, algo=SHA)
+    ref = []
+    pos, i = 0, 0
+    while pos < len(data):
+        step = min(steps[i % len(steps)], len(data) - pos)
+        i += 1
+        ref += list(op.push(data[pos:pos + step]))
+        pos += step
+    ref += list(op.finish())
+    assert [(int(r["offset"]), int(r["length"]), bytes(r["hash"])) for r in ref] == \
+        [(c.offset, c.length, c.hash) for c in got]
+
+
+def test_push_empty_and_after_finish(ca):
+    pc = ca.PushChunker()
+    assert pc.push(b"") == [] and pc.finish() == []
+    pc = ca.PushChunker()
+    pc.push(b"hello streaming world")
+    pc.finish()
+    with pytest.raises(ca.ChunkingError):
+        pc.push(b"more")
+
+
+@pytest.mark.parametrize("params,seed,n", [((None, None, None), 42, 2_500_000),
+                                           ((8_192, 32_768, 131_072), 84, 3_000_000)])
+def test_stream_matches_in_memory(ca, params, seed, n):
+    data = rand_bytes(n, seed).tobytes()
+    stream = ca.chunk_stream_with_hash(io.BufferedReader(io.BytesIO(data)), *params, hash=ca.HashAlgorithm.Blake3)
+    eager = ca.chunk_data_with_hash(data, *params, hash=ca.HashAlgorithm.Blake3)
+    assert stream == eager
+    total = 0
+    for c in stream:  # fuzz_targets/chunking.rs invariants
+        assert c.offset == total and c.payload == data[c.offset:c.offset + c.length]
+        total += c.length
+    assert total == len(data)
+
+
+def test_stream_small_read_cap(ca, monkeypatch):
+    monkeypatch.setenv("CHUNKER_READ_SLICE_CAP_BYTES", "4096")
+    data = (b"streaming chunker parity test" * 2048)
+    assert ca.chunk_stream(io.BytesIO(data)) == ca.chunk_data(data)
+    data = bytes([42]) * (3 * 1024 * 1024 + 321)
+    chunks = ca.chunk_stream(io.BytesIO(data), 16 * 1024, 32 * 1024, 64 * 1024)
+    assert sum(c.length for c in chunks) == len(data) and len(chunks) > 1
+
+
+# --- reference unit tests, src/chunking.rs:1168-1443 --------------------------
+def test_reference_unit_cases(ca):
+    chunks = ca.chunk_data(bytes(1024 * 1024))
+    assert chunks and [c.offset for c in chunks] == list(np.cumsum([0] + [c.length for c in chunks[:-1]]))
+    assert sum(c.length for c in chunks) == 1024 * 1024
+    small = ca.chunk_data(b"small data")
+    assert len(small) == 1 and small[0].offset == 0 and small[0].length == 10
+    sha = ca.chunk_data_with_hash(bytes([7]) * 4096, hash=ca.HashAlgorithm.Sha256)
+    b3 = ca.chunk_data_with_hash(bytes([7]) * 4096, hash=ca.HashAlgorithm.Blake3)
+    assert len(sha) == len(b3) and sha[0].hash != b3[0].hash
+    data = b"descriptor parity test payload" * 8192
+    d = ca.chunk_descriptors(data, 1024, 4096, 8192)
+    m = ca.chunk_data(data, 1024, 4096, 8192)
+    assert [(x.hash, x.offset, x.length) for x in d] == [(x.hash, x.offset, x.length) for x in m]
+    assert ca.chunk_data(bytes(100), 1024, 4096, 4 * 1024 * 1024)
+    data = b"stream hash parity test payload" * 1024
+    assert ca.chunk_data_with_hash(data, 1024, 4096, 8192, hash=ca.HashAlgorithm.Blake3) == \
+        ca.chunk_stream_with_hash(io.BytesIO(data), 1024, 4096, 8192, hash=ca.HashAlgorithm.Blake3)
+    # zeros: every chunk is max-size (the reference's published-bench regime)
+    z = ca.chunk_descriptors(bytes(10 * 1024 * 1024))
+    assert [c.length for c in z] == [4 << 20, 4 << 20, 2 << 20]
+
+
+# --- digests ------------------------------------------------------------------
+def test_digest_kats(ca):
+    from chunker_amd.hashing import blake3_hash, sha256_hash
+
+    assert sha256_hash(b"hello world") == "b94d27b9934d3e08a52e52d7da7dabfac484efe37a5380ee9088f7ace2efcde9"
+    assert blake3_hash(b"hello world") == "d74981efa70a0c880b8d8c1985d075dbcbf679b99a5f9914e5aaf96b831a9e24"
+    assert blake3_hash(b"") == "af1349b9f5f9a1a6a0404dea36dcc9499bcb25c9adc112b7cc9a93cae41f3262"
+
+
+def test_digest_spans_all_lengths(ca, O):
+    import torch
+
+    rng = np.random.default_rng(5)
+    data = rng.integers(0, 256, 3 << 20, dtype=np.uint8)
+    lens = list(range(0, 300)) + [511, 512, 513, 1023, 1024, 1025, 2047, 2048, 2049, 4095, 4096, 4097, 65535,
+                                  65536, 65537, 65536 * 3 + 1, 1 << 20, (1 << 20) + 3, 3 << 20]
+    offs = [int(rng.integers(0, len(data) - n + 1)) for n in lens]
+    d = torch.from_numpy(data).cuda()
+    o = torch.tensor(offs, dtype=torch.int64).cuda()
+    ln = torch.tensor(lens, dtype=torch.int64).cuda()
+    for algo in (SHA, B3):
+        dig = torch.zeros(len(lens) * 32, dtype=torch.uint8, device="cuda")
+        st = ca.lib.cg_hash_spans_device(d.data_ptr(), o.data_ptr(), ln.data_ptr(), len(lens), algo, dig.data_ptr(),
+                                         None)
+        assert st == 0
+        dig = dig.cpu().numpy().reshape(-1, 32)
+        for k, (a, n) in enumerate(zip(offs, lens)):
+            span = data[a:a + n].tobytes()
+            want = hashlib.sha256(span).digest() if algo == SHA else O.blake3(span)
+            assert bytes(dig[k]) == want, (algo, n, a)
+
+
+@pytest.mark.slow
+def test_full_size_config2_batch(ca, O):
+    """BASELINE config 2 at full size (256 x 4 MiB NARs, defaults, SHA-256): every
+    boundary and digest equal to the oracle."""
+    from chunker_amd.nar import synth_nars
+
+    sizes = [4 * 1024 * 1024] * 256
+    data, offs = synth_nars(sizes)
+    nars = [data[offs[i]:offs[i + 1]] for i in range(len(sizes))]
+    got = ca.chunk_batch(nars, *D)
+    nt = min(16, os.cpu_count() or 1)
+    for i, nar in enumerate(nars):
+        assert_same(got[i], O.chunk_descriptors(nar, *D, algo=SHA, nthreads=nt), f"nar{i}")
