@@ -83,19 +83,13 @@ def main():
     stream = torch.cuda.current_stream()
     sptr = stream.cuda_stream
 
+    from chunker_amd.dist import gather_descriptors
+
     def step():
         first = ca.chunk_batch_device(d_data.data_ptr(), offs, d_out.data_ptr(), cap, *params, hash=algo,
                                       stream=sptr)
-        n = int(first[-1])
-        if world > 1:  # gather descriptors to rank 0 over RCCL (padded all-gather of counts + gather)
-            cnt = torch.tensor([n], dtype=torch.int64, device="cuda")
-            cnts = [torch.zeros_like(cnt) for _ in range(world)]
-            dist.all_gather(cnts, cnt)
-            mx = int(max(int(c.item()) for c in cnts))
-            buf = d_out[: mx * 48] if n == mx else torch.cat(
-                [d_out[: n * 48], torch.zeros((mx - n) * 48, dtype=torch.uint8, device="cuda")])
-            gl = [torch.empty(mx * 48, dtype=torch.uint8, device="cuda") for _ in range(world)] if rank == 0 else None
-            dist.gather(buf, gl, dst=0)
+        if world > 1:  # descriptors to rank 0 over RCCL (the path's only exchange)
+            gather_descriptors(d_out, int(first[-1]))
         return first
 
     for _ in range(args.warmup):

@@ -32,7 +32,7 @@ EXPORTS = (
     "cg_chunk_batch", "cg_chunk_batch_device", "cg_push_new", "cg_push_push", "cg_push_finish",
     "cg_push_bytes_consumed", "cg_push_out_capacity", "cg_push_free", "cg_hash_spans_device",
     "cg_set_gear_table", "cg_get_gear_table", "cg_gear_is_placeholder", "cg_set_profiling",
-    "cg_last_stage_times", "cg_synth_nars",
+    "cg_last_stage_times", "cg_synth_nars", "cg_hash",
 )
 
 
@@ -77,6 +77,8 @@ def _load() -> ctypes.CDLL:
     L.cg_push_free.restype = None
     L.cg_hash_spans_device.argtypes = [p, p, p, sz, i, p, p]
     L.cg_hash_spans_device.restype = i
+    L.cg_hash.argtypes = [p, u64, i, p]
+    L.cg_hash.restype = i
     L.cg_set_gear_table.argtypes = [p]
     L.cg_set_gear_table.restype = i
     L.cg_get_gear_table.argtypes = [p]

@@ -21,20 +21,31 @@ static constexpr uint32_t SHA_K[64] = {
     0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
 
 __device__ __forceinline__ uint32_t rotr32(uint32_t x, uint32_t n) { return __builtin_amdgcn_alignbit(x, x, n); }
+// gfx950 v_bitop3_b32: one instruction for any 3-input bitwise function
+// (truth-table byte: S0 = 0xF0, S1 = 0xCC, S2 = 0xAA).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t ch(uint32_t e, uint32_t f, uint32_t g) {
+    return __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);
+}
+__device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+}
+__device__ __forceinline__ uint32_t add3(uint32_t a, uint32_t b, uint32_t c) { return a + b + c; }
 
-#define SHA_S0(a) (rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22))
-#define SHA_S1(e) (rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25))
-#define SHA_s0(x) (rotr32(x, 7) ^ rotr32(x, 18) ^ ((x) >> 3))
-#define SHA_s1(x) (rotr32(x, 17) ^ rotr32(x, 19) ^ ((x) >> 10))
-#define SHA_CH(e, f, g) ((g) ^ ((e) & ((f) ^ (g))))
-#define SHA_MAJ(a, b, c) (((a) & (b)) | ((c) & ((a) | (b))))
+#define SHA_S0(a) xor3(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22))
+#define SHA_S1(e) xor3(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25))
+#define SHA_s0(x) xor3(rotr32(x, 7), rotr32(x, 18), (x) >> 3)
+#define SHA_s1(x) xor3(rotr32(x, 17), rotr32(x, 19), (x) >> 10)
 
-#define SHA_RND(a, b, c, d, e, f, g, h, i)                                  \
-    {                                                                       \
-        const uint32_t t1 = h + SHA_S1(e) + SHA_CH(e, f, g) + SHA_K[i] + w[(i) & 15]; \
-        const uint32_t t2 = SHA_S0(a) + SHA_MAJ(a, b, c);                   \
-        d += t1;                                                            \
-        h = t1 + t2;                                                        \
+// One round: 14 VALU (4 Sigma1, 1 Ch, 4 Sigma0, 1 Maj, 4 adds); renaming by macro
+// argument rotation, so no register moves.
+#define SHA_RND(a, b, c, d, e, f, g, h, i)                          \
+    {                                                               \
+        const uint32_t t1 = add3(add3(h, w[(i) & 15], SHA_K[i]), SHA_S1(e), ch(e, f, g)); \
+        d += t1;                                                    \
+        h = add3(t1, SHA_S0(a), maj(a, b, c));                      \
     }
 
 __device__ __forceinline__ void sha256_compress(uint32_t st[8], uint32_t w[16]) {
@@ -45,7 +56,7 @@ __device__ __forceinline__ void sha256_compress(uint32_t st[8], uint32_t w[16]) 
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int t = i + j;
-                w[t & 15] += SHA_s1(w[(t - 2) & 15]) + w[(t - 7) & 15] + SHA_s0(w[(t - 15) & 15]);
+                w[t & 15] = add3(w[t & 15], SHA_s0(w[(t - 15) & 15]), w[(t - 7) & 15]) + SHA_s1(w[(t - 2) & 15]);
             }
         }
         SHA_RND(a, b, c, d, e, f, g, h, i + 0);
@@ -78,14 +89,23 @@ __global__ __launch_bounds__(64) void k_sha256(const uint8_t *__restrict__ data,
 
     uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
     const uint64_t nb = len >> 6;
+    // software pipeline: block k+1's 17 dwords are in flight while block k compresses
+    uint32_t nx[17];
+    if (nb) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) nx[i] = base[i];
+        nx[16] = shift ? base[16] : 0u;
+    }
     for (uint64_t blk = 0; blk < nb; ++blk) {
-        const uint32_t *q = base + 16 * blk;
-        uint32_t dw[17], w[16];
+        uint32_t w[16];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) dw[i] = q[i];
-        dw[16] = shift ? q[16] : 0u;
+        for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_perm(nx[i + 1], nx[i], sel);
+        if (blk + 1 < nb) {
+            const uint32_t *q = base + 16 * (blk + 1);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_perm(dw[i + 1], dw[i], sel);
+            for (int i = 0; i < 16; ++i) nx[i] = q[i];
+            nx[16] = shift ? q[16] : 0u;
+        }
         sha256_compress(st, w);
     }
     // final block(s): tail bytes, 0x80, zeros, 64-bit big-endian bit length

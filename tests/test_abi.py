@@ -1,0 +1,137 @@
+"""C-ABI and host-mirror checks that need no GPU: the library loads, exports every
+symbol include/chunker_gpu.h declares, validates options with the reference's
+messages, and the host-side types behave like the reference's."""
+import ctypes
+import re
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+@pytest.fixture(scope="module")
+def ca():
+    import chunker_amd
+
+    return chunker_amd
+
+
+def declared_symbols():
+    text = (ROOT / "include" / "chunker_gpu.h").read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(cg_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_library_exports_every_declared_symbol(ca):
+    from chunker_amd import _lib
+
+    syms = declared_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(ca.lib, s), f"missing export {s}"
+    assert set(syms) == set(_lib.EXPORTS)
+    assert ca.lib.cg_abi_version() == 1
+
+
+def test_desc_layout(ca):
+    assert ca.DESC_DTYPE.itemsize == 48
+    assert ca.DESC_DTYPE.fields["hash"][1] == 16
+
+
+def test_capacity(ca):
+    assert ca.lib.cg_capacity(0, 1024) == 0
+    assert ca.lib.cg_capacity(1, 1024) == 1
+    assert ca.lib.cg_capacity(10 << 20, 256 << 10) == 41
+    assert ca.lib.cg_capacity(1000, 65) == 1000 // 64 + 1
+
+
+@pytest.mark.parametrize("mn,avg,mx,field", [((1 << 20) + 1, 1024, 4096, "min_size"),
+                                             (64, (4 << 20) + 1, 16 << 20, "avg_size"),
+                                             (64, 1024, (16 << 20) + 1, "max_size")])
+def test_abi_validate_names_field(ca, mn, avg, mx, field):
+    """src/chunking.rs:1378-1399."""
+    msg = ctypes.create_string_buffer(256)
+    assert ca.lib.cg_validate(mn, avg, mx, msg, 256) == 4
+    assert field in msg.value.decode()
+    with pytest.raises(ca.InvalidOptionsError) as ei:
+        ca.ChunkingOptions.resolve(mn, avg, mx)
+    assert field in str(ei.value) and str(ei.value).startswith("invalid_chunking_options: ")
+
+
+def test_options_resolve(ca):
+    o = ca.ChunkingOptions.resolve()
+    assert (o.min_size, o.avg_size, o.max_size) == (256 * 1024, 1024 * 1024, 4 * 1024 * 1024)
+    for t in [(64, 256, 1024), (64, 1024, 4096), (256 << 10, 1 << 20, 4 << 20), (1 << 20, 4 << 20, 16 << 20)]:
+        o = ca.ChunkingOptions.resolve(*t)
+        assert (o.min_size, o.avg_size, o.max_size) == t
+    with pytest.raises(ca.InvalidOptionsError, match="min_size.*64"):
+        ca.ChunkingOptions.resolve(32, 64, 128)
+    with pytest.raises(ca.InvalidOptionsError):
+        ca.ChunkingOptions.resolve(64, 64, 64)  # tests/streaming_chunking.rs:167-171
+    with pytest.raises(ca.InvalidOptionsError):
+        ca.ChunkingOptions.resolve(64, 1024, 64 * 1024 * 1024)
+    with pytest.raises(ca.InvalidOptionsError, match="min_size must be <= avg_size"):
+        ca.ChunkingOptions.resolve(4096, 1024, 8192)
+    with pytest.raises(ca.InvalidOptionsError, match="avg_size must be <= max_size"):
+        ca.ChunkingOptions.resolve(64, 8192, 4096)
+    with pytest.raises(ca.InvalidOptionsError, match="got 0"):
+        ca.ChunkingOptions.resolve(0, 1024, 4096)
+
+
+def test_metadata_equality_ignores_payload(ca):
+    """src/chunking.rs:1330-1358."""
+    a = ca.ChunkMetadata(bytes([1]) * 32, 10, 5, b"payload-a")
+    b = ca.ChunkMetadata(bytes([1]) * 32, 10, 5, b"payload-b")
+    assert a == b and hash(a) == hash(b)
+    assert ca.HashAlgorithm.Blake3 == 0 and ca.HashAlgorithm.Sha256 == 1
+
+
+def test_error_display_strings(ca):
+    assert str(ca.BoundsError(3, 1, 5)) == "bounds_check_failed: offset 1 + length 5 exceeds data length 3"
+    assert str(ca.ZeroLengthChunkError()) == "zero_length_chunk: FastCDC returned a chunk with length 0"
+    assert str(ca.BufferLimitExceededError(9, 8)) == "buffer_limit_exceeded: attempted 9 bytes, limit 8 bytes"
+    assert str(ca.IoError("x")) == "io_error: x"
+
+
+def test_no_cpu_fallback_without_gpu(ca):
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(ca.DeviceUnavailableError):
+        ca.chunk_descriptors(b"hello world")
+    with pytest.raises(ca.DeviceUnavailableError):
+        ca.PushChunker().push(bytes(300_000))
+
+
+def test_gear_table_plumbing(ca):
+    from oracle import oracle as O
+
+    g = np.zeros(256, np.uint64)
+    ca.lib.cg_get_gear_table(g.ctypes.data)
+    assert np.array_equal(g, O.GEAR)
+    assert bool(ca.lib.cg_gear_is_placeholder()) == O.GEAR_IS_PLACEHOLDER
+    alt = (O.GEAR ^ np.uint64(1)).astype(np.uint64)
+    ca.lib.cg_set_gear_table(alt.ctypes.data)
+    ca.lib.cg_get_gear_table(g.ctypes.data)
+    assert np.array_equal(g, alt) and ca.lib.cg_gear_is_placeholder() == 0
+    ca.lib.cg_set_gear_table(O.GEAR.ctypes.data)
+    assert bool(ca.lib.cg_gear_is_placeholder()) == O.GEAR_IS_PLACEHOLDER
+
+
+def test_synthetic_nar_layout(ca):
+    from chunker_amd.nar import SEED_BASE, synth_nars, xorshift_bytes_py
+
+    data, offs = synth_nars([4096, 1024 + 112, 120], first_index=5)
+    assert list(offs) == [0, 4096, 4096 + 1136, 4096 + 1136 + 120]
+    for i in range(3):
+        nar = data[offs[i]:offs[i + 1]].tobytes()
+        assert nar[:8] == (13).to_bytes(8, "little") and nar[8:21] == b"nix-archive-1"
+        L = len(nar) - 112
+        assert nar[88:96] == L.to_bytes(8, "little")
+        assert nar[96:96 + L] == xorshift_bytes_py(SEED_BASE ^ (5 + i), L)
+        assert nar[-16:] == (1).to_bytes(8, "little") + b")" + bytes(7)
+    z, _ = synth_nars([4096], zeros=True)
+    assert not z[96:96 + 4096 - 112].any()
