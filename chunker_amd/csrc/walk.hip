@@ -24,109 +24,230 @@ __device__ __forceinline__ uint64_t lower_bound_u64(const uint64_t *__restrict__
     return lo;
 }
 
+#define NONE (~0ull)
+
+// Re-read of a value this wave stored earlier in the launch: an agent-scope load
+// is served from L2, never from a possibly stale L1 line.
+__device__ __forceinline__ uint64_t ld_l2(const uint64_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ uint64_t rd_u64(uint64_t v, int lane) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, lane);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), lane);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Chunk geometry of cut_gear [ext] for a chunk starting at c with rem bytes left
+// (SURVEY.md Appendix A.2): hash restarts at s; [s, cs) is tested with mask_s,
+// [cs, ce) with mask_l; no hit -> cut at c + R.
+struct Geo {
+    uint64_t R, s, cs, ce;
+};
+__device__ __forceinline__ Geo geometry(uint64_t c, uint64_t rem, const CdcParams &P) {
+    uint64_t R = rem, center = P.avg;
+    if (R > P.max)
+        R = P.max;
+    else if (R < center)
+        center = R;
+    Geo g;
+    g.R = R;
+    g.s = c + 2 * (P.min / 2);
+    g.cs = c + 2 * (center / 2);
+    g.ce = c + 2 * (R / 2);
+    return g;
+}
+
+// Exact restarted hash over the first 47 tested positions [s, min(s+47, ce)),
+// lane-parallel: lane j loads byte s+j and an inclusive shift-add scan
+// (A_j = sum_i g_i << (j-i)) gives the crate's hash at s+j.  First hit or NONE.
+__device__ __forceinline__ uint64_t warmup_exact(const uint8_t *__restrict__ data, const uint64_t *gear, const Geo &g,
+                                                 const CdcParams &P, uint32_t lane) {
+    const uint64_t wend = g.s + 47 < g.ce ? g.s + 47 : g.ce;
+    if (wend <= g.s) return NONE;
+    const uint64_t p = g.s + lane;
+    const bool in = p < wend;
+    uint64_t a = in ? gear[data[p]] : 0ull;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint64_t t = __shfl_up(a, d, 64);
+        if (lane >= d) a += t << d;
+    }
+    const uint64_t m = p < g.cs ? P.mask_s : P.mask_l;
+    const uint64_t hits = __ballot(in && (a & m) == 0);
+    return hits ? g.s + (uint64_t)__builtin_ctzll(hits) : NONE;
+}
+
+// Windowed (48-byte) hash verdict for positions [lo, hi) of a dense segment,
+// 64 positions per pass; first hit or NONE.  Only reached for inputs with more
+// candidates than the per-segment slots.
+__device__ uint64_t dense_rescan(const uint8_t *__restrict__ data, const uint64_t *gear, uint64_t lo, uint64_t hi,
+                                 uint64_t cs, const CdcParams &P, uint32_t lane) {
+    for (uint64_t b = lo; b < hi; b += 64) {
+        const uint64_t p = b + lane;
+        bool hit = false;
+        if (p < hi) {
+            uint64_t h = 0;
+            for (uint64_t q = p - 47; q <= p; ++q) h = (h << 1) + gear[data[q]];
+            hit = (h & (p < cs ? P.mask_s : P.mask_l)) == 0;
+        }
+        const uint64_t bal = __ballot(hit);
+        if (bal) return b + (uint64_t)__builtin_ctzll(bal);
+    }
+    return NONE;
+}
+
+// Window of 64 sorted candidate entries held one per lane.
+struct EntryWin {
+    uint64_t base;  // index of lane 0's entry
+    uint64_t e;     // this lane's entry (or ~0 past the end)
+};
+__device__ __forceinline__ void win_load(EntryWin &w, const uint64_t *__restrict__ entries, uint64_t n_entries,
+                                         uint32_t lane) {
+    const uint64_t i = w.base + lane;
+    w.e = i < n_entries ? entries[i] : ~0ull;
+}
+
+// First position in [q0, ce) whose verdict from the candidate list is a cut
+// (mask_s below cs, mask_l from cs), rescanning dense segments exactly.
+__device__ uint64_t list_search(EntryWin &w, const uint64_t *__restrict__ entries, uint64_t n_entries,
+                                const uint8_t *__restrict__ data, const uint64_t *gear, uint64_t q0, uint64_t cs,
+                                uint64_t ce, const CdcParams &P, uint32_t lane) {
+    for (;;) {
+        if (q0 >= ce) return NONE;
+        const uint64_t pos = w.e >> 2;
+        const uint32_t f = (uint32_t)(w.e & 3u);
+        const bool valid = w.e != ~0ull;
+        const uint64_t cover_end = f ? pos + 1 : pos + CG_SEG;
+        const bool relevant = valid && cover_end > q0;
+        const bool hit = relevant && pos < ce && (f ? (f & (pos < cs ? CG_FLAG_S : CG_FLAG_L)) != 0 : true);
+        const uint64_t hb = __ballot(hit);
+        if (hb) {
+            const int L = __builtin_ctzll(hb);
+            const uint64_t e = rd_u64(w.e, L);
+            const uint64_t epos = e >> 2;
+            if (e & 3u) return epos;
+            const uint64_t lo = epos > q0 ? epos : q0;
+            const uint64_t hi = epos + CG_SEG < ce ? epos + CG_SEG : ce;
+            const uint64_t r = dense_rescan(data, gear, lo, hi, cs, P, lane);
+            if (r != NONE) return r;
+            q0 = hi;  // marker exhausted; continue after it
+            continue;
+        }
+        // no hit in this window: advance only if every entry is below ce
+        const uint64_t last = rd_u64(w.e, 63);
+        if (last == ~0ull || (last >> 2) >= ce) return NONE;
+        w.base += 64;
+        win_load(w, entries, n_entries, lane);
+    }
+}
+
+// K2: one wave per NAR.  spec = 1: walk with the candidate list only, then verify
+// every chunk's 47-position warm-up in parallel (one lane per chunk) and re-walk
+// from the first chunk whose warm-up holds a cut (rare when mask_s has >= 14
+// bits; falls back to exact mode after 4 re-walks).  spec = 0: exact warm-up per
+// chunk.  Both produce the crate's cut sequence exactly.
 __global__ __launch_bounds__(64) void k_walk(const uint8_t *__restrict__ data, const uint64_t *__restrict__ gear_g,
                                              const uint64_t *__restrict__ entries,
                                              const uint64_t *__restrict__ eoff, uint64_t nseg,
                                              const uint64_t *__restrict__ nar_off,
                                              const uint64_t *__restrict__ cap_base, uint64_t n_nars, CdcParams P,
-                                             uint64_t *__restrict__ wchunk, uint32_t *__restrict__ nar_nchunks) {
+                                             uint64_t *__restrict__ wchunk, uint32_t *__restrict__ nar_nchunks,
+                                             int spec) {
     __shared__ uint64_t gear[256];
-    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) gear[i] = gear_g[i];
+    for (uint32_t i = threadIdx.x; i < 256; i += 64) gear[i] = gear_g[i];
     __syncthreads();
-
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_nars) return;
+    const uint64_t nar = blockIdx.x;
+    if (nar >= n_nars) return;
+    const uint32_t lane = threadIdx.x;
     const uint64_t n_entries = eoff[nseg];
-    uint64_t c = nar_off[i];
-    const uint64_t end = nar_off[i + 1];
-    uint64_t *out = wchunk + 2 * cap_base[i];
-    uint32_t k = 0;
-    uint64_t ptr = lower_bound_u64(entries, n_entries, ((c / CG_SEG) * CG_SEG) << 2);
-    const uint64_t s_off = 2 * (P.min / 2);
+    const uint64_t c0 = nar_off[nar], end = nar_off[nar + 1];
+    uint64_t *out = wchunk + 2 * cap_base[nar];
 
-    while (c < end) {
-        const uint64_t rem = end - c;
-        uint64_t len;
-        if (rem <= P.min) {
-            len = rem;
-        } else {
-            uint64_t R = rem, center = P.avg;
-            if (R > P.max)
-                R = P.max;
-            else if (R < center)
-                center = R;
-            const uint64_t s = c + s_off, cs = c + 2 * (center / 2), ce = c + 2 * (R / 2);
-            bool found = false;
-            uint64_t cut = 0;
-            // (1) exact restarted hash over the first 47 tested positions
-            const uint64_t wend = s + 47 < ce ? s + 47 : ce;
-            uint64_t h = 0;
-            for (uint64_t p = s; p < wend; ++p) {
-                h = (h << 1) + gear[data[p]];
-                const uint64_t m = p < cs ? P.mask_s : P.mask_l;
-                if ((h & m) == 0) {
-                    cut = p;
-                    found = true;
-                    break;
+    EntryWin w;
+    w.base = lower_bound_u64(entries, n_entries, ((c0 / CG_SEG) * CG_SEG) << 2);
+    win_load(w, entries, n_entries, lane);
+
+    uint64_t k = 0, c = c0;
+    uint32_t rewalks = 0;
+    bool exact = spec == 0;
+    for (;;) {
+        const uint64_t k_start = k;
+        const EntryWin w_start = w;
+        while (c < end) {
+            const uint64_t rem = end - c;
+            uint64_t len;
+            if (rem <= P.min) {
+                len = rem;
+            } else {
+                const Geo g = geometry(c, rem, P);
+                uint64_t cut = exact ? warmup_exact(data, gear, g, P, lane) : NONE;
+                if (cut == NONE) {
+                    const uint64_t q0 = g.s + 47 < g.ce ? g.s + 47 : g.ce;
+                    cut = list_search(w, entries, n_entries, data, gear, q0, g.cs, g.ce, P, lane);
                 }
+                len = cut == NONE ? g.R : cut - c;
             }
-            // (2) later positions from the candidate list (windowed hash == chunk hash there)
-            if (!found) {
-                const uint64_t q0 = wend;
-                while (ptr < n_entries) {  // drop entries wholly below q0 (monotone across chunks)
-                    const uint64_t e = entries[ptr];
-                    const uint64_t hi = (e & 3u) ? (e >> 2) + 1 : (e >> 2) + CG_SEG;
-                    if (hi <= q0)
-                        ++ptr;
-                    else
-                        break;
-                }
-                for (uint64_t sp = ptr; sp < n_entries; ++sp) {
-                    const uint64_t e = entries[sp];
-                    const uint64_t pos = e >> 2;
-                    const uint32_t f = (uint32_t)(e & 3u);
-                    if (pos >= ce) break;
-                    if (f) {
-                        if (f & (pos < cs ? CG_FLAG_S : CG_FLAG_L)) {
-                            cut = pos;
-                            found = true;
+            if (lane == 0) {
+                out[2 * k] = c;
+                out[2 * k + 1] = len;
+            }
+            ++k;
+            c += len;
+        }
+        if (exact) break;
+        // verify warm-ups of chunks [k_start, k): lane i takes chunk k_start + i + 64t
+        __syncthreads();  // out[] written by lane 0 is read by other lanes below
+        uint64_t bad = NONE, bad_cut = 0;
+        for (uint64_t b = k_start; b < k && bad == NONE; b += 64) {
+            const uint64_t j = b + lane;
+            uint64_t my_cut = NONE;
+            if (j < k) {
+                const uint64_t cj = ld_l2(out + 2 * j);
+                const uint64_t rem = end - cj;
+                if (rem > P.min) {
+                    const Geo g = geometry(cj, rem, P);
+                    const uint64_t wend = g.s + 47 < g.ce ? g.s + 47 : g.ce;
+                    uint64_t h = 0;
+                    for (uint64_t p = g.s; p < wend; ++p) {
+                        h = (h << 1) + gear[data[p]];
+                        if ((h & (p < g.cs ? P.mask_s : P.mask_l)) == 0) {
+                            my_cut = p;
                             break;
-                        }
-                    } else {  // dense segment: exact windowed rescan of [max(pos,q0), min(pos+SEG,ce))
-                        const uint64_t lo = pos > q0 ? pos : q0;
-                        const uint64_t hi = pos + CG_SEG < ce ? pos + CG_SEG : ce;
-                        if (lo < hi) {
-                            uint64_t hh = 0;
-                            for (uint64_t p = lo - CG_HALO; p < lo; ++p) hh = (hh << 1) + gear[data[p]];
-                            for (uint64_t p = lo; p < hi; ++p) {
-                                hh = (hh << 1) + gear[data[p]];
-                                if ((hh & (p < cs ? P.mask_s : P.mask_l)) == 0) {
-                                    cut = p;
-                                    found = true;
-                                    break;
-                                }
-                            }
-                            if (found) break;
                         }
                     }
                 }
             }
-            len = found ? cut - c : R;
+            const uint64_t bal = __ballot(my_cut != NONE);
+            if (bal) {
+                const int L = __builtin_ctzll(bal);
+                bad = b + (uint64_t)L;
+                bad_cut = rd_u64(my_cut, L);
+            }
         }
-        out[2 * k] = c;
-        out[2 * k + 1] = len;
-        ++k;
-        c += len;
+        if (bad == NONE) break;
+        // chunk `bad` really ends at bad_cut: fix it and re-walk from there
+        const uint64_t cb = rd_u64(lane == 0 ? ld_l2(out + 2 * bad) : 0ull, 0);
+        if (lane == 0) out[2 * bad + 1] = bad_cut - cb;
+        k = bad + 1;
+        c = bad_cut;
+        // restart the entry window at the segment holding c (entries are sorted)
+        w = w_start;
+        w.base = lower_bound_u64(entries, n_entries, ((c / CG_SEG) * CG_SEG) << 2);
+        win_load(w, entries, n_entries, lane);
+        if (++rewalks >= 4) exact = true;
+        __syncthreads();
     }
-    nar_nchunks[i] = k;
+    if (lane == 0) nar_nchunks[nar] = (uint32_t)k;
 }
 
 void launch_walk(const uint8_t *d_data, const uint64_t *d_gear, const uint64_t *d_entries, const uint64_t *d_eoff,
                  uint64_t nseg, const uint64_t *d_nar_off, const uint64_t *d_cap_base, uint64_t n_nars,
                  CdcParams p, uint64_t *d_wchunk, uint32_t *d_nar_nchunks, hipStream_t st) {
     if (n_nars == 0) return;
-    hipLaunchKernelGGL(k_walk, dim3((uint32_t)((n_nars + 63) / 64)), dim3(64), 0, st, d_data, d_gear, d_entries,
-                       d_eoff, nseg, d_nar_off, d_cap_base, n_nars, p, d_wchunk, d_nar_nchunks);
+    const int spec = __builtin_popcountll(p.mask_s) >= 14 ? 1 : 0;
+    hipLaunchKernelGGL(k_walk, dim3((uint32_t)n_nars), dim3(64), 0, st, d_data, d_gear, d_entries, d_eoff, nseg,
+                       d_nar_off, d_cap_base, n_nars, p, d_wchunk, d_nar_nchunks, spec);
 }
 
 // One wave per NAR: copy the walker's (abs offset, length) list into the caller's
