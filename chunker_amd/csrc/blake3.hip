@@ -129,17 +129,41 @@ __global__ void k_b3_count(const DescRaw *__restrict__ desc, const uint64_t *__r
     gcount[g] = g < total ? (uint32_t)b3_groups_of(desc[g].length) : 0u;
 }
 
-// One wave per 64-leaf group.
-__global__ __launch_bounds__(64) void k_b3_groups(const uint8_t *__restrict__ data, const uint64_t *__restrict__ abs,
-                                                  const DescRaw *__restrict__ desc,
-                                                  const uint64_t *__restrict__ total_p, uint64_t max_chunks,
-                                                  const uint64_t *__restrict__ group_base,
-                                                  uint8_t *__restrict__ hash_base, size_t stride,
-                                                  uint32_t *__restrict__ gcv) {
-    __shared__ uint32_t s_cv[64][9];
+// Fold the chaining values held one per lane (lanes 0..count-1) level by level,
+// the odd last node carried up (BLAKE3's left-complete tree); ROOT on the final
+// parent when `root`.  Pure register shuffles: no LDS, no barriers.
+__device__ __forceinline__ void b3_wave_fold(uint32_t cv[8], uint32_t count, bool root, uint32_t lane) {
+    while (count > 1) {
+        const uint32_t half = count >> 1;
+        uint32_t l[8], r[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            l[i] = __shfl(cv[i], (int)(2 * lane) & 63, 64);
+            r[i] = __shfl(cv[i], (int)(2 * lane + 1) & 63, 64);
+        }
+        if (lane < half) {
+            b3_parent(l, r, root && count == 2, cv);
+        } else if ((count & 1u) && lane == half) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) cv[i] = l[i];
+        }
+        count = (count + 1) >> 1;
+    }
+}
+
+#define B3_WAVES 4u
+
+// One wave per 64-leaf group (4 waves per workgroup for occupancy).
+__global__ __launch_bounds__(64 * B3_WAVES) void k_b3_groups(const uint8_t *__restrict__ data,
+                                                             const uint64_t *__restrict__ abs,
+                                                             const DescRaw *__restrict__ desc,
+                                                             const uint64_t *__restrict__ total_p, uint64_t max_chunks,
+                                                             const uint64_t *__restrict__ group_base,
+                                                             uint8_t *__restrict__ hash_base, size_t stride,
+                                                             uint32_t *__restrict__ gcv) {
     uint64_t total = *total_p;
     if (total > max_chunks) total = max_chunks;
-    const uint64_t G = blockIdx.x;
+    const uint64_t G = (uint64_t)blockIdx.x * B3_WAVES + (threadIdx.x >> 6);
     if (G >= group_base[total]) return;
     // chunk c with group_base[c] <= G < group_base[c+1]
     uint64_t lo = 0, hi = total;
@@ -155,58 +179,35 @@ __global__ __launch_bounds__(64) void k_b3_groups(const uint8_t *__restrict__ da
     const uint64_t gi = G - group_base[c];
     const uint64_t ngroups = group_base[c + 1] - group_base[c];
     const uint64_t leaves = len ? (len + 1023) / 1024 : 1;
-    const uint32_t lane = threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
     const uint32_t count0 = (uint32_t)((leaves - gi * 64) < 64 ? (leaves - gi * 64) : 64);
     const uint64_t leaf = gi * 64 + lane;
     const uint8_t *chunk = data + abs[c];
-    uint32_t cv[8];
+    uint32_t cv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (lane < count0) {
         const uint64_t off = leaf * 1024;
         const uint32_t n = (uint32_t)((len - off) < 1024 ? (len - off) : 1024);
         b3_leaf(chunk + off, len ? n : 0u, leaf, leaves == 1, cv);
-        if (leaves == 1) {
-            store_digest(hash_base + c * stride, cv);
-            return;
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) s_cv[lane][i] = cv[i];
     }
-    if (leaves == 1) return;
-    __syncthreads();
+    if (leaves == 1) {
+        if (lane == 0) store_digest(hash_base + c * stride, cv);
+        return;
+    }
     const bool whole = ngroups == 1;
-    uint32_t count = count0;
-    while (count > 1) {
-        const uint32_t half = count >> 1;
-        uint32_t t[8];
-        const bool act = lane < half;
-        if (act) b3_parent(s_cv[2 * lane], s_cv[2 * lane + 1], whole && count == 2, t);
-        const bool carry = (count & 1u) && lane == half;
-        if (carry) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) t[i] = s_cv[count - 1][i];
-        }
-        __syncthreads();
-        if (act || carry) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) s_cv[lane][i] = t[i];
-        }
-        __syncthreads();
-        count = (count + 1) >> 1;
-    }
+    b3_wave_fold(cv, count0, whole, lane);
     if (lane == 0) {
-        uint32_t r[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) r[i] = s_cv[0][i];
         if (whole) {
-            store_digest(hash_base + c * stride, r);
+            store_digest(hash_base + c * stride, cv);
         } else {
 #pragma unroll
-            for (int i = 0; i < 8; ++i) gcv[G * 8 + i] = r[i];
+            for (int i = 0; i < 8; ++i) gcv[G * 8 + i] = cv[i];
         }
     }
 }
 
-// One wave per chunk with more than one group: fold the subtree chaining values.
+// One wave per chunk with more than one group: fold the subtree chaining values
+// (<= 256 of them: chunks are <= 16 MiB).  Levels wider than 64 nodes go through
+// LDS; the last six levels are register shuffles (b3_wave_fold).
 __global__ __launch_bounds__(64) void k_b3_top(const DescRaw *__restrict__ desc, const uint64_t *__restrict__ total_p,
                                                uint64_t max_chunks, const uint64_t *__restrict__ group_base,
                                                const uint32_t *__restrict__ gcv, uint8_t *__restrict__ hash_base,
@@ -220,20 +221,29 @@ __global__ __launch_bounds__(64) void k_b3_top(const DescRaw *__restrict__ desc,
     uint32_t count = (uint32_t)(group_base[c + 1] - g0);
     if (count <= 1) return;
     const uint32_t lane = threadIdx.x;
+    if (count <= 64) {
+        uint32_t cv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (lane < count)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) cv[i] = gcv[(g0 + lane) * 8 + i];
+        b3_wave_fold(cv, count, true, lane);
+        if (lane == 0) store_digest(hash_base + c * stride, cv);
+        return;
+    }
     for (uint32_t k = lane; k < count; k += 64)
 #pragma unroll
         for (int i = 0; i < 8; ++i) s_cv[k][i] = gcv[(g0 + k) * 8 + i];
     __syncthreads();
-    while (count > 1) {
+    while (count > 64) {
         const uint32_t half = count >> 1;
-        uint32_t t[4][8];
-        bool wr[4];
+        uint32_t t[2][8];
+        bool wr[2];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
+        for (int s = 0; s < 2; ++s) {
             const uint32_t j = lane + 64u * s;
             wr[s] = false;
             if (j < half) {
-                b3_parent(s_cv[2 * j], s_cv[2 * j + 1], count == 2, t[s]);
+                b3_parent(s_cv[2 * j], s_cv[2 * j + 1], false, t[s]);
                 wr[s] = true;
             } else if ((count & 1u) && j == half) {
 #pragma unroll
@@ -243,19 +253,19 @@ __global__ __launch_bounds__(64) void k_b3_top(const DescRaw *__restrict__ desc,
         }
         __syncthreads();
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
+        for (int s = 0; s < 2; ++s)
             if (wr[s])
 #pragma unroll
                 for (int i = 0; i < 8; ++i) s_cv[lane + 64u * s][i] = t[s][i];
         __syncthreads();
         count = (count + 1) >> 1;
     }
-    if (lane == 0) {
-        uint32_t r[8];
+    uint32_t cv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (lane < count)
 #pragma unroll
-        for (int i = 0; i < 8; ++i) r[i] = s_cv[0][i];
-        store_digest(hash_base + c * stride, r);
-    }
+        for (int i = 0; i < 8; ++i) cv[i] = s_cv[lane][i];
+    b3_wave_fold(cv, count, true, lane);
+    if (lane == 0) store_digest(hash_base + c * stride, cv);
 }
 
 size_t blake3_group_bound(uint64_t total_bytes, uint64_t max_chunks) { return total_bytes / 65536 + max_chunks + 1; }
@@ -270,7 +280,7 @@ void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
                        max_chunks, d_gcount_u32);
     launch_exclusive_scan_u32(d_gcount_u32, d_group_base, max_chunks, 0, d_scan_tmp, st);
     const uint64_t gbound = blake3_group_bound(total_bytes, max_chunks);
-    hipLaunchKernelGGL(k_b3_groups, dim3((uint32_t)gbound), dim3(64), 0, st, d_data, d_abs, desc, d_total,
+    hipLaunchKernelGGL(k_b3_groups, dim3((uint32_t)((gbound + B3_WAVES - 1) / B3_WAVES)), dim3(64 * B3_WAVES), 0, st, d_data, d_abs, desc, d_total,
                        max_chunks, d_group_base, d_hash_base, hash_stride, d_gcv);
     hipLaunchKernelGGL(k_b3_top, dim3((uint32_t)max_chunks), dim3(64), 0, st, desc, d_total, max_chunks,
                        d_group_base, d_gcv, d_hash_base, hash_stride);

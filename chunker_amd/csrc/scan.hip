@@ -102,19 +102,16 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan(const uint8_t *__restrict__ da
                         acc = min(acc, ((uint32_t)h & ml) | ((uint32_t)(h >> 32) & mh));
                     }
             }
-            if (acc == 0) {  // rare: exact re-walk of this piece for this lane
+            if (acc == 0) {  // rare: exact re-walk of this piece for this lane, re-read from L2
                 uint64_t hh = h0;
-                for (int k = 0; k < (int)(PIECE / 16); ++k) {
-                    const uint32_t w[4] = {cur[k].x, cur[k].y, cur[k].z, cur[k].w};
-                    for (int j = 0; j < 4; ++j)
-                        for (int b = 0; b < 4; ++b) {
-                            hh = (hh << 1) + lds_gear(gbase, gear_addr(w[j], lo8, b));
-                            const uint32_t f = gear_flags(hh, mask_s, mask_l);
-                            if (f) {
-                                if (count < cap) cand[count] = ((uint32_t)(p - start + 16 * k + 4 * j + b) << 2) | f;
-                                ++count;
-                            }
-                        }
+#pragma unroll 1
+                for (uint32_t i = 0; i < PIECE; ++i) {
+                    hh = (hh << 1) + lds_gear(gbase, ((uint32_t)data[p + i] << 8) | lo8);
+                    const uint32_t f = gear_flags(hh, mask_s, mask_l);
+                    if (f) {
+                        if (count < cap) cand[count] = ((uint32_t)(p - start + i) << 2) | f;
+                        ++count;
+                    }
                 }
             }
         } else {
