@@ -80,7 +80,7 @@ __device__ __forceinline__ void b3_leaf(const uint8_t *p, uint32_t n, uint64_t c
 #pragma unroll
     for (int i = 0; i < 8; ++i) cv[i] = B3_IV[i];
     const uint32_t shift = (uint32_t)((uintptr_t)p & 3u);
-    const uint32_t *base = reinterpret_cast<const uint32_t *>((uintptr_t)p - shift);
+    const uint32_t *base = reinterpret_cast<const uint32_t *>(p - shift);
     const uint32_t nblk = n ? (n + 63) / 64 : 1;
     const uint8_t *endp = p + n;
     for (uint32_t j = 0; j < nblk; ++j) {

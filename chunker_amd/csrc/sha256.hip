@@ -83,7 +83,7 @@ __global__ __launch_bounds__(64) void k_sha256(const uint8_t *__restrict__ data,
     const uint64_t len = desc[g].length;
     const uint8_t *p = data + abs[g];
     const uint32_t shift = (uint32_t)((uintptr_t)p & 3u);
-    const uint32_t *base = reinterpret_cast<const uint32_t *>((uintptr_t)p - shift);
+    const uint32_t *base = reinterpret_cast<const uint32_t *>(p - shift);
     // v_perm selector: big-endian word from bytes shift..shift+3 of {hi:lo}
     const uint32_t sel = (shift << 24) | ((shift + 1) << 16) | ((shift + 2) << 8) | (shift + 3);
 

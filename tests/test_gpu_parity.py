@@ -97,6 +97,24 @@ def test_descriptors_match_oracle(ca, O, name, make, params, algo):
         assert len(data) == 0
 
 
+@pytest.mark.parametrize("params,seed", [((1024, 6000, 16384), 22), ((4096, 16384, 65536), 22)])
+def test_speculative_walk_rewalks(ca, O, params, seed):
+    """Inputs whose cuts fall inside the 47-position warm-up window (where the
+    windowed candidate list is not valid): the speculative walker must detect them in
+    its verification pass and re-walk (and fall back to exact mode after 4)."""
+    data = rand_bytes(30_000_000, seed)
+    ref = O.chunk_descriptors(data, *params, algo=SHA)
+    s_off = 2 * (params[0] // 2)
+    warm = int(np.sum((ref["length"][:-1] >= s_off) & (ref["length"][:-1] < s_off + 47)))
+    assert warm >= 2, "fixture no longer exercises warm-up cuts"
+    assert_same(ca.chunk_descriptors_array(data, *params), ref, f"warm={warm}")
+    # same bytes split into 3 NARs of one batch
+    parts = [data[:9_999_991], data[9_999_991:20_000_003], data[20_000_003:]]
+    got = ca.chunk_batch(parts, *params)
+    for i, part in enumerate(parts):
+        assert_same(got[i], O.chunk_descriptors(part, *params, algo=SHA), f"part{i}")
+
+
 @pytest.mark.parametrize("algo", [SHA, B3], ids=["sha256", "blake3"])
 def test_batch_ragged_unaligned(ca, O, algo):
     rng = np.random.default_rng(99)
