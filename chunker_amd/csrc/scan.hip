@@ -37,8 +37,42 @@ __device__ __forceinline__ uint64_t lds_gear(const char *base, uint32_t addr) {
     return *reinterpret_cast<const uint64_t *>(base + addr);
 }
 
-// K1.  Each lane owns CG_SEG bytes of the flat batch buffer.  Data arrive as 128-B
-// pieces (8 x dwordx4 per lane, next piece prefetched into registers).
+// 4x4 transpose of 16-byte elements inside each quad of lanes: on entry lane i
+// holds v[j] = quarter i of lane j's 64-byte piece; on exit lane i holds v[j] =
+// quarter j of its own piece.  Two rounds of DPP quad_perm swaps (lane^1, lane^2),
+// each a v_mov_dpp + select per dword.
+template <int CTRL, int BIT>
+__device__ __forceinline__ void quad_swap(uint4 v[4], uint32_t lane) {
+    uint4 t[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint4 src = v[j ^ BIT];
+        t[j].x = __builtin_amdgcn_mov_dpp(src.x, CTRL, 0xf, 0xf, false);
+        t[j].y = __builtin_amdgcn_mov_dpp(src.y, CTRL, 0xf, 0xf, false);
+        t[j].z = __builtin_amdgcn_mov_dpp(src.z, CTRL, 0xf, 0xf, false);
+        t[j].w = __builtin_amdgcn_mov_dpp(src.w, CTRL, 0xf, 0xf, false);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const bool take = ((lane ^ (uint32_t)j) & BIT) != 0;
+        v[j].x = take ? t[j].x : v[j].x;
+        v[j].y = take ? t[j].y : v[j].y;
+        v[j].z = take ? t[j].z : v[j].z;
+        v[j].w = take ? t[j].w : v[j].w;
+    }
+}
+
+__device__ __forceinline__ void quad_transpose(uint4 v[4], uint32_t lane) {
+    quad_swap<0xB1, 1>(v, lane);  // quad_perm [1,0,3,2]
+    quad_swap<0x4E, 2>(v, lane);  // quad_perm [2,3,0,1]
+}
+
+#define QPIECE 64u
+
+// K1.  Each lane owns CG_SEG bytes of the flat batch buffer.  Bytes arrive in 64-B
+// pieces loaded cooperatively by the 4 lanes of a quad (each dwordx4 instruction
+// reads 16 whole 64-B runs instead of 64 scattered 16-B pieces) and transposed in
+// registers; two pieces are in flight ahead of the one being hashed.
 // PRE = prefilter mode: per byte only (h & (mask_s & mask_l)) is folded into a
 // running min (5 VALU + 1 LDS read per byte); a piece whose min hits 0 in some lane
 // is re-walked exactly for that lane.  Used when mask_s & mask_l has >= 15 bits
@@ -53,16 +87,30 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan(const uint8_t *__restrict__ da
     __syncthreads();
     const char *gbase = reinterpret_cast<const char *>(s_gear);
 
+    const uint32_t lane = threadIdx.x & 63u, qi = lane & 3u;
     const uint64_t seg = (uint64_t)blockIdx.x * SCAN2_T + threadIdx.x;
-    if (seg >= nseg) return;
+    // whole waves stay active through the cooperative loop (DPP needs every lane)
+    const uint64_t wave_first = seg - lane;
+    if (wave_first >= nseg) return;
+    const bool active = seg < nseg;
     const uint32_t lo8 = (threadIdx.x & 31u) * 8u;
     const uint64_t start = seg * CG_SEG;
-    const uint64_t end = start + CG_SEG < n ? start + CG_SEG : n;
+    const uint64_t end = active ? (start + CG_SEG < n ? start + CG_SEG : n) : start;
+    const uint32_t npieces = active ? (uint32_t)((end - start) / QPIECE) : 0u;
     const uint64_t mask_c = mask_s & mask_l;
     const uint32_t ml = (uint32_t)mask_c, mh = (uint32_t)(mask_c >> 32);
 
+    // the quad's 4 owners: segments seg - qi + j; this lane loads quarter qi of each
+    uint64_t own_start[4];
+    uint32_t own_np[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        own_start[j] = __shfl(start, (int)((lane & ~3u) + j), 64);
+        own_np[j] = __shfl(npieces, (int)((lane & ~3u) + j), 64);
+    }
+
     uint64_t h = 0;
-    if (start >= CG_HALO) {  // warm-up over the 48 bytes before the segment
+    if (active && start >= CG_HALO) {  // warm-up over the 48 bytes before the segment
         const uint4 *hp = reinterpret_cast<const uint4 *>(data + start - CG_HALO);
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -77,65 +125,77 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan(const uint8_t *__restrict__ da
 
     uint32_t count = 0;
     uint32_t *cand = seg_cand + seg * cap;
-    uint64_t p = start;
-    uint4 cur[PIECE / 16], nxt[PIECE / 16];
-    if (p + PIECE <= end) {
+    const uint32_t rounds = CG_SEG / QPIECE;  // wave-uniform trip count
+    uint4 buf[3][4];
+    auto issue = [&](uint4(&v)[4], uint32_t r) {
 #pragma unroll
-        for (int k = 0; k < (int)(PIECE / 16); ++k) cur[k] = reinterpret_cast<const uint4 *>(data + p)[k];
-    }
-    while (p + PIECE <= end) {
-        if (p + 2 * PIECE <= end) {
-#pragma unroll
-            for (int k = 0; k < (int)(PIECE / 16); ++k) nxt[k] = reinterpret_cast<const uint4 *>(data + p + PIECE)[k];
-        }
-        const uint64_t h0 = h;
-        if (PRE) {
-            uint32_t acc = 0xffffffffu;
-#pragma unroll
-            for (int k = 0; k < (int)(PIECE / 16); ++k) {
-                const uint32_t w[4] = {cur[k].x, cur[k].y, cur[k].z, cur[k].w};
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-#pragma unroll
-                    for (int b = 0; b < 4; ++b) {
-                        h = (h << 1) + lds_gear(gbase, gear_addr(w[j], lo8, b));
-                        acc = min(acc, ((uint32_t)h & ml) | ((uint32_t)(h >> 32) & mh));
-                    }
-            }
-            if (acc == 0) {  // rare: exact re-walk of this piece for this lane, re-read from L2
-                uint64_t hh = h0;
+        for (int j = 0; j < 4; ++j)
+            v[j] = r < own_np[j]
+                       ? *reinterpret_cast<const uint4 *>(data + own_start[j] + (uint64_t)r * QPIECE + 16u * qi)
+                       : make_uint4(0, 0, 0, 0);
+    };
+    issue(buf[0], 0);
+    issue(buf[1], 1);
 #pragma unroll 1
-                for (uint32_t i = 0; i < PIECE; ++i) {
-                    hh = (hh << 1) + lds_gear(gbase, ((uint32_t)data[p + i] << 8) | lo8);
-                    const uint32_t f = gear_flags(hh, mask_s, mask_l);
-                    if (f) {
-                        if (count < cap) cand[count] = ((uint32_t)(p - start + i) << 2) | f;
-                        ++count;
+    for (uint32_t r = 0; r < rounds; r += 3) {
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            const uint32_t rr = r + u;
+            if (rr >= rounds) break;
+            issue(buf[(u + 2) % 3], rr + 2);
+            uint4 v[4] = {buf[u][0], buf[u][1], buf[u][2], buf[u][3]};
+            quad_transpose(v, lane);
+            if (rr < npieces) {
+                const uint64_t p = start + (uint64_t)rr * QPIECE;
+                const uint64_t h0 = h;
+                if (PRE) {
+                    uint32_t acc = 0xffffffffu;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+#pragma unroll
+                            for (int b = 0; b < 4; ++b) {
+                                h = (h << 1) + lds_gear(gbase, gear_addr(w[j], lo8, b));
+                                acc = min(acc, ((uint32_t)h & ml) | ((uint32_t)(h >> 32) & mh));
+                            }
+                    }
+                    if (acc == 0) {  // rare: exact re-walk of this piece, re-read from L2
+                        uint64_t hh = h0;
+#pragma unroll 1
+                        for (uint32_t i = 0; i < QPIECE; ++i) {
+                            hh = (hh << 1) + lds_gear(gbase, ((uint32_t)data[p + i] << 8) | lo8);
+                            const uint32_t f = gear_flags(hh, mask_s, mask_l);
+                            if (f) {
+                                if (count < cap) cand[count] = ((uint32_t)(p - start + i) << 2) | f;
+                                ++count;
+                            }
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+#pragma unroll
+                            for (int b = 0; b < 4; ++b) {
+                                h = (h << 1) + lds_gear(gbase, gear_addr(w[j], lo8, b));
+                                const uint32_t f = gear_flags(h, mask_s, mask_l);
+                                if (f) {
+                                    if (count < cap)
+                                        cand[count] = ((uint32_t)(p - start + 16 * k + 4 * j + b) << 2) | f;
+                                    ++count;
+                                }
+                            }
                     }
                 }
             }
-        } else {
-#pragma unroll
-            for (int k = 0; k < (int)(PIECE / 16); ++k) {
-                const uint32_t w[4] = {cur[k].x, cur[k].y, cur[k].z, cur[k].w};
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-#pragma unroll
-                    for (int b = 0; b < 4; ++b) {
-                        h = (h << 1) + lds_gear(gbase, gear_addr(w[j], lo8, b));
-                        const uint32_t f = gear_flags(h, mask_s, mask_l);
-                        if (f) {
-                            if (count < cap) cand[count] = ((uint32_t)(p - start + 16 * k + 4 * j + b) << 2) | f;
-                            ++count;
-                        }
-                    }
-            }
         }
-#pragma unroll
-        for (int k = 0; k < (int)(PIECE / 16); ++k) cur[k] = nxt[k];
-        p += PIECE;
     }
-    for (; p < end; ++p) {  // ragged tail of the last segment (< 128 bytes)
+    if (!active) return;
+    for (uint64_t p = start + (uint64_t)npieces * QPIECE; p < end; ++p) {  // ragged tail (< 64 bytes)
         h = (h << 1) + lds_gear(gbase, ((uint32_t)data[p] << 8) | lo8);
         const uint32_t f = gear_flags(h, mask_s, mask_l);
         if (f) {

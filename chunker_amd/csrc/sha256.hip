@@ -39,119 +39,169 @@ __device__ __forceinline__ uint32_t add3(uint32_t a, uint32_t b, uint32_t c) { r
 #define SHA_s0(x) xor3(rotr32(x, 7), rotr32(x, 18), (x) >> 3)
 #define SHA_s1(x) xor3(rotr32(x, 17), rotr32(x, 19), (x) >> 10)
 
-// One round: 14 VALU (4 Sigma1, 1 Ch, 4 Sigma0, 1 Maj, 4 adds); renaming by macro
-// argument rotation, so no register moves.
-#define SHA_RND(a, b, c, d, e, f, g, h, i)                          \
-    {                                                               \
-        const uint32_t t1 = add3(add3(h, w[(i) & 15], SHA_K[i]), SHA_S1(e), ch(e, f, g)); \
-        d += t1;                                                    \
-        h = add3(t1, SHA_S0(a), maj(a, b, c));                      \
+// ---------------------------------------------------------------------------
+// Producer/consumer SHA-256.  A chunk's compressions are a serial chain, and one
+// wave issues one VALU instruction every ~4 cycles (MI355X_MICROARCH.md, "vector-
+// instruction ISSUE cost"), so the chain's speed is set by the instructions ONE wave
+// must issue per block.  Each workgroup therefore pairs two waves on the same 64
+// chunks (one chunk per lane):
+//   wave 0 (producer): loads the block, realigns + byte-swaps it (v_perm_b32),
+//          builds the final padded block(s), expands the 64-word message schedule
+//          and writes it to an LDS row per lane (double-buffered);
+//   wave 1 (consumer): runs only the 64 rounds (14 VALU each) reading W from LDS.
+// One barrier per block hands a buffer over.  The consumer issues ~900 VALU per
+// block instead of ~1,400.
+// ---------------------------------------------------------------------------
+#define PC_ROW 68u  // 64 words + 4 pad per lane: 16 consecutive lanes' 16-B accesses hit distinct banks
+
+#define SHA_RNDW(a, b, c, d, e, f, g, h, i, wv)                                  \
+    {                                                                            \
+        const uint32_t t1 = add3(add3(h, (wv), SHA_K[i]), SHA_S1(e), ch(e, f, g)); \
+        d += t1;                                                                 \
+        h = add3(t1, SHA_S0(a), maj(a, b, c));                                   \
     }
 
-__device__ __forceinline__ void sha256_compress(uint32_t st[8], uint32_t w[16]) {
+__device__ __forceinline__ void sha_rounds_lds(uint32_t st[8], const uint32_t *row) {
     uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
 #pragma unroll
     for (int i = 0; i < 64; i += 8) {
-        if (i >= 16) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int t = i + j;
-                w[t & 15] = add3(w[t & 15], SHA_s0(w[(t - 15) & 15]), w[(t - 7) & 15]) + SHA_s1(w[(t - 2) & 15]);
-            }
-        }
-        SHA_RND(a, b, c, d, e, f, g, h, i + 0);
-        SHA_RND(h, a, b, c, d, e, f, g, i + 1);
-        SHA_RND(g, h, a, b, c, d, e, f, i + 2);
-        SHA_RND(f, g, h, a, b, c, d, e, i + 3);
-        SHA_RND(e, f, g, h, a, b, c, d, i + 4);
-        SHA_RND(d, e, f, g, h, a, b, c, i + 5);
-        SHA_RND(c, d, e, f, g, h, a, b, i + 6);
-        SHA_RND(b, c, d, e, f, g, h, a, i + 7);
+        const uint4 wa = *reinterpret_cast<const uint4 *>(row + i);
+        const uint4 wb = *reinterpret_cast<const uint4 *>(row + i + 4);
+        SHA_RNDW(a, b, c, d, e, f, g, h, i + 0, wa.x);
+        SHA_RNDW(h, a, b, c, d, e, f, g, i + 1, wa.y);
+        SHA_RNDW(g, h, a, b, c, d, e, f, i + 2, wa.z);
+        SHA_RNDW(f, g, h, a, b, c, d, e, i + 3, wa.w);
+        SHA_RNDW(e, f, g, h, a, b, c, d, i + 4, wb.x);
+        SHA_RNDW(d, e, f, g, h, a, b, c, i + 5, wb.y);
+        SHA_RNDW(c, d, e, f, g, h, a, b, i + 6, wb.z);
+        SHA_RNDW(b, c, d, e, f, g, h, a, i + 7, wb.w);
     }
     st[0] += a; st[1] += b; st[2] += c; st[3] += d;
     st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
 
-__global__ __launch_bounds__(64) void k_sha256(const uint8_t *__restrict__ data, const uint64_t *__restrict__ abs,
+// Expand w[0..15] into the full schedule and store all 64 words to `row` (LDS).
+__device__ __forceinline__ void sha_schedule_store(uint32_t w[16], uint32_t *row) {
+#pragma unroll
+    for (int i = 0; i < 16; i += 4)
+        *reinterpret_cast<uint4 *>(row + i) = make_uint4(w[i], w[i + 1], w[i + 2], w[i + 3]);
+#pragma unroll
+    for (int t = 16; t < 64; t += 4) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int u = t + j;
+            w[u & 15] = add3(w[u & 15], SHA_s0(w[(u - 15) & 15]), w[(u - 7) & 15]) + SHA_s1(w[(u - 2) & 15]);
+        }
+        *reinterpret_cast<uint4 *>(row + t) =
+            make_uint4(w[t & 15], w[(t + 1) & 15], w[(t + 2) & 15], w[(t + 3) & 15]);
+    }
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, d, 64));
+    return v;
+}
+
+__global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data, const uint64_t *__restrict__ abs,
                                                const DescRaw *__restrict__ desc, const uint64_t *__restrict__ total_p,
                                                uint64_t max_chunks, uint8_t *__restrict__ hash_base,
                                                size_t stride) {
-    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ __attribute__((aligned(16))) uint32_t sW[2][64 * PC_ROW];
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool producer = threadIdx.x < 64;
+    const uint64_t g = (uint64_t)blockIdx.x * 64 + lane;
     uint64_t total = *total_p;
     if (total > max_chunks) total = max_chunks;
-    if (g >= total) return;
-    const uint64_t len = desc[g].length;
-    const uint8_t *p = data + abs[g];
-    const uint32_t shift = (uint32_t)((uintptr_t)p & 3u);
-    const uint32_t *base = reinterpret_cast<const uint32_t *>(p - shift);
-    // v_perm selector: big-endian word from bytes shift..shift+3 of {hi:lo}
-    const uint32_t sel = (shift << 24) | ((shift + 1) << 16) | ((shift + 2) << 8) | (shift + 3);
-
-    uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    if ((uint64_t)blockIdx.x * 64 >= total) return;  // whole workgroup idle (uniform)
+    const bool valid = g < total;
+    const uint64_t len = valid ? desc[g].length : 0;
     const uint64_t nb = len >> 6;
-    // software pipeline: block k+1's 17 dwords are in flight while block k compresses
-    uint32_t nx[17];
-    if (nb) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) nx[i] = base[i];
-        nx[16] = shift ? base[16] : 0u;
-    }
-    for (uint64_t blk = 0; blk < nb; ++blk) {
-        uint32_t w[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_perm(nx[i + 1], nx[i], sel);
-        if (blk + 1 < nb) {
-            const uint32_t *q = base + 16 * (blk + 1);
-#pragma unroll
-            for (int i = 0; i < 16; ++i) nx[i] = q[i];
-            nx[16] = shift ? q[16] : 0u;
-        }
-        sha256_compress(st, w);
-    }
-    // final block(s): tail bytes, 0x80, zeros, 64-bit big-endian bit length
     const uint32_t rem = (uint32_t)(len & 63u);
-    const uint32_t *q = base + 16 * nb;
-    const uint8_t *endp = p + len;
-    uint32_t dw[17], w[16];
+    const uint32_t nbt = valid ? (uint32_t)(nb + (rem < 56 ? 1 : 2)) : 0u;  // blocks incl. padding
+    const uint32_t NB = wave_max_u32(nbt);  // identical in both waves (same 64 chunks)
+
+    if (producer) {
+        const uint8_t *p = data + (valid ? abs[g] : 0);
+        const uint32_t shift = (uint32_t)((uintptr_t)p & 3u);
+        const uint32_t *base = reinterpret_cast<const uint32_t *>(p - shift);
+        const uint32_t sel = (shift << 24) | ((shift + 1) << 16) | ((shift + 2) << 8) | (shift + 3);
+        const uint64_t bits = len << 3;
+        uint32_t dcur[17], dnx[17];
+        auto load_full = [&](uint32_t (&d)[17], uint64_t k) {
+            const uint32_t *q = base + 16 * k;
 #pragma unroll
-    for (int i = 0; i < 17; ++i) dw[i] = (reinterpret_cast<const uint8_t *>(q + i) < endp) ? q[i] : 0u;
+            for (int i = 0; i < 16; ++i) d[i] = q[i];
+            d[16] = shift ? q[16] : 0u;
+        };
+        auto fill = [&](uint32_t k, uint32_t *row) {  // block k of this lane's chunk into row
+            uint32_t w[16];
+            if (k < nb) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const uint32_t v = __builtin_amdgcn_perm(dw[i + 1], dw[i], sel);
-        const int r = (int)rem - 4 * i;  // bytes of this word that are message
-        uint32_t o;
-        if (r >= 4)
-            o = v;
-        else if (r < 0)
-            o = 0u;
-        else
-            o = (r ? (v & (0xffffffffu << (32 - 8 * r))) : 0u) | (0x80u << (24 - 8 * r));
-        w[i] = o;
-    }
-    const uint64_t bits = len << 3;
-    if (rem < 56) {
-        w[14] = (uint32_t)(bits >> 32);
-        w[15] = (uint32_t)bits;
-        sha256_compress(st, w);
+                for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_perm(dcur[i + 1], dcur[i], sel);
+            } else if (k == nb) {  // tail bytes, 0x80, zeros, [length]
+                const uint32_t *q = base + 16 * nb;
+                const uint8_t *endp = p + len;
+                uint32_t dw[17];
+#pragma unroll
+                for (int i = 0; i < 17; ++i) dw[i] = (reinterpret_cast<const uint8_t *>(q + i) < endp) ? q[i] : 0u;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const uint32_t v = __builtin_amdgcn_perm(dw[i + 1], dw[i], sel);
+                    const int r = (int)rem - 4 * i;
+                    w[i] = r >= 4 ? v : (r < 0 ? 0u : ((r ? (v & (0xffffffffu << (32 - 8 * r))) : 0u) | (0x80u << (24 - 8 * r))));
+                }
+                if (rem < 56) {
+                    w[14] = (uint32_t)(bits >> 32);
+                    w[15] = (uint32_t)bits;
+                }
+            } else {  // second padding block
+#pragma unroll
+                for (int i = 0; i < 14; ++i) w[i] = 0u;
+                w[14] = (uint32_t)(bits >> 32);
+                w[15] = (uint32_t)bits;
+            }
+            sha_schedule_store(w, row);
+        };
+        // dcur holds block k's words when fill(k) runs; dnx is the prefetched block k+1
+        if (nb > 0) load_full(dcur, 0);
+        if (nb > 1) load_full(dnx, 1);
+        if (0 < nbt) fill(0, &sW[0][lane * PC_ROW]);
+        __syncthreads();
+        for (uint32_t k = 0; k < NB; ++k) {
+            const uint32_t kn = k + 1;
+            if (kn < nbt) {
+                if (kn < nb) {
+#pragma unroll
+                    for (int i = 0; i < 17; ++i) dcur[i] = dnx[i];
+                    if (kn + 1 < nb) load_full(dnx, kn + 1);
+                }
+                fill(kn, &sW[kn & 1][lane * PC_ROW]);
+            }
+            __syncthreads();
+        }
     } else {
-        sha256_compress(st, w);
-#pragma unroll
-        for (int i = 0; i < 14; ++i) w[i] = 0u;
-        w[14] = (uint32_t)(bits >> 32);
-        w[15] = (uint32_t)bits;
-        sha256_compress(st, w);
+        uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                          0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+        __syncthreads();
+        for (uint32_t k = 0; k < NB; ++k) {
+            if (k < nbt) sha_rounds_lds(st, &sW[k & 1][lane * PC_ROW]);
+            __syncthreads();
+        }
+        if (valid) {
+            uint4 *o = reinterpret_cast<uint4 *>(hash_base + g * stride);
+            o[0] = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]), __builtin_bswap32(st[2]),
+                              __builtin_bswap32(st[3]));
+            o[1] = make_uint4(__builtin_bswap32(st[4]), __builtin_bswap32(st[5]), __builtin_bswap32(st[6]),
+                              __builtin_bswap32(st[7]));
+        }
     }
-    uint4 *o = reinterpret_cast<uint4 *>(hash_base + g * stride);
-    o[0] = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]), __builtin_bswap32(st[2]),
-                      __builtin_bswap32(st[3]));
-    o[1] = make_uint4(__builtin_bswap32(st[4]), __builtin_bswap32(st[5]), __builtin_bswap32(st[6]),
-                      __builtin_bswap32(st[7]));
 }
 
 void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
                    uint64_t max_chunks, uint8_t *d_hash_base, size_t hash_stride, hipStream_t st) {
     if (max_chunks == 0) return;
-    hipLaunchKernelGGL(k_sha256, dim3((uint32_t)((max_chunks + 63) / 64)), dim3(64), 0, st, d_data, d_abs,
+    hipLaunchKernelGGL(k_sha256, dim3((uint32_t)((max_chunks + 63) / 64)), dim3(128), 0, st, d_data, d_abs,
                        (const DescRaw *)d_desc, d_total, max_chunks, d_hash_base, hash_stride);
 }
 
