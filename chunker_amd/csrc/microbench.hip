@@ -1,0 +1,76 @@
+// microbench.hip -- diagnostic only (not on the product path): cycles per SHA-256
+// round for the round code the consumer wave of k_sha256 runs, measured with
+// s_memtime on the device.  Exposed as cg_diag_sha_rounds() for DESIGN.md's latency
+// model.
+#include "common.h"
+
+namespace cg {
+
+static constexpr uint32_t MK[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+__device__ __forceinline__ uint32_t mrot(uint32_t x, uint32_t n) { return __builtin_amdgcn_alignbit(x, x, n); }
+#define MX3(a, b, c) __builtin_amdgcn_bitop3_b32(a, b, c, 0x96)
+#define MS0(a) MX3(mrot(a, 2), mrot(a, 13), mrot(a, 22))
+#define MS1(e) MX3(mrot(e, 6), mrot(e, 11), mrot(e, 25))
+#define MRND(a, b, c, d, e, f, g, h, i, wv)                                                                  \
+    {                                                                                                        \
+        const uint32_t t1 = (h + (wv) + MK[i]) + MS1(e) + __builtin_amdgcn_bitop3_b32(e, f, g, 0xCA);      \
+        d += t1;                                                                                             \
+        h = t1 + MS0(a) + __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);                                       \
+    }
+
+__global__ void k_diag_sha_rounds(uint32_t iters, uint32_t *out, unsigned long long *cycles) {
+    const uint32_t lane = threadIdx.x;
+    uint32_t w[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i] = lane * 16 + i;
+    uint32_t a = lane, b = 1, c = 2, d = 3, e = 4, f = 5, g = 6, h = 7;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int i = 0; i < 64; i += 8) {
+            MRND(a, b, c, d, e, f, g, h, i + 0, w[(i + 0) & 15]);
+            MRND(h, a, b, c, d, e, f, g, i + 1, w[(i + 1) & 15]);
+            MRND(g, h, a, b, c, d, e, f, i + 2, w[(i + 2) & 15]);
+            MRND(f, g, h, a, b, c, d, e, i + 3, w[(i + 3) & 15]);
+            MRND(e, f, g, h, a, b, c, d, i + 4, w[(i + 4) & 15]);
+            MRND(d, e, f, g, h, a, b, c, i + 5, w[(i + 5) & 15]);
+            MRND(c, d, e, f, g, h, a, b, i + 6, w[(i + 6) & 15]);
+            MRND(b, c, d, e, f, g, h, a, i + 7, w[(i + 7) & 15]);
+        }
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+    out[blockIdx.x * blockDim.x + lane] = a ^ b ^ c ^ d ^ e ^ f ^ g ^ h;
+    if (lane == 0) {
+        const uint32_t wv = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+        cycles[2 * wv] = t1 - t0;      // shader clocks
+        cycles[2 * wv + 1] = r1 - r0;  // 100 MHz ticks
+    }
+}
+
+}  // namespace cg
+
+// cycles[2k], cycles[2k+1] = shader clocks, 100 MHz ticks of wave k; blocks x threads_per_block launched (threads multiple of 64)
+extern "C" int cg_diag_sha_rounds(uint32_t iters, uint32_t blocks, uint32_t threads, unsigned long long *h_cycles) {
+    uint32_t *d_out = nullptr;
+    unsigned long long *d_cyc = nullptr;
+    const uint32_t waves = blocks * (threads / 64);
+    if (hipMalloc(&d_out, (size_t)blocks * threads * 4) != hipSuccess) return 2;
+    if (hipMalloc(&d_cyc, waves * 16) != hipSuccess) return 2;
+    hipLaunchKernelGGL(cg::k_diag_sha_rounds, dim3(blocks), dim3(threads), 0, 0, iters, d_out, d_cyc);
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(h_cycles, d_cyc, waves * 16, hipMemcpyDeviceToHost);
+    (void)hipFree(d_out);
+    (void)hipFree(d_cyc);
+    return e == hipSuccess ? 0 : 2;
+}

@@ -62,11 +62,14 @@ __device__ __forceinline__ uint32_t add3(uint32_t a, uint32_t b, uint32_t c) { r
     }
 
 __device__ __forceinline__ void sha_rounds_lds(uint32_t st[8], const uint32_t *row) {
+    // all 16 ds_read_b128 issued up front: one LDS latency per block, not sixteen
+    uint4 wv[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) wv[i] = *reinterpret_cast<const uint4 *>(row + 4 * i);
     uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
 #pragma unroll
     for (int i = 0; i < 64; i += 8) {
-        const uint4 wa = *reinterpret_cast<const uint4 *>(row + i);
-        const uint4 wb = *reinterpret_cast<const uint4 *>(row + i + 4);
+        const uint4 wa = wv[i / 4], wb = wv[i / 4 + 1];
         SHA_RNDW(a, b, c, d, e, f, g, h, i + 0, wa.x);
         SHA_RNDW(h, a, b, c, d, e, f, g, i + 1, wa.y);
         SHA_RNDW(g, h, a, b, c, d, e, f, i + 2, wa.z);
