@@ -261,6 +261,23 @@ def chunk_batch(nars: Sequence, min_size=None, avg_size=None, max_size=None,
     return [out[int(first[i]):int(first[i + 1])] for i in range(len(arrs))]
 
 
+def chunk_batch_flat(flat, nar_offsets, min_size=None, avg_size=None, max_size=None,
+                     hash: HashAlgorithm = HashAlgorithm.Sha256, out: np.ndarray | None = None):
+    """Host-resident batch without re-packing: `flat` holds the NARs back to back,
+    NAR i = flat[nar_offsets[i]:nar_offsets[i+1]].  Returns (descriptors, nar_first)."""
+    o = ChunkingOptions.resolve(min_size, avg_size, max_size)
+    a = _as_u8(flat)
+    offs = np.ascontiguousarray(nar_offsets, dtype=np.uint64)
+    n = len(offs) - 1
+    cap = max(batch_capacity(offs, o.min_size), 1)
+    if out is None or len(out) < cap:
+        out = np.zeros(cap, DESC_DTYPE)
+    first = np.zeros(n + 1, np.uint64)
+    _check(lib.cg_chunk_batch(_ptr(a), offs.ctypes.data, n, o.min_size, o.avg_size, o.max_size, int(hash),
+                              out.ctypes.data, len(out), first.ctypes.data), len(a))
+    return out[: int(first[-1])], first
+
+
 def chunk_batch_device(d_data_ptr: int, nar_offsets: np.ndarray, d_out_ptr: int, out_cap: int,
                        min_size=None, avg_size=None, max_size=None,
                        hash: HashAlgorithm = HashAlgorithm.Sha256, stream: int = 0) -> np.ndarray:

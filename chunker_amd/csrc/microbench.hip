@@ -51,14 +51,68 @@ __global__ void k_diag_sha_rounds(uint32_t iters, uint32_t *out, unsigned long l
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
     out[blockIdx.x * blockDim.x + lane] = a ^ b ^ c ^ d ^ e ^ f ^ g ^ h;
-    if (lane == 0) {
+    if ((lane & 63) == 0) {
         const uint32_t wv = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
         cycles[2 * wv] = t1 - t0;      // shader clocks
         cycles[2 * wv + 1] = r1 - r0;  // 100 MHz ticks
     }
 }
 
+// Variant: W read from LDS every block (16 ds_read_b128 + a counter read/write),
+// as the consumer wave of k_sha256 does.
+__global__ void k_diag_sha_rounds_lds(uint32_t iters, uint32_t *out, unsigned long long *cycles) {
+    __shared__ __attribute__((aligned(16))) uint32_t sW[64 * 68];
+    __shared__ uint32_t s_ctr;
+    const uint32_t lane = threadIdx.x;
+    for (int i = 0; i < 68; ++i) sW[lane * 68 + i] = lane * 16 + i;
+    if (lane == 0) s_ctr = 0;
+    __syncthreads();
+    uint32_t a = lane, b = 1, c = 2, d = 3, e = 4, f = 5, g = 6, h = 7;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t it = 0; it < iters; ++it) {
+        while (__hip_atomic_load(&s_ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < it) __builtin_amdgcn_s_sleep(1);
+        uint4 wv[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) wv[i] = *reinterpret_cast<const uint4 *>(&sW[lane * 68 + 4 * i]);
+#pragma unroll
+        for (int i = 0; i < 64; i += 8) {
+            const uint4 wa = wv[i / 4], wb = wv[i / 4 + 1];
+            MRND(a, b, c, d, e, f, g, h, i + 0, wa.x);
+            MRND(h, a, b, c, d, e, f, g, i + 1, wa.y);
+            MRND(g, h, a, b, c, d, e, f, i + 2, wa.z);
+            MRND(f, g, h, a, b, c, d, e, i + 3, wa.w);
+            MRND(e, f, g, h, a, b, c, d, i + 4, wb.x);
+            MRND(d, e, f, g, h, a, b, c, i + 5, wb.y);
+            MRND(c, d, e, f, g, h, a, b, i + 6, wb.z);
+            MRND(b, c, d, e, f, g, h, a, i + 7, wb.w);
+        }
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        if (lane == 0) __hip_atomic_store(&s_ctr, it + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+    out[blockIdx.x * blockDim.x + lane] = a ^ b ^ c ^ d ^ e ^ f ^ g ^ h;
+    if (lane == 0) {
+        cycles[2 * blockIdx.x] = t1 - t0;
+        cycles[2 * blockIdx.x + 1] = r1 - r0;
+    }
+}
+
 }  // namespace cg
+
+extern "C" int cg_diag_sha_rounds_lds(uint32_t iters, uint32_t blocks, unsigned long long *h_cycles) {
+    uint32_t *d_out = nullptr;
+    unsigned long long *d_cyc = nullptr;
+    if (hipMalloc(&d_out, (size_t)blocks * 64 * 4) != hipSuccess) return 2;
+    if (hipMalloc(&d_cyc, blocks * 16) != hipSuccess) return 2;
+    hipLaunchKernelGGL(cg::k_diag_sha_rounds_lds, dim3(blocks), dim3(64), 0, 0, iters, d_out, d_cyc);
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(h_cycles, d_cyc, blocks * 16, hipMemcpyDeviceToHost);
+    (void)hipFree(d_out);
+    (void)hipFree(d_cyc);
+    return e == hipSuccess ? 0 : 2;
+}
 
 // cycles[2k], cycles[2k+1] = shader clocks, 100 MHz ticks of wave k; blocks x threads_per_block launched (threads multiple of 64)
 extern "C" int cg_diag_sha_rounds(uint32_t iters, uint32_t blocks, uint32_t threads, unsigned long long *h_cycles) {
@@ -73,4 +127,31 @@ extern "C" int cg_diag_sha_rounds(uint32_t iters, uint32_t blocks, uint32_t thre
     (void)hipFree(d_out);
     (void)hipFree(d_cyc);
     return e == hipSuccess ? 0 : 2;
+}
+
+namespace cg {
+extern unsigned long long *g_sha_diag;
+}
+// Enable (n_wg > 0) / read back / disable (n_wg == 0) per-workgroup SHA producer and
+// consumer timing: out[4*wg + {0,1,2,3}] = producer spin, producer total, consumer
+// spin, consumer total (shader clocks).  Diagnostics only.
+extern "C" int cg_diag_sha_stats(uint32_t n_wg, unsigned long long *out) {
+    static unsigned long long *buf = nullptr;
+    static uint32_t cap = 0;
+    if (n_wg == 0) {
+        cg::g_sha_diag = nullptr;
+        return 0;
+    }
+    if (out == nullptr) {  // arm
+        if (n_wg > cap) {
+            if (buf) (void)hipFree(buf);
+            if (hipMalloc(&buf, (size_t)n_wg * 32) != hipSuccess) return 2;
+            cap = n_wg;
+        }
+        (void)hipMemset(buf, 0, (size_t)n_wg * 32);
+        cg::g_sha_diag = buf;
+        return 0;
+    }
+    (void)hipDeviceSynchronize();
+    return hipMemcpy(out, buf, (size_t)n_wg * 32, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 2;
 }

@@ -61,24 +61,50 @@ __device__ __forceinline__ uint32_t add3(uint32_t a, uint32_t b, uint32_t c) { r
         h = add3(t1, SHA_S0(a), maj(a, b, c));                                   \
     }
 
-__device__ __forceinline__ void sha_rounds_lds(uint32_t st[8], const uint32_t *row) {
-    // all 16 ds_read_b128 issued up front: one LDS latency per block, not sixteen
-    uint4 wv[16];
+__device__ __forceinline__ uint32_t lds_load_acquire(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_store_release(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ void load_w(uint4 (&w)[16], const uint32_t *row) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) wv[i] = *reinterpret_cast<const uint4 *>(row + 4 * i);
-    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
-#pragma unroll
-    for (int i = 0; i < 64; i += 8) {
-        const uint4 wa = wv[i / 4], wb = wv[i / 4 + 1];
-        SHA_RNDW(a, b, c, d, e, f, g, h, i + 0, wa.x);
-        SHA_RNDW(h, a, b, c, d, e, f, g, i + 1, wa.y);
-        SHA_RNDW(g, h, a, b, c, d, e, f, i + 2, wa.z);
-        SHA_RNDW(f, g, h, a, b, c, d, e, i + 3, wa.w);
-        SHA_RNDW(e, f, g, h, a, b, c, d, i + 4, wb.x);
-        SHA_RNDW(d, e, f, g, h, a, b, c, i + 5, wb.y);
-        SHA_RNDW(c, d, e, f, g, h, a, b, i + 6, wb.z);
-        SHA_RNDW(b, c, d, e, f, g, h, a, i + 7, wb.w);
+    for (int i = 0; i < 16; ++i) w[i] = *reinterpret_cast<const uint4 *>(row + 4 * i);
+}
+
+#define SHA_8RND(i, W)                                       \
+    {                                                        \
+        const uint4 wa = W[(i) / 4], wb = W[(i) / 4 + 1];    \
+        SHA_RNDW(a, b, c, d, e, f, g, h, (i) + 0, wa.x);     \
+        SHA_RNDW(h, a, b, c, d, e, f, g, (i) + 1, wa.y);     \
+        SHA_RNDW(g, h, a, b, c, d, e, f, (i) + 2, wa.z);     \
+        SHA_RNDW(f, g, h, a, b, c, d, e, (i) + 3, wa.w);     \
+        SHA_RNDW(e, f, g, h, a, b, c, d, (i) + 4, wb.x);     \
+        SHA_RNDW(d, e, f, g, h, a, b, c, (i) + 5, wb.y);     \
+        SHA_RNDW(c, d, e, f, g, h, a, b, (i) + 6, wb.z);     \
+        SHA_RNDW(b, c, d, e, f, g, h, a, (i) + 7, wb.w);     \
     }
+
+// 64 rounds on `cur`; half-way through, once the producer has published block
+// `knext`, the next block's schedule is read from LDS into `nxt`, so its LDS
+// latency hides under the remaining 32 rounds.
+__device__ __forceinline__ void sha_rounds_pf(uint32_t st[8], const uint4 (&cur)[16], uint4 (&nxt)[16],
+                                              const uint32_t *next_row, uint32_t knext, bool prefetch,
+                                              const uint32_t *ready) {
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+    SHA_8RND(0, cur);
+    SHA_8RND(8, cur);
+    SHA_8RND(16, cur);
+    SHA_8RND(24, cur);
+    if (prefetch) {
+        while (lds_load_acquire(ready) <= knext) __builtin_amdgcn_s_sleep(1);
+        load_w(nxt, next_row);
+    }
+    SHA_8RND(32, cur);
+    SHA_8RND(40, cur);
+    SHA_8RND(48, cur);
+    SHA_8RND(56, cur);
     st[0] += a; st[1] += b; st[2] += c; st[3] += d;
     st[4] += e; st[5] += f; st[6] += g; st[7] += h;
 }
@@ -106,17 +132,28 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return v;
 }
 
+#define PC_RING 4u  // LDS schedule slots: the producer runs up to 4 blocks ahead
+
+// diag (optional, nullptr in production): per workgroup {producer spin, producer
+// total, consumer spin, consumer total} in shader clocks (s_memtime).
 __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data, const uint64_t *__restrict__ abs,
                                                const DescRaw *__restrict__ desc, const uint64_t *__restrict__ total_p,
                                                uint64_t max_chunks, uint8_t *__restrict__ hash_base,
-                                               size_t stride) {
-    __shared__ __attribute__((aligned(16))) uint32_t sW[2][64 * PC_ROW];
+                                               size_t stride, unsigned long long *__restrict__ diag) {
+    unsigned long long t_start = diag ? __builtin_amdgcn_s_memtime() : 0ull, t_spin = 0;
+    __shared__ __attribute__((aligned(16))) uint32_t sW[PC_RING][64 * PC_ROW];
+    __shared__ uint32_t s_ready, s_done;  // blocks filled by the producer / consumed by the consumer
     const uint32_t lane = threadIdx.x & 63u;
     const bool producer = threadIdx.x < 64;
     const uint64_t g = (uint64_t)blockIdx.x * 64 + lane;
     uint64_t total = *total_p;
     if (total > max_chunks) total = max_chunks;
     if ((uint64_t)blockIdx.x * 64 >= total) return;  // whole workgroup idle (uniform)
+    if (threadIdx.x == 0) {
+        s_ready = 0;
+        s_done = 0;
+    }
+    __syncthreads();
     const bool valid = g < total;
     const uint64_t len = valid ? desc[g].length : 0;
     const uint64_t nb = len >> 6;
@@ -131,65 +168,91 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
         const uint32_t sel = (shift << 24) | ((shift + 1) << 16) | ((shift + 2) << 8) | (shift + 3);
         const uint64_t bits = len << 3;
         uint32_t dcur[17], dnx[17];
-        auto load_full = [&](uint32_t (&d)[17], uint64_t k) {
+        auto load_full = [&](uint32_t(&d)[17], uint64_t k) {
             const uint32_t *q = base + 16 * k;
 #pragma unroll
             for (int i = 0; i < 16; ++i) d[i] = q[i];
             d[16] = shift ? q[16] : 0u;
         };
-        auto fill = [&](uint32_t k, uint32_t *row) {  // block k of this lane's chunk into row
-            uint32_t w[16];
-            if (k < nb) {
+        if (nb > 0) load_full(dcur, 0);
+        if (nb > 1) load_full(dnx, 1);
+        for (uint32_t k = 0; k < NB; ++k) {
+            // wait for a free slot (wave-uniform spin on an LDS counter)
+            if (k - lds_load_acquire(&s_done) >= PC_RING) {
+                const unsigned long long t0 = diag ? __builtin_amdgcn_s_memtime() : 0ull;
+                while (k - lds_load_acquire(&s_done) >= PC_RING) __builtin_amdgcn_s_sleep(1);
+                if (diag) t_spin += __builtin_amdgcn_s_memtime() - t0;
+            }
+            if (k < nbt) {
+                uint32_t w[16];
+                if (k < nb) {
 #pragma unroll
-                for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_perm(dcur[i + 1], dcur[i], sel);
-            } else if (k == nb) {  // tail bytes, 0x80, zeros, [length]
-                const uint32_t *q = base + 16 * nb;
-                const uint8_t *endp = p + len;
-                uint32_t dw[17];
+                    for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_perm(dcur[i + 1], dcur[i], sel);
+                } else if (k == nb) {  // tail bytes, 0x80, zeros, [length]
+                    const uint32_t *q = base + 16 * nb;
+                    const uint8_t *endp = p + len;
+                    uint32_t dw[17];
 #pragma unroll
-                for (int i = 0; i < 17; ++i) dw[i] = (reinterpret_cast<const uint8_t *>(q + i) < endp) ? q[i] : 0u;
+                    for (int i = 0; i < 17; ++i)
+                        dw[i] = (reinterpret_cast<const uint8_t *>(q + i) < endp) ? q[i] : 0u;
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const uint32_t v = __builtin_amdgcn_perm(dw[i + 1], dw[i], sel);
-                    const int r = (int)rem - 4 * i;
-                    w[i] = r >= 4 ? v : (r < 0 ? 0u : ((r ? (v & (0xffffffffu << (32 - 8 * r))) : 0u) | (0x80u << (24 - 8 * r))));
-                }
-                if (rem < 56) {
+                    for (int i = 0; i < 16; ++i) {
+                        const uint32_t v = __builtin_amdgcn_perm(dw[i + 1], dw[i], sel);
+                        const int r = (int)rem - 4 * i;
+                        w[i] = r >= 4 ? v
+                                      : (r < 0 ? 0u
+                                               : ((r ? (v & (0xffffffffu << (32 - 8 * r))) : 0u) |
+                                                  (0x80u << (24 - 8 * r))));
+                    }
+                    if (rem < 56) {
+                        w[14] = (uint32_t)(bits >> 32);
+                        w[15] = (uint32_t)bits;
+                    }
+                } else {  // second padding block
+#pragma unroll
+                    for (int i = 0; i < 14; ++i) w[i] = 0u;
                     w[14] = (uint32_t)(bits >> 32);
                     w[15] = (uint32_t)bits;
                 }
-            } else {  // second padding block
-#pragma unroll
-                for (int i = 0; i < 14; ++i) w[i] = 0u;
-                w[14] = (uint32_t)(bits >> 32);
-                w[15] = (uint32_t)bits;
-            }
-            sha_schedule_store(w, row);
-        };
-        // dcur holds block k's words when fill(k) runs; dnx is the prefetched block k+1
-        if (nb > 0) load_full(dcur, 0);
-        if (nb > 1) load_full(dnx, 1);
-        if (0 < nbt) fill(0, &sW[0][lane * PC_ROW]);
-        __syncthreads();
-        for (uint32_t k = 0; k < NB; ++k) {
-            const uint32_t kn = k + 1;
-            if (kn < nbt) {
-                if (kn < nb) {
+                sha_schedule_store(w, &sW[k % PC_RING][lane * PC_ROW]);
+                if (k + 1 < nb) {  // advance the prefetch pipeline
 #pragma unroll
                     for (int i = 0; i < 17; ++i) dcur[i] = dnx[i];
-                    if (kn + 1 < nb) load_full(dnx, kn + 1);
+                    if (k + 2 < nb) load_full(dnx, k + 2);
                 }
-                fill(kn, &sW[kn & 1][lane * PC_ROW]);
             }
-            __syncthreads();
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's schedule writes landed
+            if (lane == 0) lds_store_release(&s_ready, k + 1);
+        }
+        if (diag && lane == 0) {
+            diag[4 * blockIdx.x + 0] = t_spin;
+            diag[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memtime() - t_start;
         }
     } else {
         uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
                           0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
-        __syncthreads();
-        for (uint32_t k = 0; k < NB; ++k) {
-            if (k < nbt) sha_rounds_lds(st, &sW[k & 1][lane * PC_ROW]);
-            __syncthreads();
+        uint4 wA[16], wB[16];
+        if (lds_load_acquire(&s_ready) == 0) {
+            const unsigned long long t0 = diag ? __builtin_amdgcn_s_memtime() : 0ull;
+            while (lds_load_acquire(&s_ready) == 0) __builtin_amdgcn_s_sleep(1);
+            if (diag) t_spin += __builtin_amdgcn_s_memtime() - t0;
+        }
+        load_w(wA, &sW[0][lane * PC_ROW]);
+        for (uint32_t k = 0; k < NB; k += 2) {
+            // block k from wA, block k+1's schedule prefetched into wB
+            if (k < nbt)
+                sha_rounds_pf(st, wA, wB, &sW[(k + 1) % PC_RING][lane * PC_ROW], k + 1, k + 1 < nbt, &s_ready);
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+            if (lane == 0) lds_store_release(&s_done, k + 1);
+            if (k + 1 >= NB) break;
+            if (k + 1 < nbt)
+                sha_rounds_pf(st, wB, wA, &sW[(k + 2) % PC_RING][lane * PC_ROW], k + 2, k + 2 < nbt, &s_ready);
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            if (lane == 0) lds_store_release(&s_done, k + 2);
+        }
+        if (diag && lane == 0) {
+            diag[4 * blockIdx.x + 2] = t_spin;
+            diag[4 * blockIdx.x + 3] = __builtin_amdgcn_s_memtime() - t_start;
         }
         if (valid) {
             uint4 *o = reinterpret_cast<uint4 *>(hash_base + g * stride);
@@ -201,11 +264,13 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
     }
 }
 
+unsigned long long *g_sha_diag = nullptr;  // set by cg_diag_sha_stats (diagnostics only)
+
 void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
                    uint64_t max_chunks, uint8_t *d_hash_base, size_t hash_stride, hipStream_t st) {
     if (max_chunks == 0) return;
     hipLaunchKernelGGL(k_sha256, dim3((uint32_t)((max_chunks + 63) / 64)), dim3(128), 0, st, d_data, d_abs,
-                       (const DescRaw *)d_desc, d_total, max_chunks, d_hash_base, hash_stride);
+                       (const DescRaw *)d_desc, d_total, max_chunks, d_hash_base, hash_stride, g_sha_diag);
 }
 
 }  // namespace cg

@@ -21,4 +21,11 @@ for blocks, threads in [(1, 64), (1, 128), (1, 256), (1, 512), (1, 1024), (4, 25
     clk = cyc[0::2].astype(float) / (rt / 100e6) / 1e9
     res[f"{blocks}x{threads}"] = {"cycles_per_round_med": float(np.median(c)), "max": float(c.max()),
                                   "clock_GHz": float(np.median(clk))}
+lib.cg_diag_sha_rounds_lds.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+for blocks in [1, 16, 256]:
+    it = 2000
+    cyc = np.zeros(2 * blocks, np.uint64)
+    lib.cg_diag_sha_rounds_lds(it, blocks, cyc.ctypes.data)
+    c = cyc[0::2].astype(float) / (it * 64)
+    res[f"lds_{blocks}x64"] = {"cycles_per_round_med": float(np.median(c)), "max": float(c.max())}
 print(json.dumps(res))
