@@ -131,7 +131,11 @@ extern "C" int cg_diag_sha_rounds(uint32_t iters, uint32_t blocks, uint32_t thre
 
 namespace cg {
 extern unsigned long long *g_sha_diag;
+extern uint32_t g_sha_mode;
 }
+// 0 = product; 1 = producer idle (consumer rounds on stale LDS schedules); 2 = consumer
+// also skips its LDS schedule reads.  Digests are garbage in modes 1 and 2.
+extern "C" void cg_diag_sha_mode(uint32_t mode) { cg::g_sha_mode = mode; }
 // Enable (n_wg > 0) / read back / disable (n_wg == 0) per-workgroup SHA producer and
 // consumer timing: out[4*wg + {0,1,2,3}] = producer spin, producer total, consumer
 // spin, consumer total (shader clocks).  Diagnostics only.

@@ -91,22 +91,35 @@ __device__ __forceinline__ void load_w(uint4 (&w)[16], const uint32_t *row) {
 // latency hides under the remaining 32 rounds.
 __device__ __forceinline__ void sha_rounds_pf(uint32_t st[8], const uint4 (&cur)[16], uint4 (&nxt)[16],
                                               const uint32_t *next_row, uint32_t knext, bool prefetch,
-                                              const uint32_t *ready) {
+                                              const uint32_t *ready, bool active) {
     uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+    // readiness probe issued now, consumed after 32 rounds: its LDS latency is hidden
+    const uint32_t r0 = __hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     SHA_8RND(0, cur);
     SHA_8RND(8, cur);
     SHA_8RND(16, cur);
     SHA_8RND(24, cur);
     if (prefetch) {
-        while (lds_load_acquire(ready) <= knext) __builtin_amdgcn_s_sleep(1);
+        if (__builtin_expect(r0 <= knext, 0))
+            while (lds_load_acquire(ready) <= knext) __builtin_amdgcn_s_sleep(1);
         load_w(nxt, next_row);
     }
     SHA_8RND(32, cur);
     SHA_8RND(40, cur);
     SHA_8RND(48, cur);
     SHA_8RND(56, cur);
-    st[0] += a; st[1] += b; st[2] += c; st[3] += d;
-    st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+    // lanes past their last block computed on stale words: keep their state (select,
+    // not a branch, so the round code always runs under a full exec mask; the empty asm
+    // stops the compiler from sinking the last rounds under an `active` branch)
+    asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e), "+v"(f), "+v"(g), "+v"(h));
+    st[0] = active ? st[0] + a : st[0];
+    st[1] = active ? st[1] + b : st[1];
+    st[2] = active ? st[2] + c : st[2];
+    st[3] = active ? st[3] + d : st[3];
+    st[4] = active ? st[4] + e : st[4];
+    st[5] = active ? st[5] + f : st[5];
+    st[6] = active ? st[6] + g : st[6];
+    st[7] = active ? st[7] + h : st[7];
 }
 
 // Expand w[0..15] into the full schedule and store all 64 words to `row` (LDS).
@@ -139,7 +152,8 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data, const uint64_t *__restrict__ abs,
                                                const DescRaw *__restrict__ desc, const uint64_t *__restrict__ total_p,
                                                uint64_t max_chunks, uint8_t *__restrict__ hash_base,
-                                               size_t stride, unsigned long long *__restrict__ diag) {
+                                               size_t stride, unsigned long long *__restrict__ diag,
+                                               uint32_t mode) {
     unsigned long long t_start = diag ? __builtin_amdgcn_s_memtime() : 0ull, t_spin = 0;
     __shared__ __attribute__((aligned(16))) uint32_t sW[PC_RING][64 * PC_ROW];
     __shared__ uint32_t s_ready, s_done;  // blocks filled by the producer / consumed by the consumer
@@ -159,7 +173,8 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
     const uint64_t nb = len >> 6;
     const uint32_t rem = (uint32_t)(len & 63u);
     const uint32_t nbt = valid ? (uint32_t)(nb + (rem < 56 ? 1 : 2)) : 0u;  // blocks incl. padding
-    const uint32_t NB = wave_max_u32(nbt);  // identical in both waves (same 64 chunks)
+    // identical in both waves (same 64 chunks); scalar, so the block loops are uniform
+    const uint32_t NB = __builtin_amdgcn_readfirstlane(wave_max_u32(nbt));
 
     if (producer) {
         const uint8_t *p = data + (valid ? abs[g] : 0);
@@ -167,27 +182,35 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
         const uint32_t *base = reinterpret_cast<const uint32_t *>(p - shift);
         const uint32_t sel = (shift << 24) | ((shift + 1) << 16) | ((shift + 2) << 8) | (shift + 3);
         const uint64_t bits = len << 3;
-        uint32_t dcur[17], dnx[17];
-        auto load_full = [&](uint32_t(&d)[17], uint64_t k) {
+        // One block buffer: block k+1's bytes are requested as soon as block k's words
+        // have been realigned out of it, so a whole schedule computation (~2,000
+        // cycles) covers their latency and the only loads in flight at the next
+        // realign are exactly the ones it needs (vmcnt(0) is then the precise wait).
+        uint32_t d[17];
+        auto load_full = [&](uint64_t k) {
             const uint32_t *q = base + 16 * k;
 #pragma unroll
             for (int i = 0; i < 16; ++i) d[i] = q[i];
-            d[16] = shift ? q[16] : 0u;
+            // dword 16 holds chunk bytes whenever shift != 0; for shift == 0 the realign
+            // ignores it, so re-read dword 15 (unconditional: keeps vmcnt tracking exact)
+            d[16] = q[shift ? 16 : 15];
         };
-        if (nb > 0) load_full(dcur, 0);
-        if (nb > 1) load_full(dnx, 1);
-        for (uint32_t k = 0; k < NB; ++k) {
+        auto produce = [&](uint32_t k) {
             // wait for a free slot (wave-uniform spin on an LDS counter)
-            if (k - lds_load_acquire(&s_done) >= PC_RING) {
+            if ((int)(k - lds_load_acquire(&s_done)) >= (int)PC_RING) {
                 const unsigned long long t0 = diag ? __builtin_amdgcn_s_memtime() : 0ull;
-                while (k - lds_load_acquire(&s_done) >= PC_RING) __builtin_amdgcn_s_sleep(1);
+                while ((int)(k - lds_load_acquire(&s_done)) >= (int)PC_RING) __builtin_amdgcn_s_sleep(1);
                 if (diag) t_spin += __builtin_amdgcn_s_memtime() - t0;
             }
             if (k < nbt) {
                 uint32_t w[16];
                 if (k < nb) {
 #pragma unroll
-                    for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_perm(dcur[i + 1], dcur[i], sel);
+                    for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_perm(d[i + 1], d[i], sel);
+                    // keep the realign ahead of the reload so the loads land in d's own
+                    // registers (no copies, no wait); the last full block re-reads itself
+                    __builtin_amdgcn_sched_barrier(0);
+                    load_full(k + 1 < nb ? k + 1 : k);
                 } else if (k == nb) {  // tail bytes, 0x80, zeros, [length]
                     const uint32_t *q = base + 16 * nb;
                     const uint8_t *endp = p + len;
@@ -215,14 +238,15 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
                     w[15] = (uint32_t)bits;
                 }
                 sha_schedule_store(w, &sW[k % PC_RING][lane * PC_ROW]);
-                if (k + 1 < nb) {  // advance the prefetch pipeline
-#pragma unroll
-                    for (int i = 0; i < 17; ++i) dcur[i] = dnx[i];
-                    if (k + 2 < nb) load_full(dnx, k + 2);
-                }
             }
             __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's schedule writes landed
             if (lane == 0) lds_store_release(&s_ready, k + 1);
+        };
+        if (mode == 1) {  // diag: no producer work, consumer rounds on stale schedules
+            if (lane == 0) lds_store_release(&s_ready, 0xffffffffu);
+        } else {
+            if (nb > 0) load_full(0);
+            for (uint32_t k = 0; k < NB; ++k) produce(k);
         }
         if (diag && lane == 0) {
             diag[4 * blockIdx.x + 0] = t_spin;
@@ -238,15 +262,18 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
             if (diag) t_spin += __builtin_amdgcn_s_memtime() - t0;
         }
         load_w(wA, &sW[0][lane * PC_ROW]);
+        // Every lane runs every block's rounds (lanes whose chunk is done work on stale
+        // words and keep their state by select): with part of the wave masked off, the
+        // dependent round chain ran up to 1.7x slower per round on gfx950.
         for (uint32_t k = 0; k < NB; k += 2) {
             // block k from wA, block k+1's schedule prefetched into wB
-            if (k < nbt)
-                sha_rounds_pf(st, wA, wB, &sW[(k + 1) % PC_RING][lane * PC_ROW], k + 1, k + 1 < nbt, &s_ready);
+            sha_rounds_pf(st, wA, wB, &sW[(k + 1) % PC_RING][lane * PC_ROW], k + 1, k + 1 < NB && mode != 2,
+                          &s_ready, k < nbt);
             __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
             if (lane == 0) lds_store_release(&s_done, k + 1);
             if (k + 1 >= NB) break;
-            if (k + 1 < nbt)
-                sha_rounds_pf(st, wB, wA, &sW[(k + 2) % PC_RING][lane * PC_ROW], k + 2, k + 2 < nbt, &s_ready);
+            sha_rounds_pf(st, wB, wA, &sW[(k + 2) % PC_RING][lane * PC_ROW], k + 2, k + 2 < NB && mode != 2,
+                          &s_ready, k + 1 < nbt);
             __builtin_amdgcn_s_waitcnt(0xc07f);
             if (lane == 0) lds_store_release(&s_done, k + 2);
         }
@@ -265,12 +292,19 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
 }
 
 unsigned long long *g_sha_diag = nullptr;  // set by cg_diag_sha_stats (diagnostics only)
+uint32_t g_sha_mode = 0;                    // set by cg_diag_sha_mode (diagnostics only; 0 = product)
 
 void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
                    uint64_t max_chunks, uint8_t *d_hash_base, size_t hash_stride, hipStream_t st) {
     if (max_chunks == 0) return;
-    hipLaunchKernelGGL(k_sha256, dim3((uint32_t)((max_chunks + 63) / 64)), dim3(128), 0, st, d_data, d_abs,
-                       (const DescRaw *)d_desc, d_total, max_chunks, d_hash_base, hash_stride, g_sha_diag);
+    const uint32_t nwg = (uint32_t)((max_chunks + 63) / 64);
+    // Latency-bound batches (no more workgroups than CUs): pad the LDS request past half
+    // a CU's 160 KiB so no two workgroups share a CU, and a consumer wave never shares a
+    // SIMD with another workgroup's wave (which costs it 20-90 % per round).
+    const size_t pad = nwg <= 256 ? 16384 : 0;
+    hipLaunchKernelGGL(k_sha256, dim3(nwg), dim3(128), pad, st, d_data, d_abs,
+                       (const DescRaw *)d_desc, d_total, max_chunks, d_hash_base, hash_stride, g_sha_diag,
+                       g_sha_mode);
 }
 
 }  // namespace cg

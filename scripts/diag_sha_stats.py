@@ -12,9 +12,18 @@ from chunker_amd.nar import synth_nars  # noqa: E402
 
 lib = ca.lib
 lib.cg_diag_sha_stats.argtypes = [ctypes.c_uint32, ctypes.c_void_p]
+lib.cg_diag_sha_mode.argtypes = [ctypes.c_uint32]
 res = {}
-for name, n, size, params in [("c2", 256, 4 << 20, (256 << 10, 1 << 20, 4 << 20)),
-                              ("c4_quarter", 4, 1 << 30, (64 << 10, 256 << 10, 1 << 20))]:
+runs = [("c2", 256, 4 << 20, (256 << 10, 1 << 20, 4 << 20), 0),
+        ("c2_mode1", 256, 4 << 20, (256 << 10, 1 << 20, 4 << 20), 1),
+        ("c2_mode2", 256, 4 << 20, (256 << 10, 1 << 20, 4 << 20), 2),
+        ("c2_again", 256, 4 << 20, (256 << 10, 1 << 20, 4 << 20), 0),
+        ("c4_quarter", 4, 1 << 30, (64 << 10, 256 << 10, 1 << 20), 0)]
+if len(sys.argv) > 1:
+    runs = [r for r in runs if r[0] in sys.argv[1:]]
+for name, n, size, params, mode in runs:
+    print("run", name, flush=True, file=sys.stderr)
+    lib.cg_diag_sha_mode(mode)
     host, offs = synth_nars(np.full(n, size, np.uint64))
     d = torch.from_numpy(host).cuda()
     cap = ca.chunking.batch_capacity(offs, params[0])
@@ -32,10 +41,14 @@ for name, n, size, params in [("c2", 256, 4 << 20, (256 << 10, 1 << 20, 4 << 20)
     used = int((int(first[-1]) + 63) // 64)
     b = buf.reshape(-1, 4)[:used].astype(float)
     worst = int(np.argmax(b[:, 3]))
-    res[name] = {"digest_ms": st[4], "wgs": used,
+    lens = np.frombuffer(out.cpu().numpy().tobytes()[:48 * int(first[-1])], dtype=np.uint64).reshape(-1, 6)[:, 1]
+    max_blocks = int(lens.max()) // 64 + 1
+    res[name] = {"digest_ms": st[4], "wgs": used, "mode": mode,
+                 "worst_cycles_per_round": b[worst, 3] / (max_blocks * 64),
                  "worst_wg": {"prod_spin": b[worst, 0], "prod_total": b[worst, 1], "cons_spin": b[worst, 2],
                               "cons_total": b[worst, 3]},
                  "median_cons_spin_frac": float(np.median(b[:, 2] / np.maximum(b[:, 3], 1))),
                  "median_prod_spin_frac": float(np.median(b[:, 0] / np.maximum(b[:, 1], 1)))}
     del d, out
-print(json.dumps(res))
+lib.cg_diag_sha_mode(0)
+print(json.dumps(res, indent=1))
