@@ -47,16 +47,19 @@ __device__ __forceinline__ uint32_t add3(uint32_t a, uint32_t b, uint32_t c) { r
 // chunks (one chunk per lane):
 //   wave 0 (producer): loads the block, realigns + byte-swaps it (v_perm_b32),
 //          builds the final padded block(s), expands the 64-word message schedule
-//          and writes it to an LDS row per lane (double-buffered);
-//   wave 1 (consumer): runs only the 64 rounds (14 VALU each) reading W from LDS.
-// One barrier per block hands a buffer over.  The consumer issues ~900 VALU per
-// block instead of ~1,400.
+//          (W[t] + K[t]) into a ring of PC_RING LDS slots (one row per lane);
+//   wave 1 (consumer): runs only the 64 rounds (14 VALU each), reading the next
+//          block's words from LDS into registers half-way through the current one.
+// Two LDS counters (s_ready, s_done) with workgroup-scope acquire/release hand the
+// slots over; no barrier per block.  The consumer issues ~900 VALU per block instead
+// of ~1,400.
 // ---------------------------------------------------------------------------
 #define PC_ROW 68u  // 64 words + 4 pad per lane: 16 consecutive lanes' 16-B accesses hit distinct banks
 
+// wv = W[i] + K[i], pre-added by the producer (no constant operand in the round)
 #define SHA_RNDW(a, b, c, d, e, f, g, h, i, wv)                                  \
     {                                                                            \
-        const uint32_t t1 = add3(add3(h, (wv), SHA_K[i]), SHA_S1(e), ch(e, f, g)); \
+        const uint32_t t1 = add3(h, (wv), ch(e, f, g)) + SHA_S1(e);             \
         d += t1;                                                                 \
         h = add3(t1, SHA_S0(a), maj(a, b, c));                                   \
     }
@@ -122,11 +125,13 @@ __device__ __forceinline__ void sha_rounds_pf(uint32_t st[8], const uint4 (&cur)
     st[7] = active ? st[7] + h : st[7];
 }
 
-// Expand w[0..15] into the full schedule and store all 64 words to `row` (LDS).
+// Expand w[0..15] into the full schedule and store W[t] + K[t] for all 64 words to
+// `row` (LDS): the consumer's round then has no constant operand to materialise.
 __device__ __forceinline__ void sha_schedule_store(uint32_t w[16], uint32_t *row) {
 #pragma unroll
     for (int i = 0; i < 16; i += 4)
-        *reinterpret_cast<uint4 *>(row + i) = make_uint4(w[i], w[i + 1], w[i + 2], w[i + 3]);
+        *reinterpret_cast<uint4 *>(row + i) = make_uint4(w[i] + SHA_K[i], w[i + 1] + SHA_K[i + 1],
+                                                         w[i + 2] + SHA_K[i + 2], w[i + 3] + SHA_K[i + 3]);
 #pragma unroll
     for (int t = 16; t < 64; t += 4) {
 #pragma unroll
@@ -135,7 +140,8 @@ __device__ __forceinline__ void sha_schedule_store(uint32_t w[16], uint32_t *row
             w[u & 15] = add3(w[u & 15], SHA_s0(w[(u - 15) & 15]), w[(u - 7) & 15]) + SHA_s1(w[(u - 2) & 15]);
         }
         *reinterpret_cast<uint4 *>(row + t) =
-            make_uint4(w[t & 15], w[(t + 1) & 15], w[(t + 2) & 15], w[(t + 3) & 15]);
+            make_uint4(w[t & 15] + SHA_K[t], w[(t + 1) & 15] + SHA_K[t + 1], w[(t + 2) & 15] + SHA_K[t + 2],
+                       w[(t + 3) & 15] + SHA_K[t + 3]);
     }
 }
 
