@@ -94,32 +94,32 @@ def main():
 
     for _ in range(args.warmup):
         first = step()
+    # Per-stage device times: HIP events the library records on the stream the kernels
+    # run on, live inside the timed region (each step already ends in a stream sync
+    # for the NAR->chunk index, so reading them adds only host bookkeeping).
+    ca.lib.cg_set_profiling(1)
+    stage = np.zeros((max(args.steps, 1), 5))
+    buf = (np.ctypeslib.ctypes.c_double * 5)()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for k in range(args.steps):
         first = step()
+        ca.lib.cg_last_stage_times(buf, 5)
+        stage[k] = list(buf)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    ca.lib.cg_set_profiling(0)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     n_chunks = int(first[-1])
-
-    # per-stage device times (HIP events on the kernels' stream), separate pass
-    ca.lib.cg_set_profiling(1)
-    stage = np.zeros((max(args.steps, 1), 5))
-    for k in range(max(args.steps, 1)):
-        step()
-        buf = (np.ctypeslib.ctypes.c_double * 5)()
-        ca.lib.cg_last_stage_times(buf, 5)
-        stage[k] = list(buf)
-    ca.lib.cg_set_profiling(0)
-    stages_ms = dict(zip(["scan", "compact", "walk", "assemble", "digest"], np.median(stage, axis=0).round(4)))
+    stages_ms = dict(zip(["scan", "compact", "walk", "assemble", "digest"],
+                         stage[: max(args.steps, 1)].mean(axis=0).round(4)))
 
     # parity spot check on the last step (rank 0): descriptors cover every NAR exactly
     descs = d_out[: n_chunks * 48].cpu().numpy().view(ca.DESC_DTYPE)
@@ -140,10 +140,18 @@ def main():
         "unit": "GB/s",
         "frac": round(total_bytes / (dig_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
         "traffic": None,
-        "note": "digest stage: algorithmic bytes = every NAR byte once; scan stage reported separately",
+        "note": "digest stage: algorithmic bytes = every NAR byte once, / mean digest-stage duration over the "
+                "timed steps; scan stage reported separately",
         "scan_kernel": {"kernel": "k_scan", "achieved": round(total_bytes / (scan_ms * 1e-3) / 1e9, 2),
-                        "frac": round(total_bytes / (scan_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+                        "frac": round(total_bytes / (scan_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                        "traffic": None},
     }
+    dig_kernels = ["k_sha256"] if algo == 1 else ["k_b3_groups", "k_b3_top"]
+    traffic, src = pmc_traffic(args.config, dig_kernels)
+    if traffic is not None:
+        roofline["traffic"] = traffic
+        roofline["scan_kernel"]["traffic"] = pmc_traffic(args.config, ["k_scan"])[0]
+        roofline["traffic_source"] = src
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
@@ -174,6 +182,24 @@ def main():
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
+
+
+def pmc_traffic(config, kernels):
+    """HBM bytes per launch of `kernels` from the committed rocprofv3 --pmc summary for
+    this config (profiles/*pmc_<config>.json, written by scripts/pmc_summary.py from
+    scripts/gpu_pmc.sh passes): FETCH_SIZE x 2 (gfx950 correction, MI355X_MICROARCH.md
+    §HBM) + WRITE_SIZE.  (None, None) when no summary has been committed."""
+    files = sorted(ROOT.glob(f"profiles/*pmc_{config}.json"))
+    if not files:
+        return None, None
+    rows = json.loads(files[-1].read_text())
+    total, hit = 0.0, False
+    for name, row in rows.items():
+        base = name.split("::")[-1].split("<")[0]
+        if base in kernels and "fetch_bytes_x2" in row:
+            total += row["fetch_bytes_x2"] + row.get("write_bytes", 0.0)
+            hit = True
+    return (round(total), str(files[-1].relative_to(ROOT))) if hit else (None, None)
 
 
 def cpu_baseline(host, offs, params, algo, sample_nars):

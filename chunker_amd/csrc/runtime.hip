@@ -310,9 +310,9 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
     }
 
     const bool prof = g_profiling.load() != 0;
-    if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_START], st));
     HIP_TRY(hipMemcpyAsync(ws->nar_off.p, s_off, (n_nars + 1) * 8, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(ws->cap_base.p, s_cap, (n_nars + 1) * 8, hipMemcpyHostToDevice, st));
+    if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_START], st));  // scan stage = the scan kernel alone
 
     cg::launch_scan(d_data, total_len, ws->gear.as<uint64_t>(), P.mask_s, P.mask_l, slots,
                     ws->seg_count.as<uint32_t>(), ws->seg_cand.as<uint32_t>(), nseg, st);
