@@ -124,7 +124,7 @@ struct Workspace {
     hipStream_t stream = nullptr;
     uint64_t gear_epoch = 0;
     DevBuf gear, seg_count, seg_cand, eoff, scan_tmp, entries, nar_off, cap_base, wchunk, nar_nchunks, nar_first,
-        chunk_abs, b3_gcount, b3_gbase, b3_gcv, in, out, span_off, span_len;
+        chunk_abs, b3_gcount, b3_gbase, b3_gcv, in, out, span_off, span_len, order;
     PinBuf stage;
     hipEvent_t ev[EV_N] = {};
     int init(int dev) {
@@ -334,8 +334,9 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
     const uint64_t *d_total = ws->nar_first.as<uint64_t>() + n_nars;
     uint8_t *hash_base = reinterpret_cast<uint8_t *>(d_out) + offsetof(cg_desc, hash);
     if (algo == CG_SHA256) {
-        cg::launch_sha256(d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, hash_base,
-                          sizeof(cg_desc), st);
+        if ((rc = ws->order.ensure(cg::sha256_order_tmp_elems(chunk_bound) * 4, "order"))) return rc;
+        cg::launch_sha256(d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, o.max,
+                          ws->order.as<uint32_t>(), hash_base, sizeof(cg_desc), st);
     } else {
         cg::launch_blake3(d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, total_len, hash_base,
                           sizeof(cg_desc), nullptr, ws->b3_gbase.as<uint64_t>(), ws->b3_gcount.as<uint32_t>(),
@@ -402,7 +403,10 @@ int hash_spans(Workspace *ws, const uint8_t *d_data, const uint64_t *d_offsets, 
     cg::launch_spans_to_desc(d_offsets, d_lengths, n, ws->chunk_abs.as<uint64_t>(), ws->out.p, d_total, st);
     uint8_t *hb = ws->out.as<uint8_t>() + offsetof(cg_desc, hash);
     if (algo == CG_SHA256) {
-        cg::launch_sha256(d_data, ws->chunk_abs.as<uint64_t>(), ws->out.p, d_total, n, hb, sizeof(cg_desc), st);
+        // spans are not bounded by a max_size: bucket for the ABI's 16 MiB span cap
+        if ((rc = ws->order.ensure(cg::sha256_order_tmp_elems(n) * 4, "order"))) return rc;
+        cg::launch_sha256(d_data, ws->chunk_abs.as<uint64_t>(), ws->out.p, d_total, n, MAXIMUM_MAX,
+                          ws->order.as<uint32_t>(), hb, sizeof(cg_desc), st);
     } else {
         // group-grid bound without reading lengths back: spans are capped at 16 MiB each
         const uint64_t tb = (uint64_t)n * MAXIMUM_MAX;

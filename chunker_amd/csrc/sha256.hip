@@ -157,9 +157,9 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 // total, consumer spin, consumer total} in shader clocks (s_memtime).
 __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data, const uint64_t *__restrict__ abs,
                                                const DescRaw *__restrict__ desc, const uint64_t *__restrict__ total_p,
-                                               uint64_t max_chunks, uint8_t *__restrict__ hash_base,
-                                               size_t stride, unsigned long long *__restrict__ diag,
-                                               uint32_t mode) {
+                                               uint64_t max_chunks, const uint32_t *__restrict__ order,
+                                               uint8_t *__restrict__ hash_base, size_t stride,
+                                               unsigned long long *__restrict__ diag, uint32_t mode) {
     unsigned long long t_start = diag ? __builtin_amdgcn_s_memtime() : 0ull, t_spin = 0;
     __shared__ __attribute__((aligned(16))) uint32_t sW[PC_RING][64 * PC_ROW];
     __shared__ uint32_t s_ready, s_done;  // blocks filled by the producer / consumed by the consumer
@@ -175,7 +175,10 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
     }
     __syncthreads();
     const bool valid = g < total;
-    const uint64_t len = valid ? desc[g].length : 0;
+    // lane -> chunk through the length order (longest first, see k_len_hist): the 64
+    // chunks of a wave have nearly equal block counts and the longest start first
+    const uint64_t ci = valid ? (order ? (uint64_t)order[g] : g) : 0;
+    const uint64_t len = valid ? desc[ci].length : 0;
     const uint64_t nb = len >> 6;
     const uint32_t rem = (uint32_t)(len & 63u);
     const uint32_t nbt = valid ? (uint32_t)(nb + (rem < 56 ? 1 : 2)) : 0u;  // blocks incl. padding
@@ -183,7 +186,7 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
     const uint32_t NB = __builtin_amdgcn_readfirstlane(wave_max_u32(nbt));
 
     if (producer) {
-        const uint8_t *p = data + (valid ? abs[g] : 0);
+        const uint8_t *p = data + (valid ? abs[ci] : 0);
         const uint32_t shift = (uint32_t)((uintptr_t)p & 3u);
         const uint32_t *base = reinterpret_cast<const uint32_t *>(p - shift);
         const uint32_t sel = (shift << 24) | ((shift + 1) << 16) | ((shift + 2) << 8) | (shift + 3);
@@ -288,7 +291,7 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
             diag[4 * blockIdx.x + 3] = __builtin_amdgcn_s_memtime() - t_start;
         }
         if (valid) {
-            uint4 *o = reinterpret_cast<uint4 *>(hash_base + g * stride);
+            uint4 *o = reinterpret_cast<uint4 *>(hash_base + ci * stride);
             o[0] = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]), __builtin_bswap32(st[2]),
                               __builtin_bswap32(st[3]));
             o[1] = make_uint4(__builtin_bswap32(st[4]), __builtin_bswap32(st[5]), __builtin_bswap32(st[6]),
@@ -297,19 +300,107 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
     }
 }
 
+// ---------------------------------------------------------------------------
+// Length order.  A wave lives as long as its longest chunk, and a batch's digest
+// stage as long as its longest chunk, so lanes are handed chunks in descending
+// block count: a counting sort on SHA_NBKT buckets of (blocks >> shift), each
+// workgroup aggregating in LDS before touching the global counters.  The order
+// inside a bucket is arbitrary (atomics); digests land at their chunk's own index,
+// so results do not depend on it.
+// ---------------------------------------------------------------------------
+#define SHA_NBKT 1024u
+
+__device__ __forceinline__ uint32_t len_bucket(uint64_t len, uint32_t shift) {
+    const uint64_t nb = (len + 72) >> 6;  // blocks including padding
+    const uint64_t b = nb >> shift;
+    return SHA_NBKT - 1u - (uint32_t)(b < SHA_NBKT - 1 ? b : SHA_NBKT - 1);  // descending
+}
+
+__global__ __launch_bounds__(256) void k_len_hist(const DescRaw *__restrict__ desc, const uint64_t *__restrict__ total_p,
+                                                 uint64_t max_chunks, uint32_t shift, uint32_t *__restrict__ bkt) {
+    __shared__ uint32_t h[SHA_NBKT];
+    for (uint32_t i = threadIdx.x; i < SHA_NBKT; i += 256) h[i] = 0;
+    __syncthreads();
+    uint64_t total = *total_p;
+    if (total > max_chunks) total = max_chunks;
+    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (g < total) atomicAdd(&h[len_bucket(desc[g].length, shift)], 1u);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < SHA_NBKT; i += 256)
+        if (h[i]) atomicAdd(&bkt[i], h[i]);
+}
+
+// one workgroup: bkt[i] <- exclusive prefix sum of the bucket counts
+__global__ __launch_bounds__(SHA_NBKT) void k_len_base(uint32_t *__restrict__ bkt) {
+    __shared__ uint32_t wsum[SHA_NBKT / 64];
+    const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    const uint32_t v = bkt[t];
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+        if ((int)lane >= d) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t off = 0;
+    for (uint32_t k = 0; k < w; ++k) off += wsum[k];
+    bkt[t] = off + x - v;
+}
+
+__global__ __launch_bounds__(256) void k_len_scatter(const DescRaw *__restrict__ desc,
+                                                    const uint64_t *__restrict__ total_p, uint64_t max_chunks,
+                                                    uint32_t shift, uint32_t *__restrict__ bkt,
+                                                    uint32_t *__restrict__ order) {
+    __shared__ uint32_t h[SHA_NBKT];
+    __shared__ uint32_t base[SHA_NBKT];
+    for (uint32_t i = threadIdx.x; i < SHA_NBKT; i += 256) h[i] = 0;
+    __syncthreads();
+    uint64_t total = *total_p;
+    if (total > max_chunks) total = max_chunks;
+    const uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    uint32_t b = 0, r = 0;
+    if (g < total) {
+        b = len_bucket(desc[g].length, shift);
+        r = atomicAdd(&h[b], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < SHA_NBKT; i += 256)
+        if (h[i]) base[i] = atomicAdd(&bkt[i], h[i]);
+    __syncthreads();
+    if (g < total) order[base[b] + r] = (uint32_t)g;
+}
+
+size_t sha256_order_tmp_elems(uint64_t max_chunks) { return max_chunks + SHA_NBKT + 64; }
+
 unsigned long long *g_sha_diag = nullptr;  // set by cg_diag_sha_stats (diagnostics only)
 uint32_t g_sha_mode = 0;                    // set by cg_diag_sha_mode (diagnostics only; 0 = product)
 
 void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
-                   uint64_t max_chunks, uint8_t *d_hash_base, size_t hash_stride, hipStream_t st) {
+                   uint64_t max_chunks, uint64_t max_len, uint32_t *d_order_tmp, uint8_t *d_hash_base,
+                   size_t hash_stride, hipStream_t st) {
     if (max_chunks == 0) return;
     const uint32_t nwg = (uint32_t)((max_chunks + 63) / 64);
+    const uint32_t *order = nullptr;
+    if (d_order_tmp && nwg > 1) {  // one workgroup has nothing to balance
+        uint32_t shift = 0;
+        while ((((max_len + 72) >> 6) >> shift) >= SHA_NBKT - 1) ++shift;
+        uint32_t *bkt = d_order_tmp, *ord = d_order_tmp + SHA_NBKT;
+        const uint32_t nb = (uint32_t)((max_chunks + 255) / 256);
+        (void)hipMemsetAsync(bkt, 0, SHA_NBKT * sizeof(uint32_t), st);
+        hipLaunchKernelGGL(k_len_hist, dim3(nb), dim3(256), 0, st, (const DescRaw *)d_desc, d_total, max_chunks,
+                           shift, bkt);
+        hipLaunchKernelGGL(k_len_base, dim3(1), dim3(SHA_NBKT), 0, st, bkt);
+        hipLaunchKernelGGL(k_len_scatter, dim3(nb), dim3(256), 0, st, (const DescRaw *)d_desc, d_total,
+                           max_chunks, shift, bkt, ord);
+        order = ord;
+    }
     // Latency-bound batches (no more workgroups than CUs): pad the LDS request past half
     // a CU's 160 KiB so no two workgroups share a CU, and a consumer wave never shares a
     // SIMD with another workgroup's wave (which costs it 20-90 % per round).
     const size_t pad = nwg <= 256 ? 16384 : 0;
     hipLaunchKernelGGL(k_sha256, dim3(nwg), dim3(128), pad, st, d_data, d_abs,
-                       (const DescRaw *)d_desc, d_total, max_chunks, d_hash_base, hash_stride, g_sha_diag,
+                       (const DescRaw *)d_desc, d_total, max_chunks, order, d_hash_base, hash_stride, g_sha_diag,
                        g_sha_mode);
 }
 
