@@ -136,6 +136,10 @@ extern uint32_t g_sha_mode;
 // 0 = product; 1 = producer idle (consumer rounds on stale LDS schedules); 2 = consumer
 // also skips its LDS schedule reads.  Digests are garbage in modes 1 and 2.
 extern "C" void cg_diag_sha_mode(uint32_t mode) { cg::g_sha_mode = mode; }
+namespace cg {
+extern uint32_t g_scan_diag;
+}
+extern "C" void cg_diag_scan_mode(uint32_t mode) { cg::g_scan_diag = mode; }
 // Enable (n_wg > 0) / read back / disable (n_wg == 0) per-workgroup SHA producer and
 // consumer timing: out[4*wg + {0,1,2,3}] = producer spin, producer total, consumer
 // spin, consumer total (shader clocks).  Diagnostics only.
@@ -158,4 +162,147 @@ extern "C" int cg_diag_sha_stats(uint32_t n_wg, unsigned long long *out) {
     }
     (void)hipDeviceSynchronize();
     return hipMemcpy(out, buf, (size_t)n_wg * 32, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 2;
+}
+
+// ---------------------------------------------------------------------------
+// HBM read-pattern microbenchmark (diagnostics only): 512 x 512-thread workgroups,
+// each wave owns a contiguous 256 KiB region read in 64 rounds of 4 KiB; in a round
+// the wave reads 4096/L runs of L contiguous bytes from 4096/L different 4 KiB
+// segments (L = 64 is the scan's quad-cooperative pattern, L = 4096 fully
+// contiguous).  Two rounds are kept in flight.
+// ---------------------------------------------------------------------------
+namespace cg {
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+template <int DEPTH, bool NT>
+__global__ __launch_bounds__(512) void k_diag_read(const uint8_t *__restrict__ data, uint32_t run_log2,
+                                                   uint32_t *__restrict__ out) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t wave = (uint64_t)blockIdx.x * 8 + (threadIdx.x >> 6);
+    const uint8_t *region = data + wave * (256u << 10);
+    const uint32_t L = 1u << run_log2, k = 4096u >> run_log2, groups = 64u / k;
+    auto addr = [&](uint32_t r, uint32_t i) {
+        r = r < 64 ? r : 63;
+        const uint32_t g = r % groups, off = (r / groups) * L;
+        const uint32_t b = i * 1024u + lane * 16u, run = b >> run_log2, within = b & (L - 1u);
+        return reinterpret_cast<const u32x4 *>(region + (uint64_t)(g * k + run) * 4096u + off + within);
+    };
+    auto ld = [&](const u32x4 *p) { return NT ? __builtin_nontemporal_load(p) : *p; };
+    u32x4 buf[DEPTH + 1][4];
+    uint32_t acc = 0;
+#pragma unroll
+    for (int d = 0; d < DEPTH; ++d)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) buf[d][i] = ld(addr(d, i));
+#pragma unroll 1
+    for (uint32_t r = 0; r < 64; r += DEPTH + 1) {
+#pragma unroll
+        for (int u = 0; u < DEPTH + 1; ++u) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) buf[(u + DEPTH) % (DEPTH + 1)][i] = ld(addr(r + u + DEPTH, i));
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc ^= buf[u][i].x ^ buf[u][i].y ^ buf[u][i].z ^ buf[u][i].w;
+        }
+    }
+    out[blockIdx.x * 512 + threadIdx.x] = acc;
+}
+}  // namespace cg
+
+extern "C" float cg_diag_read_pattern(const uint8_t *d_data, uint32_t run_log2, uint32_t *d_out) {
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    // run_log2 bits 0-7: run length; bit 8: nt loads; bits 12-15: in-flight depth (2 or 4)
+    const bool nt = (run_log2 >> 8) & 1u;
+    const uint32_t depth = (run_log2 >> 12) & 15u;
+    auto k = depth == 4 ? (nt ? cg::k_diag_read<4, true> : cg::k_diag_read<4, false>)
+                        : (nt ? cg::k_diag_read<2, true> : cg::k_diag_read<2, false>);
+    run_log2 &= 0xffu;
+    hipLaunchKernelGGL(k, dim3(512), dim3(512), 0, 0, d_data, run_log2, d_out);
+    (void)hipEventRecord(a, 0);
+    hipLaunchKernelGGL(k, dim3(512), dim3(512), 0, 0, d_data, run_log2, d_out);
+    (void)hipEventRecord(b, 0);
+    (void)hipEventSynchronize(b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    return ms;
+}
+
+// ---------------------------------------------------------------------------
+// Instruction issue-cost microbenchmark (diagnostics only): each wave runs `iters`
+// x 16 instructions of one kind over 8 independent register chains (inline asm, so
+// the compiler cannot rewrite them); cycles per instruction per wave via s_memtime.
+// kind: 0 v_add_u32, 1 v_lshl_add_u64, 2 v_perm_b32, 3 v_add_co_u32+v_addc_co_u32
+// pair (counted as 2), 4 v_alignbit_b32, 5 v_bitop3_b32, 6 v_lshlrev_b64,
+// 7 v_mov_b32_dpp quad_perm, 8 v_add3_u32, 9 v_cndmask_b32, 10 dependent v_lshl_add_u64
+// chain (one chain), 11 dependent v_add_u32 chain (one chain).
+// ---------------------------------------------------------------------------
+namespace cg {
+template <int KIND>
+__device__ __forceinline__ void op16(uint32_t (&r)[16], uint64_t (&q)[8]) {
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            if constexpr (KIND == 0) asm volatile("v_add_u32 %0, %0, %1" : "+v"(r[c]) : "v"(r[c + 8]));
+            if constexpr (KIND == 1) asm volatile("v_lshl_add_u64 %0, %0, 1, %0" : "+v"(q[c]));
+            if constexpr (KIND == 2) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(r[c]) : "v"(r[c + 8]), "s"(0x0c0c0001u));
+            if constexpr (KIND == 3) {
+                if (c & 1) continue;
+                asm volatile("v_add_co_u32 %0, vcc, %0, %1\n\tv_addc_co_u32 %2, vcc, %2, %3, vcc"
+                             : "+v"(r[c]), "+v"(r[c + 1]) : "v"(r[c + 8]), "v"(r[c + 9]) : "vcc");
+            }
+            if constexpr (KIND == 4) asm volatile("v_alignbit_b32 %0, %0, %0, 7" : "+v"(r[c]));
+            if constexpr (KIND == 5) asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x96" : "+v"(r[c]) : "v"(r[c + 8]), "v"(r[(c + 9) & 15]));
+            if constexpr (KIND == 6) asm volatile("v_lshlrev_b64 %0, 1, %0" : "+v"(q[c]));
+            if constexpr (KIND == 7) asm volatile("v_mov_b32_dpp %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "=v"(r[c]) : "v"(r[c + 8]));
+            if constexpr (KIND == 8) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(r[c]) : "v"(r[c + 8]), "v"(r[(c + 9) & 15]));
+            if constexpr (KIND == 9) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(r[c]) : "v"(r[c + 8]));
+            if constexpr (KIND == 10) asm volatile("v_lshl_add_u64 %0, %0, 1, %1" : "+v"(q[0]) : "v"(q[1 + (c & 1)]));
+            if constexpr (KIND == 11) asm volatile("v_add_u32 %0, %0, %1" : "+v"(r[0]) : "v"(r[c + 8]));
+        }
+    }
+}
+
+template <int KIND>
+__global__ void k_diag_ops(uint32_t iters, uint32_t *out, unsigned long long *cycles) {
+    uint32_t r[16];
+    uint64_t q[8];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r[i] = threadIdx.x * 16 + i;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q[i] = threadIdx.x * 8ull + i;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    for (uint32_t it = 0; it < iters; ++it) op16<KIND>(r, q);
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    uint32_t x = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x ^= r[i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x ^= (uint32_t)q[i] ^ (uint32_t)(q[i] >> 32);
+    out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+    if ((threadIdx.x & 63) == 0) cycles[blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)] = t1 - t0;
+}
+}  // namespace cg
+
+// cycles per wave for `iters` x 16 instructions of `kind`; one workgroup of `threads`
+extern "C" int cg_diag_ops(int kind, uint32_t iters, uint32_t threads, unsigned long long *h_cycles) {
+    const uint32_t waves = threads / 64;
+    uint32_t *d_out = nullptr;
+    unsigned long long *d_c = nullptr;
+    if (hipMalloc(&d_out, threads * 4) != hipSuccess) return 2;
+    if (hipMalloc(&d_c, waves * 8) != hipSuccess) return 2;
+    void (*ks[12])(uint32_t, uint32_t *, unsigned long long *) = {
+        cg::k_diag_ops<0>, cg::k_diag_ops<1>, cg::k_diag_ops<2>, cg::k_diag_ops<3>, cg::k_diag_ops<4>,  cg::k_diag_ops<5>,
+        cg::k_diag_ops<6>, cg::k_diag_ops<7>, cg::k_diag_ops<8>, cg::k_diag_ops<9>, cg::k_diag_ops<10>, cg::k_diag_ops<11>};
+    if (kind < 0 || kind > 11) return 1;
+    hipLaunchKernelGGL(ks[kind], dim3(1), dim3(threads), 0, 0, iters, d_out, d_c);
+    hipLaunchKernelGGL(ks[kind], dim3(1), dim3(threads), 0, 0, iters, d_out, d_c);
+    (void)hipDeviceSynchronize();
+    (void)hipMemcpy(h_cycles, d_c, waves * 8, hipMemcpyDeviceToHost);
+    (void)hipFree(d_out);
+    (void)hipFree(d_c);
+    return 0;
 }

@@ -52,13 +52,17 @@ __device__ __forceinline__ void quad_swap(uint4 v[4], uint32_t lane) {
         t[j].z = __builtin_amdgcn_mov_dpp(src.z, CTRL, 0xf, 0xf, false);
         t[j].w = __builtin_amdgcn_mov_dpp(src.w, CTRL, 0xf, 0xf, false);
     }
+    // select by a lane-constant all-ones/zero VGPR mask with v_bitop3 (m ? t : v):
+    // v_cndmask on an SGPR lane mask cost ~13 cycles per wave-instruction per SIMD at
+    // 4 waves/SIMD in our measurements (scripts/diag_ops.py), bitop3 ~1.6
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const bool take = ((lane ^ (uint32_t)j) & BIT) != 0;
-        v[j].x = take ? t[j].x : v[j].x;
-        v[j].y = take ? t[j].y : v[j].y;
-        v[j].z = take ? t[j].z : v[j].z;
-        v[j].w = take ? t[j].w : v[j].w;
+        uint32_t m = 0u - (((lane ^ (uint32_t)j) & BIT) != 0 ? 1u : 0u);
+        asm volatile("" : "+v"(m));  // keep the mask in a VGPR (no re-derivation into an SGPR lane mask)
+        v[j].x = __builtin_amdgcn_bitop3_b32(m, t[j].x, v[j].x, 0xCA);
+        v[j].y = __builtin_amdgcn_bitop3_b32(m, t[j].y, v[j].y, 0xCA);
+        v[j].z = __builtin_amdgcn_bitop3_b32(m, t[j].z, v[j].z, 0xCA);
+        v[j].w = __builtin_amdgcn_bitop3_b32(m, t[j].w, v[j].w, 0xCA);
     }
 }
 
@@ -77,7 +81,10 @@ __device__ __forceinline__ void quad_transpose(uint4 v[4], uint32_t lane) {
 // running min (5 VALU + 1 LDS read per byte); a piece whose min hits 0 in some lane
 // is re-walked exactly for that lane.  Used when mask_s & mask_l has >= 15 bits
 // (hits are rarer than ~1 per 32 KiB); otherwise every byte is tested exactly.
-template <bool PRE>
+// DIAG (diagnostics only, 0 = product): 1 = loads only, 2 = loads + transpose,
+// 3 = hashing on register-resident bytes without loads, 4 = as 3 without LDS reads;
+// + 8 = non-temporal loads.
+template <bool PRE, int DIAG = 0>
 __global__ __launch_bounds__(SCAN2_T) void k_scan(const uint8_t *__restrict__ data, uint64_t n,
                                                   const uint64_t *__restrict__ gear_g, uint64_t mask_s,
                                                   uint64_t mask_l, uint32_t cap, uint32_t *__restrict__ seg_count,
@@ -124,56 +131,113 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan(const uint8_t *__restrict__ da
     }
 
     uint32_t count = 0;
+    uint64_t hits = 0;  // PRE: bit r = piece r may hold a candidate (CG_SEG / QPIECE == 64 pieces)
     uint32_t *cand = seg_cand + seg * cap;
     const uint32_t rounds = CG_SEG / QPIECE;  // wave-uniform trip count
-    uint4 buf[3][4];
+    static_assert(CG_SEG / QPIECE == 64, "hits mask holds one bit per piece");
+    uint4 buf[4][4];
+    // Loads are unconditional (a piece index past the owner's last piece is clamped to
+    // a valid address and its bytes are never hashed): with no exec-masked loads the
+    // compiler counts vmcnt exactly and waits only for the piece about to be hashed,
+    // keeping the two pieces behind it in flight.
+    // Per owner: base address of this lane's quarter and the last valid piece index, so
+    // a load address is one v_min_u32 + one v_lshl_add_u64 (no lane-mask selects).
+    const uint8_t *own_base[4];
+    uint32_t own_last[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        own_base[j] = own_np[j] ? data + own_start[j] + 16u * qi : data;
+        own_last[j] = own_np[j] ? own_np[j] - 1u : 0u;
+    }
     auto issue = [&](uint4(&v)[4], uint32_t r) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-            v[j] = r < own_np[j]
-                       ? *reinterpret_cast<const uint4 *>(data + own_start[j] + (uint64_t)r * QPIECE + 16u * qi)
-                       : make_uint4(0, 0, 0, 0);
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t rj = min(r, own_last[j]);
+            const uint8_t *a = own_base[j] + (uint64_t)rj * QPIECE;
+            if constexpr ((DIAG & 8) != 0) {
+                typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(a));
+                v[j] = make_uint4(t.x, t.y, t.z, t.w);
+            } else {
+                v[j] = *reinterpret_cast<const uint4 *>(a);
+            }
+        }
     };
     issue(buf[0], 0);
     issue(buf[1], 1);
+    // 4-deep register ring.  Pieces are fetched in pairs -- both 64-B halves of each
+    // segment's 128-B line in one burst, so no line is requested twice (a lone half
+    // re-requested a piece later was re-fetched from HBM: +22 % traffic) -- two to
+    // three pieces ahead of the one being hashed.  The trip count is a multiple of the
+    // unroll, so the body has one path and the compiler's vmcnt waits are exact.
 #pragma unroll 1
-    for (uint32_t r = 0; r < rounds; r += 3) {
+    for (uint32_t r = 0; r < rounds; r += 4) {
 #pragma unroll
-        for (int u = 0; u < 3; ++u) {
+        for (int u = 0; u < 4; ++u) {
             const uint32_t rr = r + u;
-            if (rr >= rounds) break;
-            issue(buf[(u + 2) % 3], rr + 2);
+            if constexpr ((DIAG & 7) < 3) {
+                if ((u & 1) == 0) {
+                    issue(buf[(u + 2) & 3], rr + 2);
+                    issue(buf[(u + 3) & 3], rr + 3);
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);  // keep each piece's loads in program order
             uint4 v[4] = {buf[u][0], buf[u][1], buf[u][2], buf[u][3]};
-            quad_transpose(v, lane);
-            if (rr < npieces) {
-                const uint64_t p = start + (uint64_t)rr * QPIECE;
-                const uint64_t h0 = h;
-                if (PRE) {
-                    uint32_t acc = 0xffffffffu;
+            if constexpr ((DIAG & 7) >= 3) {
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+                for (int k = 0; k < 4; ++k) v[k] = make_uint4(lane * 0x01010101u + rr, (uint32_t)h, k, rr * 77u);
+            }
+            if constexpr ((DIAG & 7) != 1) quad_transpose(v, lane);
+            if constexpr ((DIAG & 7) == 1 || (DIAG & 7) == 2) {
+                uint32_t x = 0;
 #pragma unroll
-                        for (int j = 0; j < 4; ++j)
+                for (int k = 0; k < 4; ++k) x ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+                h += x;
+                hits |= (x == 0x12345678u) ? 1ull : 0ull;
+            } else if (PRE) {
+                // Branch-free: fold (h & mask_s & mask_l) into a running min; a piece
+                // whose min reaches 0 only sets its bit in `hits` and is re-walked
+                // exactly after the loop.  No stores inside the loop, so the compiler's
+                // vmcnt stays exact and two pieces stay in flight.
+                uint64_t hn = h;
+                uint32_t acc = 0xffffffffu;
+                const uint32_t wd[16] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
+                                         v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w};
+                // Gear lookups run GRP bytes ahead of the shift-add chain (two groups of
+                // LDS reads in flight per wave instead of four reads).
+                constexpr int GRP = 4;
+                uint64_t g[2][GRP];
+                auto fetch = [&](uint64_t(&dst)[GRP], int grp) {
 #pragma unroll
-                            for (int b = 0; b < 4; ++b) {
-                                h = (h << 1) + lds_gear(gbase, gear_addr(w[j], lo8, b));
-                                acc = min(acc, ((uint32_t)h & ml) | ((uint32_t)(h >> 32) & mh));
-                            }
-                    }
-                    if (acc == 0) {  // rare: exact re-walk of this piece, re-read from L2
-                        uint64_t hh = h0;
-#pragma unroll 1
-                        for (uint32_t i = 0; i < QPIECE; ++i) {
-                            hh = (hh << 1) + lds_gear(gbase, ((uint32_t)data[p + i] << 8) | lo8);
-                            const uint32_t f = gear_flags(hh, mask_s, mask_l);
-                            if (f) {
-                                if (count < cap) cand[count] = ((uint32_t)(p - start + i) << 2) | f;
-                                ++count;
-                            }
+                    for (int t = 0; t < GRP; ++t) {
+                        const int byte = grp * GRP + t;
+                        if constexpr ((DIAG & 7) == 4) {
+                            const uint32_t a = gear_addr(wd[byte >> 2], lo8, byte & 3);
+                            dst[t] = ((uint64_t)a << 32) | a;
+                        } else {
+                            dst[t] = lds_gear(gbase, gear_addr(wd[byte >> 2], lo8, byte & 3));
                         }
                     }
-                } else {
+                };
+                fetch(g[0], 0);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int grp = 0; grp < QPIECE / GRP; ++grp) {
+                    if (grp + 1 < QPIECE / GRP) fetch(g[(grp + 1) & 1], grp + 1);
+                    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead of the chain
+#pragma unroll
+                    for (int t = 0; t < GRP; ++t) {
+                        hn = (hn << 1) + g[grp & 1][t];
+                        // (lo & ml) | (hi & mh) in two ops: v_and + v_bitop3 (S0&S1)|S2
+                        acc = min(acc, (uint32_t)__builtin_amdgcn_bitop3_b32((uint32_t)(hn >> 32), mh, (uint32_t)hn & ml, 0xEA));
+                    }
+                }
+                const bool live = rr < npieces;
+                h = live ? hn : h;
+                hits |= (live && acc == 0) ? (1ull << rr) : 0ull;
+            } else if (rr < npieces) {
+                const uint64_t p = start + (uint64_t)rr * QPIECE;
+                {
 #pragma unroll
                     for (int k = 0; k < 4; ++k) {
                         const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
@@ -195,6 +259,42 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan(const uint8_t *__restrict__ da
         }
     }
     if (!active) return;
+    if (PRE) {
+        // Exact re-walk of the flagged pieces, in order, from L2/MALL-resident bytes.
+        // The hash restarts 48 bytes before the piece (or at 0 for the batch's first
+        // bytes, where the scan itself started): the tested bits (<= 47) equal the
+        // scan's, which restarted at the segment's own halo.
+        while (hits) {
+            const uint32_t r = (uint32_t)__builtin_ctzll(hits);
+            hits &= hits - 1;
+            const uint64_t p = start + (uint64_t)r * QPIECE;
+            const uint64_t q0 = p >= CG_HALO ? p - CG_HALO : 0;
+            uint64_t hh = 0;
+            for (uint64_t q = q0; q < p; q += 16) {
+                const uint4 x = *reinterpret_cast<const uint4 *>(data + q);
+                const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) hh = (hh << 1) + lds_gear(gbase, gear_addr(w[j], lo8, b));
+            }
+            for (uint32_t k = 0; k < QPIECE; k += 16) {
+                const uint4 x = *reinterpret_cast<const uint4 *>(data + p + k);
+                const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        hh = (hh << 1) + lds_gear(gbase, gear_addr(w[j], lo8, b));
+                        const uint32_t f = gear_flags(hh, mask_s, mask_l);
+                        if (f) {
+                            if (count < cap) cand[count] = ((uint32_t)(p - start + k + 4 * j + b) << 2) | f;
+                            ++count;
+                        }
+                    }
+            }
+        }
+    }
     for (uint64_t p = start + (uint64_t)npieces * QPIECE; p < end; ++p) {  // ragged tail (< 64 bytes)
         h = (h << 1) + lds_gear(gbase, ((uint32_t)data[p] << 8) | lo8);
         const uint32_t f = gear_flags(h, mask_s, mask_l);
@@ -206,11 +306,22 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan(const uint8_t *__restrict__ da
     seg_count[seg] = count;
 }
 
+uint32_t g_scan_diag = 0;  // set by cg_diag_scan_mode (diagnostics only; 0 = product)
+
 void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint64_t mask_s, uint64_t mask_l,
                  uint32_t cap, uint32_t *d_seg_count, uint32_t *d_seg_cand, uint64_t nseg, hipStream_t st) {
     if (nseg == 0) return;
     const uint64_t blocks = (nseg + SCAN2_T - 1) / SCAN2_T;
-    if (__builtin_popcountll(mask_s & mask_l) >= 15)
+    if (g_scan_diag && __builtin_popcountll(mask_s & mask_l) >= 15) {
+        auto k = g_scan_diag == 1   ? k_scan<true, 1>
+                 : g_scan_diag == 2 ? k_scan<true, 2>
+                 : g_scan_diag == 3 ? k_scan<true, 3>
+                 : g_scan_diag == 4 ? k_scan<true, 4>
+                 : g_scan_diag == 8 ? k_scan<true, 8>
+                                    : k_scan<true, 9>;
+        hipLaunchKernelGGL(k, dim3((uint32_t)blocks), dim3(SCAN2_T), 0, st, d_data, n, d_gear, mask_s, mask_l, cap,
+                           d_seg_count, d_seg_cand, nseg);
+    } else if (__builtin_popcountll(mask_s & mask_l) >= 15)
         hipLaunchKernelGGL(k_scan<true>, dim3((uint32_t)blocks), dim3(SCAN2_T), 0, st, d_data, n, d_gear, mask_s,
                            mask_l, cap, d_seg_count, d_seg_cand, nseg);
     else

@@ -1,0 +1,29 @@
+"""Diagnostic: issue cost (cycles per instruction per wave) of the integer VALU
+instructions the scan / SHA-256 / BLAKE3 kernels are built from, for 1, 4, 8 and 16
+waves in one workgroup (s_memtime, shader clocks)."""
+import ctypes
+import json
+import sys
+
+import numpy as np
+import torch  # noqa: F401
+
+sys.path.insert(0, ".")
+from chunker_amd._lib import lib  # noqa: E402
+
+NAMES = ["v_add_u32", "v_lshl_add_u64", "v_perm_b32", "v_add_co+v_addc_co", "v_alignbit_b32", "v_bitop3_b32",
+         "v_lshlrev_b64", "v_mov_b32_dpp", "v_add3_u32", "v_cndmask_b32", "dep_chain v_lshl_add_u64",
+         "dep_chain v_add_u32"]
+lib.cg_diag_ops.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+it = 500
+res = {}
+for k, name in enumerate(NAMES):
+    row = {}
+    for threads in [64, 256, 512, 1024]:
+        w = threads // 64
+        cyc = np.zeros(w, np.uint64)
+        rc = lib.cg_diag_ops(k, it, threads, cyc.ctypes.data)
+        assert rc == 0
+        row[f"{w}w"] = round(float(np.median(cyc)) / (it * 256), 2)
+    res[name] = row
+print(json.dumps(res))

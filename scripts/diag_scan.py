@@ -1,0 +1,67 @@
+"""Diagnostic: k_scan stage time by diag mode (0 product, 1 loads only, 2 loads +
+transpose, 3 hashing without loads) on config-2 and config-4 shaped batches."""
+import ctypes
+import json
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+import chunker_amd as ca  # noqa: E402
+from chunker_amd.nar import synth_nars  # noqa: E402
+
+import argparse  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--modes", default="0,8,1,9,2,3,4,0")
+ap.add_argument("--configs", default="c2,c4")
+ap.add_argument("--no-pattern", action="store_true")
+args = ap.parse_args()
+lib = ca.lib
+lib.cg_diag_scan_mode.argtypes = [ctypes.c_uint32]
+res = {}
+for name, n, size, params in [("c2", 256, 4 << 20, (256 << 10, 1 << 20, 4 << 20)),
+                              ("c4", 4, 1 << 30, (64 << 10, 256 << 10, 1 << 20))]:
+    if name not in args.configs.split(","):
+        continue
+    host, offs = synth_nars(np.full(n, size, np.uint64))
+    d = torch.empty(len(host) + 256, dtype=torch.uint8, device="cuda")
+    d[:len(host)].copy_(torch.from_numpy(host))
+    del host
+    cap = ca.chunking.batch_capacity(offs, params[0])
+    out = torch.empty(cap * 48, dtype=torch.uint8, device="cuda")
+    sp = torch.cuda.current_stream().cuda_stream
+    buf = (ctypes.c_double * 5)()
+    for mode in [int(m) for m in args.modes.split(",")]:
+        lib.cg_diag_scan_mode(mode)
+        ms = []
+        for it in range(6):
+            lib.cg_set_profiling(1)
+            ca.chunk_batch_device(d.data_ptr(), offs, out.data_ptr(), cap, *params, hash=0, stream=sp)
+            lib.cg_last_stage_times(buf, 5)
+            if it >= 2:
+                ms.append(buf[0])
+        gib = int(offs[-1]) / 2**30
+        res[f"{name}_mode{mode}"] = {"scan_ms": round(float(np.median(ms)), 4),
+                                     "GBps": round(int(offs[-1]) / (np.median(ms) * 1e-3) / 1e9, 1)}
+    lib.cg_diag_scan_mode(0)
+    del d, out
+    torch.cuda.empty_cache()
+print(json.dumps(res))
+
+# HBM read patterns: 1 GiB, runs of L contiguous bytes per 4 KiB segment per round
+if args.no_pattern:
+    sys.exit(0)
+lib.cg_diag_read_pattern.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+lib.cg_diag_read_pattern.restype = ctypes.c_float
+d = torch.randint(0, 255, (1 << 30,), dtype=torch.uint8, device="cuda")
+o = torch.empty(512 * 512, dtype=torch.int32, device="cuda")
+pat = {}
+for lg in [6, 7, 8, 10, 12]:
+    for depth in [2, 4]:
+        for nt in [0, 1]:
+            code = lg | (nt << 8) | (depth << 12)
+            ms = sorted(lib.cg_diag_read_pattern(d.data_ptr(), code, o.data_ptr()) for _ in range(5))[2]
+            pat[f"run{1 << lg}_d{depth}{'_nt' if nt else ''}"] = round(2**30 / (ms * 1e-3) / 1e9, 1)
+print(json.dumps(pat))
