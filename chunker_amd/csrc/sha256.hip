@@ -71,6 +71,8 @@ __device__ __forceinline__ void lds_store_release(uint32_t *p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+__device__ __forceinline__ unsigned long long wait_ready(const uint32_t *ctr, uint32_t k, bool timed);
+
 __device__ __forceinline__ void load_w(uint4 (&w)[16], const uint32_t *row) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) w[i] = *reinterpret_cast<const uint4 *>(row + 4 * i);
@@ -103,8 +105,7 @@ __device__ __forceinline__ void sha_rounds_pf(uint32_t st[8], const uint4 (&cur)
     SHA_8RND(16, cur);
     SHA_8RND(24, cur);
     if (prefetch) {
-        if (__builtin_expect(r0 <= knext, 0))
-            while (lds_load_acquire(ready) <= knext) __builtin_amdgcn_s_sleep(1);
+        if (__builtin_expect(r0 <= knext, 0)) wait_ready(ready, knext, false);
         load_w(nxt, next_row);
     }
     SHA_8RND(32, cur);
@@ -153,123 +154,425 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 
 #define PC_RING 4u  // LDS schedule slots: the producer runs up to 4 blocks ahead
 
+// Spin guard: no legitimate wait for a ring slot lasts more than a few blocks
+// (~10^4 clocks); 2^26 sleeps (~2 s) ends a wait that would otherwise hang the GPU.
+#define SHA_SPIN_LIMIT (1u << 26)
+
+// Wait until `*ctr` moved past `k` (consumer: producer filled slot k) -- `ready`
+// form -- or until slot k is free (producer: consumer released k - PC_RING).
+__device__ __forceinline__ unsigned long long wait_ready(const uint32_t *ctr, uint32_t k, bool timed) {
+    if (lds_load_acquire(ctr) > k) return 0;
+    const unsigned long long t0 = timed ? __builtin_amdgcn_s_memtime() : 0ull;
+    for (uint32_t it = 0; lds_load_acquire(ctr) <= k && it < SHA_SPIN_LIMIT; ++it) __builtin_amdgcn_s_sleep(1);
+    return timed ? __builtin_amdgcn_s_memtime() - t0 : 0ull;
+}
+__device__ __forceinline__ unsigned long long wait_slot(const uint32_t *done, uint32_t k, bool timed) {
+    if ((int)(k - lds_load_acquire(done)) < (int)PC_RING) return 0;
+    const unsigned long long t0 = timed ? __builtin_amdgcn_s_memtime() : 0ull;
+    for (uint32_t it = 0; (int)(k - lds_load_acquire(done)) >= (int)PC_RING && it < SHA_SPIN_LIMIT; ++it)
+        __builtin_amdgcn_s_sleep(1);
+    return timed ? __builtin_amdgcn_s_memtime() - t0 : 0ull;
+}
+// This wave's schedule writes for block k have landed: publish k + 1.
+__device__ __forceinline__ void publish(uint32_t *ready, uint32_t k, uint32_t lane) {
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    if (lane == 0) lds_store_release(ready, k + 1);
+}
+
+// Words of a chunk's tail block (k == nb: tail bytes, 0x80, zeros, [bit length]) or
+// of its second padding block (k == nb + 1).  Loads stop at the chunk's end.
+__device__ __forceinline__ void sha_pad_words(uint32_t w[16], const uint8_t *p, const uint32_t *base, uint32_t sel,
+                                              uint64_t len, uint64_t k) {
+    const uint64_t nb = len >> 6;
+    const uint32_t rem = (uint32_t)(len & 63u);
+    const uint64_t bits = len << 3;
+    if (k == nb) {
+        const uint32_t *q = base + 16 * nb;
+        const uint8_t *endp = p + len;
+        uint32_t dw[17];
+#pragma unroll
+        for (int i = 0; i < 17; ++i) dw[i] = (reinterpret_cast<const uint8_t *>(q + i) < endp) ? q[i] : 0u;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t v = __builtin_amdgcn_perm(dw[i + 1], dw[i], sel);
+            const int r = (int)rem - 4 * i;
+            w[i] = r >= 4 ? v
+                          : (r < 0 ? 0u
+                                   : ((r ? (v & (0xffffffffu << (32 - 8 * r))) : 0u) | (0x80u << (24 - 8 * r))));
+        }
+        if (rem < 56) {
+            w[14] = (uint32_t)(bits >> 32);
+            w[15] = (uint32_t)bits;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 14; ++i) w[i] = 0u;
+        w[14] = (uint32_t)(bits >> 32);
+        w[15] = (uint32_t)bits;
+    }
+}
+
+__device__ __forceinline__ uint32_t perm_sel(uint32_t shift) {
+    return (shift << 24) | ((shift + 1) << 16) | ((shift + 2) << 8) | (shift + 3);
+}
+
+// Producer wave of a one-lane-per-chunk workgroup: for k = 0..NB-1 wait for a free
+// ring slot, load + realign + pad block k of this lane's chunk, expand its schedule
+// (W[t] + K[t], 64 words) into row `row` of slot k % PC_RING, publish.
+__device__ unsigned long long sha_produce(const uint8_t *p, uint64_t len, uint32_t nbt, uint32_t NB,
+                                          uint32_t (*sW)[64 * PC_ROW], uint32_t row, uint32_t lane,
+                                          uint32_t *s_ready, const uint32_t *s_done, bool timed) {
+    unsigned long long t_spin = 0;
+    const uint64_t nb = len >> 6;
+    const uint32_t shift = (uint32_t)((uintptr_t)p & 3u);
+    const uint32_t *base = reinterpret_cast<const uint32_t *>(p - shift);
+    const uint32_t sel = perm_sel(shift);
+    // One block buffer: block k+1's bytes are requested as soon as block k's words
+    // have been realigned out of it, so a whole schedule computation (~2,000
+    // cycles) covers their latency and the only loads in flight at the next
+    // realign are exactly the ones it needs (vmcnt(0) is then the precise wait).
+    uint32_t d[17];
+    auto load_full = [&](uint64_t k) {
+        const uint32_t *q = base + 16 * k;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) d[i] = q[i];
+        // dword 16 holds chunk bytes whenever shift != 0; for shift == 0 the realign
+        // ignores it, so re-read dword 15 (unconditional: keeps vmcnt tracking exact)
+        d[16] = q[shift ? 16 : 15];
+    };
+    if (nb > 0) load_full(0);
+    for (uint32_t k = 0; k < NB; ++k) {
+        t_spin += wait_slot(s_done, k, timed);
+        if (k < nbt) {
+            uint32_t w[16];
+            if (k < nb) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_perm(d[i + 1], d[i], sel);
+                // keep the realign ahead of the reload so the loads land in d's own
+                // registers (no copies, no wait); the last full block re-reads itself
+                __builtin_amdgcn_sched_barrier(0);
+                load_full(k + 1 < nb ? k + 1 : k);
+            } else {
+                sha_pad_words(w, p, base, sel, len, k);
+            }
+            sha_schedule_store(w, &sW[k % PC_RING][row * PC_ROW]);
+        }
+        publish(s_ready, k, lane);
+    }
+    return t_spin;
+}
+
+// ---------------------------------------------------------------------------
+// Split-lane workgroups: ONE chunk per PAIR of lanes.
+//
+// A batch's digest stage lasts as long as its longest chunk, whose 64 rounds per
+// block are a chain that one wave issues at ~4.2 clocks per VALU instruction: the
+// chain's instruction count per round is the whole cost.  The longest chunks
+// therefore run with each round spread over two lanes 4 apart in a DPP row
+// ("lo" = banks 0/2, "hi" = banks 1/3).  lo holds e,f,g,h and hi holds a,b,c,d in
+// the same four registers X0..X3 (newest first), so one instruction stream
+// computes both halves of the round:
+//   r1..r3 = rotations of X0       per-lane amounts 6/11/25 (lo), 2/13/22 (hi)
+//   x      = X0 ^ (X2 & LM)        LM = 0 (lo), ~0 (hi): e (lo), a^c (hi)
+//   S      = r1 ^ r2 ^ r3          Sigma1(e) (lo), Sigma0(a) (hi)
+//   F      = x ? X1 : X2           Ch(e,f,g) (lo), Maj(a,b,c) = (a^c) ? b : c (hi)
+//   P      = Z + S + F             T1 with Z = h + W[t]+K[t] (lo), T2 with Z = 0 (hi)
+//   X3    <- P + d                 lo lanes; d = hi's X3 through DPP row_shl:4 -> new e
+//   Z     <- X2 + W[t+1]+K[t+1]    lo lanes (next round's h is this round's g)
+//   X3    <- P + T1                hi lanes; T1 = lo's P through DPP row_shr:4 -> new a
+// 10 VALU per round instead of 14.  The three partial writes are DPP bank masks
+// (0x5 lo, 0xA hi): no exec-mask change.  Every DPP source was written at least two
+// instructions earlier (the gfx9 VALU-write -> DPP-read hazard), so the rounds need
+// no s_nop.  Per block the pair reads the schedule by parity (see
+// sha_produce_pair): lo lanes hold the even words, hi lanes the odd ones, and the
+// Z step takes W[t+1] from its own registers (t+1 even) or from hi's through DPP.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t split_slot(uint32_t lane) {
+    return ((lane >> 4) << 3) | (((lane >> 3) & 1u) << 2) | (lane & 3u);
+}
+// LDS row of chunk slot j: rows 8..15 of each 16 swapped in halves, so the 16 lanes
+// of every ds_read_b128 lane group (lo at word 0, hi at word 32 of a row) start on
+// 16 distinct 4-bank quads.
+__device__ __forceinline__ uint32_t split_row(uint32_t j) { return j ^ ((j >> 1) & 4u); }
+
+struct SplitLane {
+    uint32_t sh1, sh2, sh3, lm;  // rotation amounts, Maj-select mask
+};
+
+template <int I>
+__device__ __forceinline__ uint32_t w_at(const uint4 (&W)[8]) {
+    if constexpr ((I & 3) == 0)
+        return W[I >> 2].x;
+    else if constexpr ((I & 3) == 1)
+        return W[I >> 2].y;
+    else if constexpr ((I & 3) == 2)
+        return W[I >> 2].z;
+    else
+        return W[I >> 2].w;
+}
+
+// One split round as asm text, registers named by role: A = X0 (newest) .. D = X3;
+// the new X0 is written into D.  ZOP prepares the next round's Z.
+#define SR(A, B, C, D, ZOP)                                                               \
+    "v_alignbit_b32 %[r1], %[" #A "], %[" #A "], %[s1]\n\t"                               \
+    "v_alignbit_b32 %[r2], %[" #A "], %[" #A "], %[s2]\n\t"                               \
+    "v_alignbit_b32 %[r3], %[" #A "], %[" #A "], %[s3]\n\t"                               \
+    "v_bitop3_b32 %[xx], %[" #A "], %[" #C "], %[lm] bitop3:0x78\n\t"                     \
+    "v_bitop3_b32 %[s], %[r1], %[r2], %[r3] bitop3:0x96\n\t"                              \
+    "v_bitop3_b32 %[f], %[xx], %[" #B "], %[" #C "] bitop3:0xca\n\t"                      \
+    "v_add3_u32 %[p], %[z], %[s], %[f]\n\t"                                               \
+    "v_add_u32_dpp %[" #D "], %[" #D "], %[p] row_shl:4 row_mask:0xf bank_mask:0x5\n\t"   \
+    ZOP "v_add_u32_dpp %[" #D "], %[p], %[p] row_shr:4 row_mask:0xf bank_mask:0xa\n\t"
+// next word from lo's own register / from hi's register (row_shl:4) / none (the
+// s_nop keeps two wait states between p's write and its DPP read)
+#define ZLO(C, W) "v_add_u32_dpp %[z], %[" #C "], %[" #W "] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x5\n\t"
+#define ZHI(C, W) "v_add_u32_dpp %[z], %[" #W "], %[" #C "] row_shl:4 row_mask:0xf bank_mask:0x5\n\t"
+#define ZNONE "s_nop 0\n\t"
+#define SR8_HEAD                                                                       \
+    SR(x0, x1, x2, x3, ZHI(x2, w0)) SR(x3, x0, x1, x2, ZLO(x1, w1)) SR(x2, x3, x0, x1, ZHI(x0, w1)) \
+    SR(x1, x2, x3, x0, ZLO(x3, w2)) SR(x0, x1, x2, x3, ZHI(x2, w2)) SR(x3, x0, x1, x2, ZLO(x1, w3)) \
+    SR(x2, x3, x0, x1, ZHI(x0, w3))
+#define SR8_OUTS                                                                                                 \
+    [x0] "+v"(x0), [x1] "+v"(x1), [x2] "+v"(x2), [x3] "+v"(x3), [z] "+v"(z), [r1] "=&v"(r1), [r2] "=&v"(r2),     \
+        [r3] "=&v"(r3), [xx] "=&v"(xx), [s] "=&v"(s), [f] "=&v"(f), [p] "=&v"(p)
+#define SR8_INS                                                                                              \
+    [s1] "v"(c.sh1), [s2] "v"(c.sh2), [s3] "v"(c.sh3), [lm] "v"(c.lm), [w0] "v"(w_at<T / 2>(W)),             \
+        [w1] "v"(w_at<T / 2 + 1>(W)), [w2] "v"(w_at<T / 2 + 2>(W)), [w3] "v"(w_at<T / 2 + 3>(W))
+
+// Rounds T..T+7 of a block in one asm statement (hipcc pads every asm boundary with
+// an s_nop, so one statement per round would cost an 11th issue slot).  Round r's
+// Z step needs word r+1: odd -> hi's register (r+1-1)/2, even -> lo's (r+1)/2.
+template <int T>
+__device__ __forceinline__ void spl_round8(uint32_t &x0, uint32_t &x1, uint32_t &x2, uint32_t &x3, uint32_t &z,
+                                           const uint4 (&W)[8], const SplitLane &c) {
+    uint32_t r1, r2, r3, xx, s, f, p;
+    if constexpr (T + 8 < 64) {
+        asm volatile(SR8_HEAD SR(x1, x2, x3, x0, ZLO(x3, w4))
+                     : SR8_OUTS
+                     : SR8_INS, [w4] "v"(w_at<T / 2 + 4>(W)));
+    } else {
+        asm volatile(SR8_HEAD SR(x1, x2, x3, x0, ZNONE) : SR8_OUTS : SR8_INS);
+    }
+}
+
+// Z for round 0 of the next block: h (lo's X3 after the state add) + W[0]+K[0], lo lanes only.
+__device__ __forceinline__ void spl_z(uint32_t &z, uint32_t h, uint32_t wv0) {
+    asm volatile("s_nop 1\n\tv_add_u32_dpp %0, %1, %2 quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x5"
+                 : "+v"(z)
+                 : "v"(h), "v"(wv0));
+}
+
+#define SPL32(T, W)                                \
+    spl_round8<(T)>(x0, x1, x2, x3, z, W, c);      \
+    spl_round8<(T) + 8>(x0, x1, x2, x3, z, W, c);  \
+    spl_round8<(T) + 16>(x0, x1, x2, x3, z, W, c); \
+    spl_round8<(T) + 24>(x0, x1, x2, x3, z, W, c);
+
+__device__ __forceinline__ void load_w8(uint4 (&w)[8], const uint32_t *row) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) w[i] = *reinterpret_cast<const uint4 *>(row + 4 * i);
+}
+
+// 64 split rounds on `cur` (this lane's 32 schedule words); half-way through, once
+// the producer has published block `knext`, the next block's words are read into `nxt`.
+__device__ __forceinline__ void sha_rounds_split(uint32_t st[4], const uint4 (&cur)[8], uint4 (&nxt)[8],
+                                                 const uint32_t *next_row, uint32_t knext, bool prefetch,
+                                                 const uint32_t *ready, bool active, const SplitLane &c,
+                                                 uint32_t &z) {
+    uint32_t x0 = st[0], x1 = st[1], x2 = st[2], x3 = st[3];
+    const uint32_t r0 = __hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    SPL32(0, cur)
+    if (prefetch) {
+        if (__builtin_expect(r0 <= knext, 0)) wait_ready(ready, knext, false);
+        load_w8(nxt, next_row);
+    }
+    SPL32(32, cur)
+    st[0] = active ? st[0] + x0 : st[0];
+    st[1] = active ? st[1] + x1 : st[1];
+    st[2] = active ? st[2] + x2 : st[2];
+    st[3] = active ? st[3] + x3 : st[3];
+}
+
+// Producer wave of a split workgroup.  The pair shares the message schedule by
+// parity: lo lanes own the even words w[2i], hi lanes the odd words w[2i+1].  In
+//   w[t] = s1(w[t-2]) + w[t-16] + (w[t-7] + s0(w[t-15]))
+// the first two terms have t's parity (own registers) and the bracket the other
+// one: the partner computes X = R[i-3] + s0(R[i-7]) on its own words, which is the
+// bracket hi needs at step i (lo's X) and lo needs at step i+1 (hi's X), and hands
+// it over in one DPP add.  Each lane expands 24 words instead of 48 and stores its
+// 32 (+K) to its half of the chunk's row (lo: words 0-31, hi: 32-63).
+__device__ __forceinline__ void sha_schedule_pair_store(const uint32_t R0[8], const uint32_t Kp[32], uint32_t *dst) {
+    uint32_t R[32];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) R[i] = R0[i];
+#pragma unroll
+    for (int i = 0; i < 8; i += 4)
+        *reinterpret_cast<uint4 *>(dst + i) =
+            make_uint4(R[i] + Kp[i], R[i + 1] + Kp[i + 1], R[i + 2] + Kp[i + 2], R[i + 3] + Kp[i + 3]);
+    uint32_t xprev = R[4] + SHA_s0(R[0]);  // X of step 7 (hi's is what lo needs at step 8)
+#pragma unroll
+    for (int i = 8; i < 32; ++i) {
+        const uint32_t x = R[i - 3] + SHA_s0(R[i - 7]);
+        const uint32_t y = SHA_s1(R[i - 1]) + R[i - 8];
+        uint32_t r;
+        asm volatile(
+            "s_nop 1\n\t"
+            "v_add_u32_dpp %0, %1, %2 row_shl:4 row_mask:0xf bank_mask:0x5\n\t"
+            "v_add_u32_dpp %0, %3, %2 row_shr:4 row_mask:0xf bank_mask:0xa"
+            : "=&v"(r)
+            : "v"(xprev), "v"(y), "v"(x));
+        R[i] = r;
+        xprev = x;
+        if ((i & 3) == 3)
+            *reinterpret_cast<uint4 *>(dst + i - 3) =
+                make_uint4(R[i - 3] + Kp[i - 3], R[i - 2] + Kp[i - 2], R[i - 1] + Kp[i - 1], R[i] + Kp[i]);
+    }
+}
+
+__device__ unsigned long long sha_produce_pair(const uint8_t *p, uint64_t len, uint32_t nbt, uint32_t NB,
+                                               uint32_t (*sW)[64 * PC_ROW], uint32_t row, bool hi, uint32_t lane,
+                                               uint32_t *s_ready, const uint32_t *s_done, bool timed) {
+    unsigned long long t_spin = 0;
+    const uint64_t nb = len >> 6;
+    const uint32_t shift = (uint32_t)((uintptr_t)p & 3u);
+    const uint32_t *base = reinterpret_cast<const uint32_t *>(p - shift);
+    const uint32_t sel = perm_sel(shift);
+    // hi lanes load from one dword further on: their d[i] is the block's dword i+1,
+    // so perm(d[2i+1], d[2i]) is word 2i+1 there and word 2i in lo lanes.  The last
+    // load is the block's dword 16 in hi lanes when shift != 0, else a re-read
+    // inside the block.
+    const uint32_t *mine = base + (hi ? 1 : 0);
+    const uint32_t last = (hi && shift == 0) ? 14u : 15u;
+    uint32_t d[16];
+    auto load_full = [&](uint64_t k) {
+        const uint32_t *q = mine + 16 * k;
+#pragma unroll
+        for (int i = 0; i < 15; ++i) d[i] = q[i];
+        d[15] = q[last];
+    };
+    uint32_t Kp[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) Kp[i] = hi ? SHA_K[2 * i + 1] : SHA_K[2 * i];
+    uint32_t *const dst0 = &sW[0][row * PC_ROW + (hi ? 32u : 0u)];
+    if (nb > 0) load_full(0);
+    for (uint32_t k = 0; k < NB; ++k) {
+        t_spin += wait_slot(s_done, k, timed);
+        if (k < nbt) {
+            uint32_t R[8];
+            if (k < nb) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) R[i] = __builtin_amdgcn_perm(d[2 * i + 1], d[2 * i], sel);
+                __builtin_amdgcn_sched_barrier(0);
+                load_full(k + 1 < nb ? k + 1 : k);
+            } else {
+                uint32_t w[16];
+                sha_pad_words(w, p, base, sel, len, k);
+#pragma unroll
+                for (int i = 0; i < 8; ++i) R[i] = hi ? w[2 * i + 1] : w[2 * i];
+            }
+            sha_schedule_pair_store(R, Kp, dst0 + (k % PC_RING) * (64 * PC_ROW));
+        }
+        publish(s_ready, k, lane);
+    }
+    return t_spin;
+}
+
+// Workgroups [0, nsplit) take 32 chunks each, one per lane pair (the length order
+// puts the longest chunks there); the rest take 64 chunks, one per lane.
 // diag (optional, nullptr in production): per workgroup {producer spin, producer
 // total, consumer spin, consumer total} in shader clocks (s_memtime).
 __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data, const uint64_t *__restrict__ abs,
                                                const DescRaw *__restrict__ desc, const uint64_t *__restrict__ total_p,
                                                uint64_t max_chunks, const uint32_t *__restrict__ order,
                                                uint8_t *__restrict__ hash_base, size_t stride,
-                                               unsigned long long *__restrict__ diag, uint32_t mode) {
+                                               unsigned long long *__restrict__ diag, uint32_t mode,
+                                               uint32_t nsplit) {
     unsigned long long t_start = diag ? __builtin_amdgcn_s_memtime() : 0ull, t_spin = 0;
     __shared__ __attribute__((aligned(16))) uint32_t sW[PC_RING][64 * PC_ROW];
     __shared__ uint32_t s_ready, s_done;  // blocks filled by the producer / consumed by the consumer
     const uint32_t lane = threadIdx.x & 63u;
     const bool producer = threadIdx.x < 64;
-    const uint64_t g = (uint64_t)blockIdx.x * 64 + lane;
+    const bool split = blockIdx.x < nsplit;
+    const uint64_t wg_base = split ? 32ull * blockIdx.x : 32ull * nsplit + 64ull * (blockIdx.x - nsplit);
+    const bool hi = split && ((lane >> 2) & 1u);
+    const uint32_t slot = split ? split_slot(lane) : lane;
+    const uint32_t row = split ? split_row(slot) : lane;
     uint64_t total = *total_p;
     if (total > max_chunks) total = max_chunks;
-    if ((uint64_t)blockIdx.x * 64 >= total) return;  // whole workgroup idle (uniform)
+    if (wg_base >= total) return;  // whole workgroup idle (uniform)
     if (threadIdx.x == 0) {
         s_ready = 0;
         s_done = 0;
     }
     __syncthreads();
+    const uint64_t g = wg_base + slot;
     const bool valid = g < total;
-    // lane -> chunk through the length order (longest first, see k_len_hist): the 64
+    // slot -> chunk through the length order (longest first, see k_len_hist): the
     // chunks of a wave have nearly equal block counts and the longest start first
     const uint64_t ci = valid ? (order ? (uint64_t)order[g] : g) : 0;
     const uint64_t len = valid ? desc[ci].length : 0;
     const uint64_t nb = len >> 6;
     const uint32_t rem = (uint32_t)(len & 63u);
     const uint32_t nbt = valid ? (uint32_t)(nb + (rem < 56 ? 1 : 2)) : 0u;  // blocks incl. padding
-    // identical in both waves (same 64 chunks); scalar, so the block loops are uniform
+    // identical in both waves (same chunks); scalar, so the block loops are uniform
     const uint32_t NB = __builtin_amdgcn_readfirstlane(wave_max_u32(nbt));
 
     if (producer) {
         const uint8_t *p = data + (valid ? abs[ci] : 0);
-        const uint32_t shift = (uint32_t)((uintptr_t)p & 3u);
-        const uint32_t *base = reinterpret_cast<const uint32_t *>(p - shift);
-        const uint32_t sel = (shift << 24) | ((shift + 1) << 16) | ((shift + 2) << 8) | (shift + 3);
-        const uint64_t bits = len << 3;
-        // One block buffer: block k+1's bytes are requested as soon as block k's words
-        // have been realigned out of it, so a whole schedule computation (~2,000
-        // cycles) covers their latency and the only loads in flight at the next
-        // realign are exactly the ones it needs (vmcnt(0) is then the precise wait).
-        uint32_t d[17];
-        auto load_full = [&](uint64_t k) {
-            const uint32_t *q = base + 16 * k;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) d[i] = q[i];
-            // dword 16 holds chunk bytes whenever shift != 0; for shift == 0 the realign
-            // ignores it, so re-read dword 15 (unconditional: keeps vmcnt tracking exact)
-            d[16] = q[shift ? 16 : 15];
-        };
-        auto produce = [&](uint32_t k) {
-            // wait for a free slot (wave-uniform spin on an LDS counter)
-            if ((int)(k - lds_load_acquire(&s_done)) >= (int)PC_RING) {
-                const unsigned long long t0 = diag ? __builtin_amdgcn_s_memtime() : 0ull;
-                while ((int)(k - lds_load_acquire(&s_done)) >= (int)PC_RING) __builtin_amdgcn_s_sleep(1);
-                if (diag) t_spin += __builtin_amdgcn_s_memtime() - t0;
-            }
-            if (k < nbt) {
-                uint32_t w[16];
-                if (k < nb) {
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_perm(d[i + 1], d[i], sel);
-                    // keep the realign ahead of the reload so the loads land in d's own
-                    // registers (no copies, no wait); the last full block re-reads itself
-                    __builtin_amdgcn_sched_barrier(0);
-                    load_full(k + 1 < nb ? k + 1 : k);
-                } else if (k == nb) {  // tail bytes, 0x80, zeros, [length]
-                    const uint32_t *q = base + 16 * nb;
-                    const uint8_t *endp = p + len;
-                    uint32_t dw[17];
-#pragma unroll
-                    for (int i = 0; i < 17; ++i)
-                        dw[i] = (reinterpret_cast<const uint8_t *>(q + i) < endp) ? q[i] : 0u;
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        const uint32_t v = __builtin_amdgcn_perm(dw[i + 1], dw[i], sel);
-                        const int r = (int)rem - 4 * i;
-                        w[i] = r >= 4 ? v
-                                      : (r < 0 ? 0u
-                                               : ((r ? (v & (0xffffffffu << (32 - 8 * r))) : 0u) |
-                                                  (0x80u << (24 - 8 * r))));
-                    }
-                    if (rem < 56) {
-                        w[14] = (uint32_t)(bits >> 32);
-                        w[15] = (uint32_t)bits;
-                    }
-                } else {  // second padding block
-#pragma unroll
-                    for (int i = 0; i < 14; ++i) w[i] = 0u;
-                    w[14] = (uint32_t)(bits >> 32);
-                    w[15] = (uint32_t)bits;
-                }
-                sha_schedule_store(w, &sW[k % PC_RING][lane * PC_ROW]);
-            }
-            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's schedule writes landed
-            if (lane == 0) lds_store_release(&s_ready, k + 1);
-        };
         if (mode == 1) {  // diag: no producer work, consumer rounds on stale schedules
             if (lane == 0) lds_store_release(&s_ready, 0xffffffffu);
+        } else if (split) {
+            t_spin = sha_produce_pair(p, len, nbt, NB, sW, row, hi, lane, &s_ready, &s_done, diag != nullptr);
         } else {
-            if (nb > 0) load_full(0);
-            for (uint32_t k = 0; k < NB; ++k) produce(k);
+            t_spin = sha_produce(p, len, nbt, NB, sW, row, lane, &s_ready, &s_done, diag != nullptr);
         }
         if (diag && lane == 0) {
             diag[4 * blockIdx.x + 0] = t_spin;
             diag[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memtime() - t_start;
         }
+    } else if (split) {
+        SplitLane c;
+        c.sh1 = hi ? 2u : 6u;
+        c.sh2 = hi ? 13u : 11u;
+        c.sh3 = hi ? 22u : 25u;
+        c.lm = hi ? 0xffffffffu : 0u;
+        asm volatile("" : "+v"(c.sh1), "+v"(c.sh2), "+v"(c.sh3), "+v"(c.lm));
+        uint32_t st[4] = {hi ? 0x6a09e667u : 0x510e527fu, hi ? 0xbb67ae85u : 0x9b05688cu,
+                          hi ? 0x3c6ef372u : 0x1f83d9abu, hi ? 0xa54ff53au : 0x5be0cd19u};
+        uint32_t z = 0;  // stays 0 in hi lanes: every write to it is masked to lo lanes
+        uint4 wA[8], wB[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) wA[i] = wB[i] = make_uint4(0u, 0u, 0u, 0u);
+        const uint32_t off = row * PC_ROW + (hi ? 32u : 0u);
+        if (NB > 0) {
+            t_spin += wait_ready(&s_ready, 0, diag != nullptr);
+            load_w8(wA, &sW[0][off]);
+            spl_z(z, st[3], wA[0].x);
+        }
+        for (uint32_t k = 0; k < NB; k += 2) {
+            sha_rounds_split(st, wA, wB, &sW[(k + 1) % PC_RING][off], k + 1, k + 1 < NB, &s_ready, k < nbt, c, z);
+            spl_z(z, st[3], wB[0].x);
+            publish(&s_done, k, lane);
+            if (k + 1 >= NB) break;
+            sha_rounds_split(st, wB, wA, &sW[(k + 2) % PC_RING][off], k + 2, k + 2 < NB, &s_ready, k + 1 < nbt, c,
+                             z);
+            spl_z(z, st[3], wA[0].x);
+            publish(&s_done, k + 1, lane);
+        }
+        if (diag && lane == 0) {
+            diag[4 * blockIdx.x + 2] = t_spin;
+            diag[4 * blockIdx.x + 3] = __builtin_amdgcn_s_memtime() - t_start;
+        }
+        if (valid) {  // hi: H0..H3 (bytes 0-15), lo: H4..H7 (bytes 16-31)
+            uint4 *o = reinterpret_cast<uint4 *>(hash_base + ci * stride + (hi ? 0 : 16));
+            *o = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]), __builtin_bswap32(st[2]),
+                            __builtin_bswap32(st[3]));
+        }
     } else {
         uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
                           0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
         uint4 wA[16], wB[16];
-        if (lds_load_acquire(&s_ready) == 0) {
-            const unsigned long long t0 = diag ? __builtin_amdgcn_s_memtime() : 0ull;
-            while (lds_load_acquire(&s_ready) == 0) __builtin_amdgcn_s_sleep(1);
-            if (diag) t_spin += __builtin_amdgcn_s_memtime() - t0;
-        }
+        t_spin += wait_ready(&s_ready, 0, diag != nullptr);
         load_w(wA, &sW[0][lane * PC_ROW]);
         // Every lane runs every block's rounds (lanes whose chunk is done work on stale
         // words and keep their state by select): with part of the wave masked off, the
@@ -375,14 +678,26 @@ size_t sha256_order_tmp_elems(uint64_t max_chunks) { return max_chunks + SHA_NBK
 
 unsigned long long *g_sha_diag = nullptr;  // set by cg_diag_sha_stats (diagnostics only)
 uint32_t g_sha_mode = 0;                    // set by cg_diag_sha_mode (diagnostics only; 0 = product)
+// Split-lane workgroups per launch (32 longest chunks each): one per CU.  Set by
+// cg_diag_sha_split_max (diagnostics; 0 = one lane per chunk everywhere).
+uint32_t g_sha_split_max = 256;
+
+uint32_t sha256_grid(uint64_t max_chunks, uint32_t *nsplit_out) {
+    uint64_t ns = (max_chunks + 31) / 32;
+    if (ns > g_sha_split_max) ns = g_sha_split_max;
+    const uint64_t rest = max_chunks > 32 * ns ? max_chunks - 32 * ns : 0;
+    if (nsplit_out) *nsplit_out = (uint32_t)ns;
+    return (uint32_t)(ns + (rest + 63) / 64);
+}
 
 void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
                    uint64_t max_chunks, uint64_t max_len, uint32_t *d_order_tmp, uint8_t *d_hash_base,
                    size_t hash_stride, hipStream_t st) {
     if (max_chunks == 0) return;
-    const uint32_t nwg = (uint32_t)((max_chunks + 63) / 64);
+    uint32_t nsplit = 0;
+    const uint32_t nwg = sha256_grid(max_chunks, &nsplit);
     const uint32_t *order = nullptr;
-    if (d_order_tmp && nwg > 1) {  // one workgroup has nothing to balance
+    if (d_order_tmp && max_chunks > 32) {  // one workgroup has nothing to balance
         uint32_t shift = 0;
         while ((((max_len + 72) >> 6) >> shift) >= SHA_NBKT - 1) ++shift;
         uint32_t *bkt = d_order_tmp, *ord = d_order_tmp + SHA_NBKT;
@@ -401,7 +716,89 @@ void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
     const size_t pad = nwg <= 256 ? 16384 : 0;
     hipLaunchKernelGGL(k_sha256, dim3(nwg), dim3(128), pad, st, d_data, d_abs,
                        (const DescRaw *)d_desc, d_total, max_chunks, order, d_hash_base, hash_stride, g_sha_diag,
-                       g_sha_mode);
+                       g_sha_mode, nsplit);
 }
+
+// ---------------------------------------------------------------------------
+// Diagnostics: cycles per split round for a lone wave (the same round code the
+// split consumer runs, schedule words held in registers).
+// ---------------------------------------------------------------------------
+__global__ void k_diag_sha_rounds_split(uint32_t iters, uint32_t *out, unsigned long long *cycles) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool hi = (lane >> 2) & 1u;
+    SplitLane c;
+    c.sh1 = hi ? 2u : 6u;
+    c.sh2 = hi ? 13u : 11u;
+    c.sh3 = hi ? 22u : 25u;
+    c.lm = hi ? 0xffffffffu : 0u;
+    asm volatile("" : "+v"(c.sh1), "+v"(c.sh2), "+v"(c.sh3), "+v"(c.lm));
+    uint4 W[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) W[i] = make_uint4(lane * 32 + 4 * i, lane * 32 + 4 * i + 1, lane + i, lane ^ i);
+    uint32_t st[4] = {lane, 1u, 2u, 3u};
+    uint32_t z = 0;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    for (uint32_t it = 0; it < iters; ++it) {
+        uint32_t x0 = st[0], x1 = st[1], x2 = st[2], x3 = st[3];
+        SPL32(0, W)
+        SPL32(32, W)
+        st[0] += x0;
+        st[1] += x1;
+        st[2] += x2;
+        st[3] += x3;
+        spl_z(z, st[3], W[0].x);
+    }
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    out[blockIdx.x * blockDim.x + threadIdx.x] = st[0] ^ st[1] ^ st[2] ^ st[3];
+    if (lane == 0) cycles[blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)] = t1 - t0;
+}
+
+// DPP lane probe: v_add_u32_dpp row_shl:4 with bank_mask 0x5 (the split round's lo
+// write): lanes of banks 0/2 get (1000 + lane + 4) + lane, banks 1/3 keep lane.
+__global__ void k_diag_dpp_probe(uint32_t *out) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t a = 1000u + lane;
+    uint32_t b = lane;
+    asm volatile("s_nop 1\n\tv_add_u32_dpp %0, %1, %0 row_shl:4 row_mask:0xf bank_mask:0x5" : "+v"(b) : "v"(a));
+    out[lane] = b;
+}
+
+}  // namespace cg
+
+extern "C" int cg_diag_sha_rounds_split(uint32_t iters, uint32_t blocks, uint32_t threads,
+                                        unsigned long long *h_cycles) {
+    uint32_t *d_out = nullptr;
+    unsigned long long *d_cyc = nullptr;
+    const uint32_t waves = blocks * (threads / 64);
+    if (hipMalloc(&d_out, (size_t)blocks * threads * 4) != hipSuccess) return 2;
+    if (hipMalloc(&d_cyc, waves * 8) != hipSuccess) return 2;
+    hipLaunchKernelGGL(cg::k_diag_sha_rounds_split, dim3(blocks), dim3(threads), 0, 0, iters, d_out, d_cyc);
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(h_cycles, d_cyc, waves * 8, hipMemcpyDeviceToHost);
+    (void)hipFree(d_out);
+    (void)hipFree(d_cyc);
+    return e == hipSuccess ? 0 : 2;
+}
+
+extern "C" int cg_diag_dpp_probe(uint32_t *h_out) {
+    uint32_t *d = nullptr;
+    if (hipMalloc(&d, 256) != hipSuccess) return 2;
+    hipLaunchKernelGGL(cg::k_diag_dpp_probe, dim3(1), dim3(64), 0, 0, d);
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(h_out, d, 256, hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    return e == hipSuccess ? 0 : 2;
+}
+
+extern "C" uint32_t cg_diag_sha_split_max(uint32_t v) {
+    const uint32_t old = cg::g_sha_split_max;
+    cg::g_sha_split_max = v;
+    return old;
+}
+
+// workgroups the digest launch uses for `max_chunks` (diagnostics: sizes cg_diag_sha_stats)
+extern "C" uint32_t cg_diag_sha_grid(uint64_t max_chunks) { return cg::sha256_grid(max_chunks, nullptr); }
+
+namespace cg {
 
 }  // namespace cg

@@ -6,6 +6,7 @@ tests/proptest_suite.rs, fuzz/fuzz_targets/chunking.rs) plus edge cases of the
 GPU design (segment/halo seams, dense candidate segments, unaligned chunk
 starts, empty and ragged NARs, digest padding boundaries).
 """
+import ctypes
 import hashlib
 import io
 import os
@@ -293,6 +294,59 @@ def test_digest_spans_all_lengths(ca, O):
             span = data[a:a + n].tobytes()
             want = hashlib.sha256(span).digest() if algo == SHA else O.blake3(span)
             assert bytes(dig[k]) == want, (algo, n, a)
+
+
+def _sha_split_max(ca, v):
+    f = ca.lib.cg_diag_sha_split_max
+    f.argtypes = [ctypes.c_uint32]
+    f.restype = ctypes.c_uint32
+    return f(v)
+
+
+def test_dpp_bank_mask_lane_probe(ca):
+    """The split-lane SHA-256 rounds pair lanes 4 apart in a DPP row: a row_shl:4 add
+    with bank_mask 0x5 writes lanes 0-3 and 8-11 of each row from lanes 4-7 / 12-15
+    and leaves the others untouched."""
+    ca.lib.cg_diag_dpp_probe.argtypes = [ctypes.c_void_p]
+    out = np.zeros(64, np.uint32)
+    assert ca.lib.cg_diag_dpp_probe(out.ctypes.data) == 0
+    want = [(1000 + 2 * L + 4) if ((L >> 2) & 1) == 0 else L for L in range(64)]
+    assert out.tolist() == want
+
+
+@pytest.mark.parametrize("split_max", [0, 3, 1 << 20], ids=["one_lane", "mixed", "split"])
+def test_sha_workgroup_kinds_agree(ca, O, split_max):
+    """k_sha256 runs the longest chunks on split-lane workgroups (a round spread over
+    a lane pair) and the rest one chunk per lane; every mix gives hashlib's digests,
+    over every padding boundary, unaligned starts and multi-block chunks."""
+    import torch
+
+    prev = _sha_split_max(ca, split_max)
+    try:
+        rng = np.random.default_rng(17)
+        data = rng.integers(0, 256, 3 << 20, dtype=np.uint8)
+        lens = list(range(0, 200)) + [511, 512, 513, 4095, 4096, 4097, 65537, 1 << 20, (1 << 20) + 3, 2_000_001]
+        offs = [int(rng.integers(0, len(data) - n + 1)) for n in lens]
+        d = torch.from_numpy(data).cuda()
+        o = torch.tensor(offs, dtype=torch.int64).cuda()
+        ln = torch.tensor(lens, dtype=torch.int64).cuda()
+        dig = torch.zeros(len(lens) * 32, dtype=torch.uint8, device="cuda")
+        assert ca.lib.cg_hash_spans_device(d.data_ptr(), o.data_ptr(), ln.data_ptr(), len(lens), SHA,
+                                           dig.data_ptr(), None) == 0
+        dig = dig.cpu().numpy().reshape(-1, 32)
+        for k, (a, n) in enumerate(zip(offs, lens)):
+            assert bytes(dig[k]) == hashlib.sha256(data[a:a + n].tobytes()).digest(), (split_max, n, a)
+        # and through the whole pipeline
+        from chunker_amd.nar import synth_nars
+
+        sizes = [1024 * 1024 + 8 * k for k in range(6)]
+        nd, no = synth_nars(sizes, first_index=3)
+        nars = [nd[no[i]:no[i + 1]] for i in range(len(sizes))]
+        got = ca.chunk_batch(nars, 4096, 16384, 65536)
+        for i, nar in enumerate(nars):
+            assert_same(got[i], O.chunk_descriptors(nar, 4096, 16384, 65536, algo=SHA), f"nar{i}")
+    finally:
+        _sha_split_max(ca, prev)
 
 
 @pytest.mark.slow
