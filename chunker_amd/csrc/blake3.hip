@@ -28,16 +28,45 @@ static constexpr uint32_t B3_IV[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54f
 
 __device__ __forceinline__ uint32_t rotr32b(uint32_t x, uint32_t n) { return __builtin_amdgcn_alignbit(x, x, n); }
 
-#define B3_G(a, b, c, d, x, y)            \
-    {                                     \
-        v[a] = v[a] + v[b] + (x);         \
-        v[d] = rotr32b(v[d] ^ v[a], 16);  \
-        v[c] = v[c] + v[d];               \
-        v[b] = rotr32b(v[b] ^ v[c], 12);  \
-        v[a] = v[a] + v[b] + (y);         \
-        v[d] = rotr32b(v[d] ^ v[a], 8);   \
-        v[c] = v[c] + v[d];               \
-        v[b] = rotr32b(v[b] ^ v[c], 7);   \
+
+// The four G functions of a column (or diagonal) step are independent, each a
+// strictly serial chain of 12 VALU ops (2 v_add3, 2 v_add, 4 xor, 4 v_alignbit: no
+// shorter form exists on gfx950).  They are interleaved op by op so that each op's
+// producer is 4 instructions back.
+#define B3_G4(a0, b0, c0, d0, a1, b1, c1, d1, a2, b2, c2, d2, a3, b3, c3, d3, mi)                                   \
+    {                                                                                                               \
+        v[a0] = v[a0] + v[b0] + m[mi[0]];                                                                           \
+        v[a1] = v[a1] + v[b1] + m[mi[2]];                                                                           \
+        v[a2] = v[a2] + v[b2] + m[mi[4]];                                                                           \
+        v[a3] = v[a3] + v[b3] + m[mi[6]];                                                                           \
+        v[d0] = rotr32b(v[d0] ^ v[a0], 16);                                                                         \
+        v[d1] = rotr32b(v[d1] ^ v[a1], 16);                                                                         \
+        v[d2] = rotr32b(v[d2] ^ v[a2], 16);                                                                         \
+        v[d3] = rotr32b(v[d3] ^ v[a3], 16);                                                                         \
+        v[c0] = v[c0] + v[d0];                                                                                      \
+        v[c1] = v[c1] + v[d1];                                                                                      \
+        v[c2] = v[c2] + v[d2];                                                                                      \
+        v[c3] = v[c3] + v[d3];                                                                                      \
+        v[b0] = rotr32b(v[b0] ^ v[c0], 12);                                                                         \
+        v[b1] = rotr32b(v[b1] ^ v[c1], 12);                                                                         \
+        v[b2] = rotr32b(v[b2] ^ v[c2], 12);                                                                         \
+        v[b3] = rotr32b(v[b3] ^ v[c3], 12);                                                                         \
+        v[a0] = v[a0] + v[b0] + m[mi[1]];                                                                           \
+        v[a1] = v[a1] + v[b1] + m[mi[3]];                                                                           \
+        v[a2] = v[a2] + v[b2] + m[mi[5]];                                                                           \
+        v[a3] = v[a3] + v[b3] + m[mi[7]];                                                                           \
+        v[d0] = rotr32b(v[d0] ^ v[a0], 8);                                                                          \
+        v[d1] = rotr32b(v[d1] ^ v[a1], 8);                                                                          \
+        v[d2] = rotr32b(v[d2] ^ v[a2], 8);                                                                          \
+        v[d3] = rotr32b(v[d3] ^ v[a3], 8);                                                                          \
+        v[c0] = v[c0] + v[d0];                                                                                      \
+        v[c1] = v[c1] + v[d1];                                                                                      \
+        v[c2] = v[c2] + v[d2];                                                                                      \
+        v[c3] = v[c3] + v[d3];                                                                                      \
+        v[b0] = rotr32b(v[b0] ^ v[c0], 7);                                                                          \
+        v[b1] = rotr32b(v[b1] ^ v[c1], 7);                                                                          \
+        v[b2] = rotr32b(v[b2] ^ v[c2], 7);                                                                          \
+        v[b3] = rotr32b(v[b3] ^ v[c3], 7);                                                                          \
     }
 
 // Compress one block; returns the new chaining value in cv (first 8 output words).
@@ -48,14 +77,8 @@ __device__ __forceinline__ void b3_compress(uint32_t cv[8], const uint32_t m[16]
                       blen, flags};
 #pragma unroll
     for (int r = 0; r < 7; ++r) {
-        B3_G(0, 4, 8, 12, m[B3S.s[r][0]], m[B3S.s[r][1]]);
-        B3_G(1, 5, 9, 13, m[B3S.s[r][2]], m[B3S.s[r][3]]);
-        B3_G(2, 6, 10, 14, m[B3S.s[r][4]], m[B3S.s[r][5]]);
-        B3_G(3, 7, 11, 15, m[B3S.s[r][6]], m[B3S.s[r][7]]);
-        B3_G(0, 5, 10, 15, m[B3S.s[r][8]], m[B3S.s[r][9]]);
-        B3_G(1, 6, 11, 12, m[B3S.s[r][10]], m[B3S.s[r][11]]);
-        B3_G(2, 7, 8, 13, m[B3S.s[r][12]], m[B3S.s[r][13]]);
-        B3_G(3, 4, 9, 14, m[B3S.s[r][14]], m[B3S.s[r][15]]);
+        B3_G4(0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14, 3, 7, 11, 15, B3S.s[r]);
+        B3_G4(0, 5, 10, 15, 1, 6, 11, 12, 2, 7, 8, 13, 3, 4, 9, 14, (B3S.s[r] + 8));
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) cv[i] = v[i] ^ v[i + 8];
@@ -75,23 +98,52 @@ __device__ __forceinline__ void b3_parent(const uint32_t *l, const uint32_t *r, 
 }
 
 // Leaf of `n` (0..1024) bytes at p with leaf index ctr.  Words are little-endian;
-// p may be unaligned (v_alignbyte realigns aligned dword loads).
+// p may be unaligned (v_alignbyte realigns dword-aligned loads).  Blocks lying
+// wholly inside the leaf are fetched as four 16-byte loads (+ the dword after them
+// when p is unaligned), one block ahead of the compression that uses them (the lanes
+// of a wave sit 1 KiB apart, each on its own cache line).  With loads removed
+// altogether (NOLOAD) the kernel is only ~10 % faster: it is bound by the ~700 VALU
+// of each compression (scripts/diag_b3.py).
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+// NOLOAD (diagnostics only): compress lane-dependent register words instead of
+// loading the leaf, to time the compression alone.
+template <bool NOLOAD = false>
 __device__ __forceinline__ void b3_leaf(const uint8_t *p, uint32_t n, uint64_t ctr, bool root, uint32_t cv[8]) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) cv[i] = B3_IV[i];
     const uint32_t shift = (uint32_t)((uintptr_t)p & 3u);
     const uint32_t *base = reinterpret_cast<const uint32_t *>(p - shift);
     const uint32_t nblk = n ? (n + 63) / 64 : 1;
+    const uint32_t nfull = n / 64;  // blocks with all 64 bytes inside the leaf
     const uint8_t *endp = p + n;
+    u32x4_a4 nx[4];
+    uint32_t nx16 = 0;
+    auto fetch = [&](uint32_t j) {
+        const uint32_t *q = base + 16 * j;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) nx[i] = *reinterpret_cast<const u32x4_a4 *>(q + 4 * i);
+        // the dword after the block starts inside the leaf whenever shift != 0
+        nx16 = shift ? q[16] : 0u;
+    };
+    if (!NOLOAD && nfull) fetch(0);
     for (uint32_t j = 0; j < nblk; ++j) {
         const uint32_t *q = base + 16 * j;
         const bool last = j + 1 == nblk;
         const uint32_t blen = last ? n - 64 * j : 64u;
         uint32_t dw[17], m[16];
-        if (!last) {
+        if (NOLOAD) {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) dw[i] = q[i];
-            dw[16] = shift ? q[16] : 0u;
+            for (int i = 0; i < 16; ++i) m[i] = (uint32_t)ctr * 0x9E3779B9u + (uint32_t)(i * 0x01010101) + j;
+        } else if (j < nfull) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                dw[4 * i] = nx[i].x;
+                dw[4 * i + 1] = nx[i].y;
+                dw[4 * i + 2] = nx[i].z;
+                dw[4 * i + 3] = nx[i].w;
+            }
+            dw[16] = nx16;
+            if (!NOLOAD && j + 1 < nfull) fetch(j + 1);
 #pragma unroll
             for (int i = 0; i < 16; ++i) m[i] = __builtin_amdgcn_alignbyte(dw[i + 1], dw[i], shift);
         } else {
@@ -153,28 +205,32 @@ __device__ __forceinline__ void b3_wave_fold(uint32_t cv[8], uint32_t count, boo
 
 #define B3_WAVES 4u
 
+// group -> chunk map: thread c writes c into its chunk's group slots
+__global__ __launch_bounds__(256) void k_b3_map(const uint64_t *__restrict__ group_base,
+                                                const uint64_t *__restrict__ total_p, uint64_t max_chunks,
+                                                uint32_t *__restrict__ gmap) {
+    uint64_t total = *total_p;
+    if (total > max_chunks) total = max_chunks;
+    const uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c >= total) return;
+    for (uint64_t g = group_base[c]; g < group_base[c + 1]; ++g) gmap[g] = (uint32_t)c;
+}
+
 // One wave per 64-leaf group (4 waves per workgroup for occupancy).
+template <bool NOLOAD = false>
 __global__ __launch_bounds__(64 * B3_WAVES) void k_b3_groups(const uint8_t *__restrict__ data,
                                                              const uint64_t *__restrict__ abs,
                                                              const DescRaw *__restrict__ desc,
                                                              const uint64_t *__restrict__ total_p, uint64_t max_chunks,
                                                              const uint64_t *__restrict__ group_base,
+                                                             const uint32_t *__restrict__ gmap,
                                                              uint8_t *__restrict__ hash_base, size_t stride,
                                                              uint32_t *__restrict__ gcv) {
     uint64_t total = *total_p;
     if (total > max_chunks) total = max_chunks;
     const uint64_t G = (uint64_t)blockIdx.x * B3_WAVES + (threadIdx.x >> 6);
     if (G >= group_base[total]) return;
-    // chunk c with group_base[c] <= G < group_base[c+1]
-    uint64_t lo = 0, hi = total;
-    while (hi - lo > 1) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (group_base[mid] <= G)
-            lo = mid;
-        else
-            hi = mid;
-    }
-    const uint64_t c = lo;
+    const uint64_t c = gmap[G];  // chunk c with group_base[c] <= G < group_base[c+1]
     const uint64_t len = desc[c].length;
     const uint64_t gi = G - group_base[c];
     const uint64_t ngroups = group_base[c + 1] - group_base[c];
@@ -187,7 +243,7 @@ __global__ __launch_bounds__(64 * B3_WAVES) void k_b3_groups(const uint8_t *__re
     if (lane < count0) {
         const uint64_t off = leaf * 1024;
         const uint32_t n = (uint32_t)((len - off) < 1024 ? (len - off) : 1024);
-        b3_leaf(chunk + off, len ? n : 0u, leaf, leaves == 1, cv);
+        b3_leaf<NOLOAD>(chunk + off, len ? n : 0u, leaf, leaves == 1, cv);
     }
     if (leaves == 1) {
         if (lane == 0) store_digest(hash_base + c * stride, cv);
@@ -268,20 +324,24 @@ __global__ __launch_bounds__(64) void k_b3_top(const DescRaw *__restrict__ desc,
     if (lane == 0) store_digest(hash_base + c * stride, cv);
 }
 
+uint32_t g_b3_diag = 0;  // set by cg_diag_b3_mode (diagnostics only; 0 = product)
+
 size_t blake3_group_bound(uint64_t total_bytes, uint64_t max_chunks) { return total_bytes / 65536 + max_chunks + 1; }
 
 void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
                    uint64_t max_chunks, uint64_t total_bytes, uint8_t *d_hash_base, size_t hash_stride,
-                   uint64_t * /*unused*/, uint64_t *d_group_base, uint32_t *d_gcount_u32, uint64_t *d_scan_tmp,
+                   uint32_t *d_gmap, uint64_t *d_group_base, uint32_t *d_gcount_u32, uint64_t *d_scan_tmp,
                    uint32_t *d_gcv, hipStream_t st) {
     if (max_chunks == 0) return;
     const DescRaw *desc = (const DescRaw *)d_desc;
-    hipLaunchKernelGGL(k_b3_count, dim3((uint32_t)((max_chunks + 255) / 256)), dim3(256), 0, st, desc, d_total,
-                       max_chunks, d_gcount_u32);
+    const uint32_t cblocks = (uint32_t)((max_chunks + 255) / 256);
+    hipLaunchKernelGGL(k_b3_count, dim3(cblocks), dim3(256), 0, st, desc, d_total, max_chunks, d_gcount_u32);
     launch_exclusive_scan_u32(d_gcount_u32, d_group_base, max_chunks, 0, d_scan_tmp, st);
+    hipLaunchKernelGGL(k_b3_map, dim3(cblocks), dim3(256), 0, st, d_group_base, d_total, max_chunks, d_gmap);
     const uint64_t gbound = blake3_group_bound(total_bytes, max_chunks);
-    hipLaunchKernelGGL(k_b3_groups, dim3((uint32_t)((gbound + B3_WAVES - 1) / B3_WAVES)), dim3(64 * B3_WAVES), 0, st, d_data, d_abs, desc, d_total,
-                       max_chunks, d_group_base, d_hash_base, hash_stride, d_gcv);
+    hipLaunchKernelGGL(g_b3_diag ? k_b3_groups<true> : k_b3_groups<false>,
+                       dim3((uint32_t)((gbound + B3_WAVES - 1) / B3_WAVES)), dim3(64 * B3_WAVES), 0, st, d_data, d_abs, desc, d_total, max_chunks, d_group_base, d_gmap, d_hash_base, hash_stride,
+                       d_gcv);
     hipLaunchKernelGGL(k_b3_top, dim3((uint32_t)max_chunks), dim3(64), 0, st, desc, d_total, max_chunks,
                        d_group_base, d_gcv, d_hash_base, hash_stride);
 }

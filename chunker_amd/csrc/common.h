@@ -61,7 +61,7 @@ size_t sha256_order_tmp_elems(uint64_t max_chunks);
 
 void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
                    uint64_t max_chunks, uint64_t total_bytes, uint8_t *d_hash_base, size_t hash_stride,
-                   uint64_t *d_group_count_tmp, uint64_t *d_group_base, uint32_t *d_gcount_u32,
+                   uint32_t *d_gmap, uint64_t *d_group_base, uint32_t *d_gcount_u32,
                    uint64_t *d_scan_tmp, uint32_t *d_gcv, hipStream_t st);
 size_t blake3_group_bound(uint64_t total_bytes, uint64_t max_chunks);
 

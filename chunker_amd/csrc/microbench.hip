@@ -140,6 +140,11 @@ namespace cg {
 extern uint32_t g_scan_diag;
 }
 extern "C" void cg_diag_scan_mode(uint32_t mode) { cg::g_scan_diag = mode; }
+namespace cg {
+extern uint32_t g_b3_diag;
+}
+// 1 = BLAKE3 leaves compress register words without loading them (digests garbage)
+extern "C" void cg_diag_b3_mode(uint32_t mode) { cg::g_b3_diag = mode; }
 // Enable (n_wg > 0) / read back / disable (n_wg == 0) per-workgroup SHA producer and
 // consumer timing: out[4*wg + {0,1,2,3}] = producer spin, producer total, consumer
 // spin, consumer total (shader clocks).  Diagnostics only.

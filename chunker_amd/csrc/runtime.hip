@@ -124,7 +124,7 @@ struct Workspace {
     hipStream_t stream = nullptr;
     uint64_t gear_epoch = 0;
     DevBuf gear, seg_count, seg_cand, eoff, scan_tmp, entries, nar_off, cap_base, wchunk, nar_nchunks, nar_first,
-        chunk_abs, b3_gcount, b3_gbase, b3_gcv, in, out, span_off, span_len, order;
+        chunk_abs, b3_gcount, b3_gbase, b3_gcv, b3_gmap, in, out, span_off, span_len, order;
     PinBuf stage;
     hipEvent_t ev[EV_N] = {};
     int init(int dev) {
@@ -307,6 +307,7 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
         if ((rc = ws->b3_gcount.ensure((chunk_bound + 1) * 4, "b3_gcount"))) return rc;
         if ((rc = ws->b3_gbase.ensure((chunk_bound + 1) * 8, "b3_gbase"))) return rc;
         if ((rc = ws->b3_gcv.ensure((cg::blake3_group_bound(total_len, chunk_bound) + 1) * 32, "b3_gcv"))) return rc;
+        if ((rc = ws->b3_gmap.ensure((cg::blake3_group_bound(total_len, chunk_bound) + 1) * 4, "b3_gmap"))) return rc;
     }
 
     const bool prof = g_profiling.load() != 0;
@@ -339,8 +340,8 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
                           ws->order.as<uint32_t>(), hash_base, sizeof(cg_desc), st);
     } else {
         cg::launch_blake3(d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, total_len, hash_base,
-                          sizeof(cg_desc), nullptr, ws->b3_gbase.as<uint64_t>(), ws->b3_gcount.as<uint32_t>(),
-                          ws->scan_tmp.as<uint64_t>(), ws->b3_gcv.as<uint32_t>(), st);
+                          sizeof(cg_desc), ws->b3_gmap.as<uint32_t>(), ws->b3_gbase.as<uint64_t>(),
+                          ws->b3_gcount.as<uint32_t>(), ws->scan_tmp.as<uint64_t>(), ws->b3_gcv.as<uint32_t>(), st);
     }
     if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_DIGEST], st));
     HIP_TRY(hipGetLastError());
@@ -414,8 +415,9 @@ int hash_spans(Workspace *ws, const uint8_t *d_data, const uint64_t *d_offsets, 
         if ((rc = ws->b3_gcount.ensure((n + 1) * 4, "b3_gcount"))) return rc;
         if ((rc = ws->b3_gbase.ensure((n + 1) * 8, "b3_gbase"))) return rc;
         if ((rc = ws->b3_gcv.ensure((gb + 1) * 32, "b3_gcv"))) return rc;
+        if ((rc = ws->b3_gmap.ensure((gb + 1) * 4, "b3_gmap"))) return rc;
         cg::launch_blake3(d_data, ws->chunk_abs.as<uint64_t>(), ws->out.p, d_total, n, tb, hb, sizeof(cg_desc),
-                          nullptr, ws->b3_gbase.as<uint64_t>(), ws->b3_gcount.as<uint32_t>(),
+                          ws->b3_gmap.as<uint32_t>(), ws->b3_gbase.as<uint64_t>(), ws->b3_gcount.as<uint32_t>(),
                           ws->scan_tmp.as<uint64_t>(), ws->b3_gcv.as<uint32_t>(), st);
     }
     HIP_TRY(hipMemcpy2DAsync(d_digests, 32, hb, sizeof(cg_desc), 32, n, hipMemcpyDeviceToDevice, st));
