@@ -336,7 +336,9 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
     uint8_t *hash_base = reinterpret_cast<uint8_t *>(d_out) + offsetof(cg_desc, hash);
     if (algo == CG_SHA256) {
         if ((rc = ws->order.ensure(cg::sha256_order_tmp_elems(chunk_bound) * 4, "order"))) return rc;
-        cg::launch_sha256(d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, o.max,
+        // expected chunk count: FastCDC's mean chunk is about min + avg on random data
+        const uint64_t expected = std::min<uint64_t>(chunk_bound, total_len / (o.min + o.avg) + n_nars);
+        cg::launch_sha256(d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, expected, o.max,
                           ws->order.as<uint32_t>(), hash_base, sizeof(cg_desc), st);
     } else {
         cg::launch_blake3(d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, total_len, hash_base,
@@ -406,7 +408,7 @@ int hash_spans(Workspace *ws, const uint8_t *d_data, const uint64_t *d_offsets, 
     if (algo == CG_SHA256) {
         // spans are not bounded by a max_size: bucket for the ABI's 16 MiB span cap
         if ((rc = ws->order.ensure(cg::sha256_order_tmp_elems(n) * 4, "order"))) return rc;
-        cg::launch_sha256(d_data, ws->chunk_abs.as<uint64_t>(), ws->out.p, d_total, n, MAXIMUM_MAX,
+        cg::launch_sha256(d_data, ws->chunk_abs.as<uint64_t>(), ws->out.p, d_total, n, n, MAXIMUM_MAX,
                           ws->order.as<uint32_t>(), hb, sizeof(cg_desc), st);
     } else {
         // group-grid bound without reading lengths back: spans are capped at 16 MiB each

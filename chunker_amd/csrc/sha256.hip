@@ -355,6 +355,44 @@ __device__ __forceinline__ void spl_round8(uint32_t &x0, uint32_t &x1, uint32_t 
     }
 }
 
+// Quad variant (8 lanes per chunk): each half of the pair is replicated over the 4
+// lanes of a DPP bank (lanes 0-2 compute; lane 3 runs isolated garbage).  Sigma
+// then takes ONE v_alignbit (per-lane amount, lanes 0-2) and two v_xor_b32 with
+// quad_perm rotations of the three rotations, so a round is 9 VALU.  The other
+// steps, the bank masks and the schedule words are those of the pair round.
+#define QR(A, B, C, D, ZOP)                                                               \
+    "v_alignbit_b32 %[r1], %[" #A "], %[" #A "], %[s1]\n\t"                               \
+    "v_bitop3_b32 %[xx], %[" #A "], %[" #C "], %[lm] bitop3:0x78\n\t"                     \
+    "v_bitop3_b32 %[f], %[xx], %[" #B "], %[" #C "] bitop3:0xca\n\t"                      \
+    "v_xor_b32_dpp %[r2], %[r1], %[r1] quad_perm:[1,2,0,3] row_mask:0xf bank_mask:0xf\n\t" \
+    "v_xor_b32_dpp %[s], %[r1], %[r2] quad_perm:[2,0,1,3] row_mask:0xf bank_mask:0xf\n\t"  \
+    "v_add3_u32 %[p], %[z], %[s], %[f]\n\t"                                               \
+    "v_add_u32_dpp %[" #D "], %[" #D "], %[p] row_shl:4 row_mask:0xf bank_mask:0x5\n\t"   \
+    ZOP "v_add_u32_dpp %[" #D "], %[p], %[p] row_shr:4 row_mask:0xf bank_mask:0xa\n\t"
+#define QR8_HEAD                                                                       \
+    QR(x0, x1, x2, x3, ZHI(x2, w0)) QR(x3, x0, x1, x2, ZLO(x1, w1)) QR(x2, x3, x0, x1, ZHI(x0, w1)) \
+    QR(x1, x2, x3, x0, ZLO(x3, w2)) QR(x0, x1, x2, x3, ZHI(x2, w2)) QR(x3, x0, x1, x2, ZLO(x1, w3)) \
+    QR(x2, x3, x0, x1, ZHI(x0, w3))
+#define QR8_OUTS                                                                                              \
+    [x0] "+v"(x0), [x1] "+v"(x1), [x2] "+v"(x2), [x3] "+v"(x3), [z] "+v"(z), [r1] "=&v"(r1), [r2] "=&v"(r2),  \
+        [xx] "=&v"(xx), [s] "=&v"(s), [f] "=&v"(f), [p] "=&v"(p)
+#define QR8_INS                                                                                  \
+    [s1] "v"(c.sh1), [lm] "v"(c.lm), [w0] "v"(w_at<T / 2>(W)), [w1] "v"(w_at<T / 2 + 1>(W)),     \
+        [w2] "v"(w_at<T / 2 + 2>(W)), [w3] "v"(w_at<T / 2 + 3>(W))
+
+template <int T>
+__device__ __forceinline__ void quad_round8(uint32_t &x0, uint32_t &x1, uint32_t &x2, uint32_t &x3, uint32_t &z,
+                                            const uint4 (&W)[8], const SplitLane &c) {
+    uint32_t r1, r2, xx, s, f, p;
+    if constexpr (T + 8 < 64) {
+        asm volatile(QR8_HEAD QR(x1, x2, x3, x0, ZLO(x3, w4))
+                     : QR8_OUTS
+                     : QR8_INS, [w4] "v"(w_at<T / 2 + 4>(W)));
+    } else {
+        asm volatile(QR8_HEAD QR(x1, x2, x3, x0, ZNONE) : QR8_OUTS : QR8_INS);
+    }
+}
+
 // Z for round 0 of the next block: h (lo's X3 after the state add) + W[0]+K[0], lo lanes only.
 __device__ __forceinline__ void spl_z(uint32_t &z, uint32_t h, uint32_t wv0) {
     asm volatile("s_nop 1\n\tv_add_u32_dpp %0, %1, %2 quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x5"
@@ -362,11 +400,19 @@ __device__ __forceinline__ void spl_z(uint32_t &z, uint32_t h, uint32_t wv0) {
                  : "v"(h), "v"(wv0));
 }
 
-#define SPL32(T, W)                                \
-    spl_round8<(T)>(x0, x1, x2, x3, z, W, c);      \
-    spl_round8<(T) + 8>(x0, x1, x2, x3, z, W, c);  \
-    spl_round8<(T) + 16>(x0, x1, x2, x3, z, W, c); \
-    spl_round8<(T) + 24>(x0, x1, x2, x3, z, W, c);
+template <bool QUAD, int T>
+__device__ __forceinline__ void round8(uint32_t &x0, uint32_t &x1, uint32_t &x2, uint32_t &x3, uint32_t &z,
+                                       const uint4 (&W)[8], const SplitLane &c) {
+    if constexpr (QUAD)
+        quad_round8<T>(x0, x1, x2, x3, z, W, c);
+    else
+        spl_round8<T>(x0, x1, x2, x3, z, W, c);
+}
+#define SPL32(T, W)                                         \
+    round8<QUAD, (T)>(x0, x1, x2, x3, z, W, c);             \
+    round8<QUAD, (T) + 8>(x0, x1, x2, x3, z, W, c);         \
+    round8<QUAD, (T) + 16>(x0, x1, x2, x3, z, W, c);        \
+    round8<QUAD, (T) + 24>(x0, x1, x2, x3, z, W, c);
 
 __device__ __forceinline__ void load_w8(uint4 (&w)[8], const uint32_t *row) {
 #pragma unroll
@@ -375,6 +421,7 @@ __device__ __forceinline__ void load_w8(uint4 (&w)[8], const uint32_t *row) {
 
 // 64 split rounds on `cur` (this lane's 32 schedule words); half-way through, once
 // the producer has published block `knext`, the next block's words are read into `nxt`.
+template <bool QUAD>
 __device__ __forceinline__ void sha_rounds_split(uint32_t st[4], const uint4 (&cur)[8], uint4 (&nxt)[8],
                                                  const uint32_t *next_row, uint32_t knext, bool prefetch,
                                                  const uint32_t *ready, bool active, const SplitLane &c,
@@ -477,8 +524,53 @@ __device__ unsigned long long sha_produce_pair(const uint8_t *p, uint64_t len, u
     return t_spin;
 }
 
-// Workgroups [0, nsplit) take 32 chunks each, one per lane pair (the length order
-// puts the longest chunks there); the rest take 64 chunks, one per lane.
+// Consumer wave of a pair (QUAD = false: lo/hi = banks 0,2 / 1,3 of a DPP row, one
+// lane each) or quad (QUAD = true: the same banks, 4 lanes each) workgroup.
+template <bool QUAD>
+__device__ void split_consumer(uint32_t (*sW)[64 * PC_ROW], uint32_t row, bool hi, uint32_t lane, uint32_t NB,
+                               uint32_t nbt, uint32_t *s_ready, uint32_t *s_done, uint32_t st[4],
+                               unsigned long long *t_spin, bool timed) {
+    SplitLane c;
+    if (QUAD) {  // lanes 0-2 of a bank take one rotation each; lane 3 is idle garbage
+        const uint32_t q = lane & 3u;
+        c.sh1 = hi ? (q == 0 ? 2u : q == 1 ? 13u : q == 2 ? 22u : 0u) : (q == 0 ? 6u : q == 1 ? 11u : q == 2 ? 25u : 0u);
+        c.sh2 = c.sh3 = 0;
+    } else {
+        c.sh1 = hi ? 2u : 6u;
+        c.sh2 = hi ? 13u : 11u;
+        c.sh3 = hi ? 22u : 25u;
+    }
+    c.lm = hi ? 0xffffffffu : 0u;
+    asm volatile("" : "+v"(c.sh1), "+v"(c.sh2), "+v"(c.sh3), "+v"(c.lm));
+    st[0] = hi ? 0x6a09e667u : 0x510e527fu;
+    st[1] = hi ? 0xbb67ae85u : 0x9b05688cu;
+    st[2] = hi ? 0x3c6ef372u : 0x1f83d9abu;
+    st[3] = hi ? 0xa54ff53au : 0x5be0cd19u;
+    uint32_t z = 0;  // stays 0 in hi lanes: every write to it is masked to lo lanes
+    uint4 wA[8], wB[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) wA[i] = wB[i] = make_uint4(0u, 0u, 0u, 0u);
+    const uint32_t off = row * PC_ROW + (hi ? 32u : 0u);
+    if (NB > 0) {
+        *t_spin += wait_ready(s_ready, 0, timed);
+        load_w8(wA, &sW[0][off]);
+        spl_z(z, st[3], wA[0].x);
+    }
+    for (uint32_t k = 0; k < NB; k += 2) {
+        sha_rounds_split<QUAD>(st, wA, wB, &sW[(k + 1) % PC_RING][off], k + 1, k + 1 < NB, s_ready, k < nbt, c, z);
+        spl_z(z, st[3], wB[0].x);
+        publish(s_done, k, lane);
+        if (k + 1 >= NB) break;
+        sha_rounds_split<QUAD>(st, wB, wA, &sW[(k + 2) % PC_RING][off], k + 2, k + 2 < NB, s_ready, k + 1 < nbt, c,
+                               z);
+        spl_z(z, st[3], wA[0].x);
+        publish(s_done, k + 1, lane);
+    }
+}
+
+// Workgroup kinds, longest chunks first (the length order): [0, nquad) take 8 chunks
+// on 8 lanes each, [nquad, nquad + npair) 32 chunks on lane pairs, the rest 64
+// chunks on one lane each.  The quad and pair kinds share the pair producer.
 // diag (optional, nullptr in production): per workgroup {producer spin, producer
 // total, consumer spin, consumer total} in shader clocks (s_memtime).
 __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data, const uint64_t *__restrict__ abs,
@@ -486,16 +578,26 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
                                                uint64_t max_chunks, const uint32_t *__restrict__ order,
                                                uint8_t *__restrict__ hash_base, size_t stride,
                                                unsigned long long *__restrict__ diag, uint32_t mode,
-                                               uint32_t nsplit) {
+                                               uint32_t nquad, uint32_t npair) {
     unsigned long long t_start = diag ? __builtin_amdgcn_s_memtime() : 0ull, t_spin = 0;
     __shared__ __attribute__((aligned(16))) uint32_t sW[PC_RING][64 * PC_ROW];
     __shared__ uint32_t s_ready, s_done;  // blocks filled by the producer / consumed by the consumer
     const uint32_t lane = threadIdx.x & 63u;
     const bool producer = threadIdx.x < 64;
-    const bool split = blockIdx.x < nsplit;
-    const uint64_t wg_base = split ? 32ull * blockIdx.x : 32ull * nsplit + 64ull * (blockIdx.x - nsplit);
+    const uint32_t b = blockIdx.x;
+    const bool quad = b < nquad;
+    const bool split = b < nquad + npair;  // quad or pair
+    const uint64_t wg_base = quad    ? 8ull * b
+                             : split ? 8ull * nquad + 32ull * (b - nquad)
+                                     : 8ull * nquad + 32ull * npair + 64ull * (b - nquad - npair);
+    const uint32_t wg_chunks = quad ? 8u : split ? 32u : 64u;
     const bool hi = split && ((lane >> 2) & 1u);
-    const uint32_t slot = split ? split_slot(lane) : lane;
+    // the producer of a quad or pair workgroup pairs lanes as split_slot does (a quad
+    // workgroup uses its first 16 lanes); a quad consumer gives chunk j lanes
+    // 16r + 8h + 0..7 with j = 2r + h
+    const uint32_t slot = !split ? lane
+                          : (quad && !producer) ? (((lane >> 4) << 1) | ((lane >> 3) & 1u))
+                                                : split_slot(lane);
     const uint32_t row = split ? split_row(slot) : lane;
     uint64_t total = *total_p;
     if (total > max_chunks) total = max_chunks;
@@ -506,7 +608,7 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
     }
     __syncthreads();
     const uint64_t g = wg_base + slot;
-    const bool valid = g < total;
+    const bool valid = slot < wg_chunks && g < total;
     // slot -> chunk through the length order (longest first, see k_len_hist): the
     // chunks of a wave have nearly equal block counts and the longest start first
     const uint64_t ci = valid ? (order ? (uint64_t)order[g] : g) : 0;
@@ -531,39 +633,16 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
             diag[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memtime() - t_start;
         }
     } else if (split) {
-        SplitLane c;
-        c.sh1 = hi ? 2u : 6u;
-        c.sh2 = hi ? 13u : 11u;
-        c.sh3 = hi ? 22u : 25u;
-        c.lm = hi ? 0xffffffffu : 0u;
-        asm volatile("" : "+v"(c.sh1), "+v"(c.sh2), "+v"(c.sh3), "+v"(c.lm));
-        uint32_t st[4] = {hi ? 0x6a09e667u : 0x510e527fu, hi ? 0xbb67ae85u : 0x9b05688cu,
-                          hi ? 0x3c6ef372u : 0x1f83d9abu, hi ? 0xa54ff53au : 0x5be0cd19u};
-        uint32_t z = 0;  // stays 0 in hi lanes: every write to it is masked to lo lanes
-        uint4 wA[8], wB[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) wA[i] = wB[i] = make_uint4(0u, 0u, 0u, 0u);
-        const uint32_t off = row * PC_ROW + (hi ? 32u : 0u);
-        if (NB > 0) {
-            t_spin += wait_ready(&s_ready, 0, diag != nullptr);
-            load_w8(wA, &sW[0][off]);
-            spl_z(z, st[3], wA[0].x);
-        }
-        for (uint32_t k = 0; k < NB; k += 2) {
-            sha_rounds_split(st, wA, wB, &sW[(k + 1) % PC_RING][off], k + 1, k + 1 < NB, &s_ready, k < nbt, c, z);
-            spl_z(z, st[3], wB[0].x);
-            publish(&s_done, k, lane);
-            if (k + 1 >= NB) break;
-            sha_rounds_split(st, wB, wA, &sW[(k + 2) % PC_RING][off], k + 2, k + 2 < NB, &s_ready, k + 1 < nbt, c,
-                             z);
-            spl_z(z, st[3], wA[0].x);
-            publish(&s_done, k + 1, lane);
-        }
+        uint32_t st[4];
+        if (quad)
+            split_consumer<true>(sW, row, hi, lane, NB, nbt, &s_ready, &s_done, st, &t_spin, diag != nullptr);
+        else
+            split_consumer<false>(sW, row, hi, lane, NB, nbt, &s_ready, &s_done, st, &t_spin, diag != nullptr);
         if (diag && lane == 0) {
             diag[4 * blockIdx.x + 2] = t_spin;
             diag[4 * blockIdx.x + 3] = __builtin_amdgcn_s_memtime() - t_start;
         }
-        if (valid) {  // hi: H0..H3 (bytes 0-15), lo: H4..H7 (bytes 16-31)
+        if (valid && (!quad || (lane & 3u) == 0)) {  // hi: H0..H3 (bytes 0-15), lo: H4..H7 (bytes 16-31)
             uint4 *o = reinterpret_cast<uint4 *>(hash_base + ci * stride + (hi ? 0 : 16));
             *o = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]), __builtin_bswap32(st[2]),
                             __builtin_bswap32(st[3]));
@@ -681,23 +760,39 @@ uint32_t g_sha_mode = 0;                    // set by cg_diag_sha_mode (diagnost
 // Split-lane workgroups per launch (32 longest chunks each): one per CU.  Set by
 // cg_diag_sha_split_max (diagnostics; 0 = one lane per chunk everywhere).
 uint32_t g_sha_split_max = 256;
+// Quad workgroups per launch (8 longest chunks each).  cg_diag_sha_quad_max.
+uint32_t g_sha_quad_max = 256;
 
-uint32_t sha256_grid(uint64_t max_chunks, uint32_t *nsplit_out) {
-    uint64_t ns = (max_chunks + 31) / 32;
-    if (ns > g_sha_split_max) ns = g_sha_split_max;
-    const uint64_t rest = max_chunks > 32 * ns ? max_chunks - 32 * ns : 0;
-    if (nsplit_out) *nsplit_out = (uint32_t)ns;
-    return (uint32_t)(ns + (rest + 63) / 64);
+// Workgroup tiers for a launch of up to max_chunks chunks, `expected` of them
+// likely (total bytes / (min + avg)).  A quad workgroup holds a whole workgroup's
+// LDS for 8 chunks, so quads are used only when the one-lane tier left behind them
+// fits in one round of workgroups (<= 256 x 64 chunks): on a batch that fills the
+// GPU (config 4) they would hold back the one-lane workgroups queued behind them.
+uint32_t sha256_grid(uint64_t max_chunks, uint64_t expected, uint32_t *nquad_out, uint32_t *npair_out) {
+    auto tiers = [&](uint64_t qmax, uint64_t &nq, uint64_t &np) {
+        nq = (max_chunks + 7) / 8;
+        if (nq > qmax) nq = qmax;
+        const uint64_t rest = max_chunks > 8 * nq ? max_chunks - 8 * nq : 0;
+        np = (rest + 31) / 32;
+        if (np > g_sha_split_max) np = g_sha_split_max;
+    };
+    uint64_t nq, np;
+    tiers(g_sha_quad_max, nq, np);
+    if (expected > 8 * nq + 32 * np + 256 * 64) tiers(0, nq, np);
+    const uint64_t rest = max_chunks > 8 * nq + 32 * np ? max_chunks - 8 * nq - 32 * np : 0;
+    if (nquad_out) *nquad_out = (uint32_t)nq;
+    if (npair_out) *npair_out = (uint32_t)np;
+    return (uint32_t)(nq + np + (rest + 63) / 64);
 }
 
 void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
-                   uint64_t max_chunks, uint64_t max_len, uint32_t *d_order_tmp, uint8_t *d_hash_base,
-                   size_t hash_stride, hipStream_t st) {
+                   uint64_t max_chunks, uint64_t expected, uint64_t max_len, uint32_t *d_order_tmp,
+                   uint8_t *d_hash_base, size_t hash_stride, hipStream_t st) {
     if (max_chunks == 0) return;
-    uint32_t nsplit = 0;
-    const uint32_t nwg = sha256_grid(max_chunks, &nsplit);
+    uint32_t nquad = 0, npair = 0;
+    const uint32_t nwg = sha256_grid(max_chunks, expected, &nquad, &npair);
     const uint32_t *order = nullptr;
-    if (d_order_tmp && max_chunks > 32) {  // one workgroup has nothing to balance
+    if (d_order_tmp && max_chunks > 8) {  // one workgroup has nothing to balance
         uint32_t shift = 0;
         while ((((max_len + 72) >> 6) >> shift) >= SHA_NBKT - 1) ++shift;
         uint32_t *bkt = d_order_tmp, *ord = d_order_tmp + SHA_NBKT;
@@ -716,18 +811,20 @@ void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
     const size_t pad = nwg <= 256 ? 16384 : 0;
     hipLaunchKernelGGL(k_sha256, dim3(nwg), dim3(128), pad, st, d_data, d_abs,
                        (const DescRaw *)d_desc, d_total, max_chunks, order, d_hash_base, hash_stride, g_sha_diag,
-                       g_sha_mode, nsplit);
+                       g_sha_mode, nquad, npair);
 }
 
 // ---------------------------------------------------------------------------
 // Diagnostics: cycles per split round for a lone wave (the same round code the
 // split consumer runs, schedule words held in registers).
 // ---------------------------------------------------------------------------
+template <bool QUAD>
 __global__ void k_diag_sha_rounds_split(uint32_t iters, uint32_t *out, unsigned long long *cycles) {
     const uint32_t lane = threadIdx.x & 63u;
     const bool hi = (lane >> 2) & 1u;
+    const uint32_t q = lane & 3u;
     SplitLane c;
-    c.sh1 = hi ? 2u : 6u;
+    c.sh1 = QUAD ? (hi ? (q == 0 ? 2u : q == 1 ? 13u : 22u) : (q == 0 ? 6u : q == 1 ? 11u : 25u)) : (hi ? 2u : 6u);
     c.sh2 = hi ? 13u : 11u;
     c.sh3 = hi ? 22u : 25u;
     c.lm = hi ? 0xffffffffu : 0u;
@@ -765,14 +862,16 @@ __global__ void k_diag_dpp_probe(uint32_t *out) {
 
 }  // namespace cg
 
-extern "C" int cg_diag_sha_rounds_split(uint32_t iters, uint32_t blocks, uint32_t threads,
+// quad != 0: the 9-VALU quad round; else the 10-VALU pair round
+extern "C" int cg_diag_sha_rounds_split(uint32_t iters, uint32_t blocks, uint32_t threads, int quad,
                                         unsigned long long *h_cycles) {
     uint32_t *d_out = nullptr;
     unsigned long long *d_cyc = nullptr;
     const uint32_t waves = blocks * (threads / 64);
     if (hipMalloc(&d_out, (size_t)blocks * threads * 4) != hipSuccess) return 2;
     if (hipMalloc(&d_cyc, waves * 8) != hipSuccess) return 2;
-    hipLaunchKernelGGL(cg::k_diag_sha_rounds_split, dim3(blocks), dim3(threads), 0, 0, iters, d_out, d_cyc);
+    hipLaunchKernelGGL(quad ? cg::k_diag_sha_rounds_split<true> : cg::k_diag_sha_rounds_split<false>, dim3(blocks),
+                       dim3(threads), 0, 0, iters, d_out, d_cyc);
     hipError_t e = hipDeviceSynchronize();
     if (e == hipSuccess) e = hipMemcpy(h_cycles, d_cyc, waves * 8, hipMemcpyDeviceToHost);
     (void)hipFree(d_out);
@@ -797,7 +896,15 @@ extern "C" uint32_t cg_diag_sha_split_max(uint32_t v) {
 }
 
 // workgroups the digest launch uses for `max_chunks` (diagnostics: sizes cg_diag_sha_stats)
-extern "C" uint32_t cg_diag_sha_grid(uint64_t max_chunks) { return cg::sha256_grid(max_chunks, nullptr); }
+extern "C" uint32_t cg_diag_sha_grid(uint64_t max_chunks, uint64_t expected) {
+    return cg::sha256_grid(max_chunks, expected, nullptr, nullptr);
+}
+
+extern "C" uint32_t cg_diag_sha_quad_max(uint32_t v) {
+    const uint32_t old = cg::g_sha_quad_max;
+    cg::g_sha_quad_max = v;
+    return old;
+}
 
 namespace cg {
 

@@ -21,7 +21,10 @@ from chunker_amd.nar import synth_nars  # noqa: E402
 lib.cg_diag_sha_split_max.argtypes = [ctypes.c_uint32]
 lib.cg_diag_sha_split_max.restype = ctypes.c_uint32
 lib.cg_diag_dpp_probe.argtypes = [ctypes.c_void_p]
-lib.cg_diag_sha_rounds_split.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+lib.cg_diag_sha_quad_max.argtypes = [ctypes.c_uint32]
+lib.cg_diag_sha_quad_max.restype = ctypes.c_uint32
+lib.cg_diag_sha_rounds_split.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+                                         ctypes.c_void_p]
 lib.cg_diag_sha_rounds.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
 
 res = {}
@@ -34,8 +37,10 @@ if not res["dpp_probe_ok"]:
 
 it = 2000
 cyc = np.zeros(1, np.uint64)
-lib.cg_diag_sha_rounds_split(it, 1, 64, cyc.ctypes.data)
-res["split_cycles_per_round_1wave"] = float(cyc[0]) / (it * 64)
+lib.cg_diag_sha_rounds_split(it, 1, 64, 0, cyc.ctypes.data)
+res["pair_cycles_per_round_1wave"] = float(cyc[0]) / (it * 64)
+lib.cg_diag_sha_rounds_split(it, 1, 64, 1, cyc.ctypes.data)
+res["quad_cycles_per_round_1wave"] = float(cyc[0]) / (it * 64)
 cyc2 = np.zeros(2, np.uint64)
 lib.cg_diag_sha_rounds(it, 1, 64, cyc2.ctypes.data)
 res["onelane_cycles_per_round_1wave"] = float(cyc2[0]) / (it * 64)
@@ -53,7 +58,8 @@ for name, (n, size, params) in CFG.items():
     st = torch.cuda.current_stream().cuda_stream
     ref = None
     row = {}
-    for smax in (0, 64, 256, 1 << 20):
+    for qmax, smax in ((0, 0), (0, 256), (256, 0), (256, 256), (64, 256)):
+        prevq = lib.cg_diag_sha_quad_max(qmax)
         prev = lib.cg_diag_sha_split_max(smax)
         lib.cg_set_profiling(1)
         times = []
@@ -63,11 +69,12 @@ for name, (n, size, params) in CFG.items():
             times.append(buf[4])
         lib.cg_set_profiling(0)
         lib.cg_diag_sha_split_max(prev)
+        lib.cg_diag_sha_quad_max(prevq)
         nch = int(first[-1])
         dig = out[: nch * 48].view(-1, 48)[:, 16:].cpu().numpy()
         if ref is None:
             ref = dig
-        row[str(smax)] = {"digest_ms": round(float(np.median(times)), 3), "chunks": nch,
+        row[f"quad{qmax}_pair{smax}"] = {"digest_ms": round(float(np.median(times)), 3), "chunks": nch,
                           "same_as_onelane": bool(np.array_equal(dig, ref))}
     res[name] = row
     del d, out

@@ -296,11 +296,13 @@ def test_digest_spans_all_lengths(ca, O):
             assert bytes(dig[k]) == want, (algo, n, a)
 
 
-def _sha_split_max(ca, v):
-    f = ca.lib.cg_diag_sha_split_max
-    f.argtypes = [ctypes.c_uint32]
-    f.restype = ctypes.c_uint32
-    return f(v)
+def _sha_kinds(ca, quad_max, pair_max):
+    """Cap the quad and pair workgroups of the SHA-256 launch; returns the old caps."""
+    fq, fp = ca.lib.cg_diag_sha_quad_max, ca.lib.cg_diag_sha_split_max
+    for f in (fq, fp):
+        f.argtypes = [ctypes.c_uint32]
+        f.restype = ctypes.c_uint32
+    return fq(quad_max), fp(pair_max)
 
 
 def test_dpp_bank_mask_lane_probe(ca):
@@ -314,14 +316,17 @@ def test_dpp_bank_mask_lane_probe(ca):
     assert out.tolist() == want
 
 
-@pytest.mark.parametrize("split_max", [0, 3, 1 << 20], ids=["one_lane", "mixed", "split"])
-def test_sha_workgroup_kinds_agree(ca, O, split_max):
-    """k_sha256 runs the longest chunks on split-lane workgroups (a round spread over
-    a lane pair) and the rest one chunk per lane; every mix gives hashlib's digests,
-    over every padding boundary, unaligned starts and multi-block chunks."""
+@pytest.mark.parametrize("quad_max,pair_max", [(0, 0), (0, 3), (2, 3), (1 << 20, 0), (0, 1 << 20)],
+                         ids=["one_lane", "pair_mixed", "quad_pair_one", "quad", "pair"])
+def test_sha_workgroup_kinds_agree(ca, O, quad_max, pair_max):
+    """k_sha256 runs the longest chunks on quad workgroups (a round spread over 8
+    lanes), the next on pair workgroups (2 lanes) and the rest one chunk per lane;
+    every mix gives hashlib's digests, over every padding boundary, unaligned starts
+    and multi-block chunks."""
     import torch
 
-    prev = _sha_split_max(ca, split_max)
+    prev = _sha_kinds(ca, quad_max, pair_max)
+    split_max = (quad_max, pair_max)
     try:
         rng = np.random.default_rng(17)
         data = rng.integers(0, 256, 3 << 20, dtype=np.uint8)
@@ -346,7 +351,7 @@ def test_sha_workgroup_kinds_agree(ca, O, split_max):
         for i, nar in enumerate(nars):
             assert_same(got[i], O.chunk_descriptors(nar, 4096, 16384, 65536, algo=SHA), f"nar{i}")
     finally:
-        _sha_split_max(ca, prev)
+        _sha_kinds(ca, *prev)
 
 
 @pytest.mark.slow
