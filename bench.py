@@ -146,6 +146,8 @@ def main():
                         "frac": round(total_bytes / (scan_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                         "traffic": None},
     }
+    if algo == 1:
+        roofline["latency_floor"] = sha_chain_floor(descs, n_nars, total_bytes, params, dig_ms)
     dig_kernels = ["k_sha256"] if algo == 1 else ["k_b3_groups", "k_b3_top"]
     traffic, src = pmc_traffic(args.config, dig_kernels)
     if traffic is not None:
@@ -182,6 +184,23 @@ def main():
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
+
+
+def sha_chain_floor(descs, n_nars, total_bytes, params, dig_ms):
+    """The SHA-256 digest stage cannot end before the longest chunk's serial chain of
+    64-round compressions has issued: blocks x 64 x (VALU per round x ~4.64 clocks,
+    lone-wave issue cost measured by scripts/diag_sha_split.py: 41.8 quad, 46.5 pair)
+    at 2.4 GHz.  The tier rule mirrors sha256_grid (quads when the expected chunk
+    count leaves <= 256 x 64 chunks for one-lane workgroups)."""
+    longest = int(descs["length"].max()) if len(descs) else 0
+    blocks = (longest + 9 + 63) // 64
+    expected = total_bytes // (params[0] + params[1]) + n_nars
+    quad = expected <= 8 * 256 + 32 * 256 + 256 * 64
+    cyc = 41.8 if quad else 46.5
+    floor_ms = blocks * 64 * cyc / 2.4e9 * 1e3
+    return {"longest_chunk_bytes": longest, "blocks": blocks, "tier": "quad" if quad else "pair",
+            "cycles_per_round": cyc, "clock_GHz": 2.4, "floor_ms": round(floor_ms, 3),
+            "frac": round(floor_ms / dig_ms, 4) if dig_ms else None}
 
 
 def pmc_traffic(config, kernels):
