@@ -32,7 +32,8 @@ EXPORTS = (
     "cg_chunk_batch", "cg_chunk_batch_device", "cg_push_new", "cg_push_push", "cg_push_finish",
     "cg_push_bytes_consumed", "cg_push_out_capacity", "cg_push_free", "cg_hash_spans_device",
     "cg_set_gear_table", "cg_get_gear_table", "cg_gear_is_placeholder", "cg_set_profiling",
-    "cg_last_stage_times", "cg_synth_nars", "cg_hash",
+    "cg_last_stage_times", "cg_synth_nars", "cg_hash", "cg_cas_ids_device", "cg_cas_id",
+    "cg_node_put_batch_device", "cg_node_put",
 )
 
 
@@ -79,6 +80,14 @@ def _load() -> ctypes.CDLL:
     L.cg_hash_spans_device.restype = i
     L.cg_hash.argtypes = [p, u64, i, p]
     L.cg_hash.restype = i
+    L.cg_cas_ids_device.argtypes = [p, p, p, sz, ctypes.c_uint32, p, p]
+    L.cg_cas_ids_device.restype = i
+    L.cg_cas_id.argtypes = [p, u64, ctypes.c_uint32, p]
+    L.cg_cas_id.restype = i
+    L.cg_node_put_batch_device.argtypes = [p, p, sz, u64, u64, u64, p, sz, p, p, p, p]
+    L.cg_node_put_batch_device.restype = i
+    L.cg_node_put.argtypes = [p, u64, u64, u64, u64, p, sz, psz, p, p]
+    L.cg_node_put.restype = i
     L.cg_set_gear_table.argtypes = [p]
     L.cg_set_gear_table.restype = i
     L.cg_get_gear_table.argtypes = [p]

@@ -1,0 +1,216 @@
+// cas.hip -- K5: CAS content identifiers, the second per-chunk
+// digest of the reference's ingest path.  Node::put (crates/node/src/lib.rs:114-132)
+// stores every chunk under
+//   ContentId::compute(kind, payload) = SHAKE256-256("flakecache-cas" || 0x00 ||
+//       kind || u16le(FORMAT_VERSION = 1) || u64le(payload.len()) || payload)
+// (crates/core/cas/src/lib.rs:23-26, :53-69; shake256_256 in
+// crates/core/crypto/src/hash.rs:34-41), and the manifest (the ordered chunk ids)
+// under kind Level1Manifest (crates/node/src/lib.rs:124-129).
+//
+// One lane absorbs one span: a Keccak-f[1600] sponge (FIPS 202; rate 136 B, SHAKE
+// padding 0x1F .. 0x80) with the 25 lanes of state as 50 dword registers, every
+// 64-bit rotation two v_alignbit, theta's parities and the a ^= d fold as
+// v_bitop3 xor3, chi as one v_bitop3 per dword.  The sponge is serial per span, so
+// like SHA-256 this stage is bound by the chain of its longest span; lanes take spans
+// longest first (the SHA-256 length order) so a wave's lanes finish together.
+#include "common.h"
+
+namespace cg {
+
+namespace {
+
+__device__ __forceinline__ uint32_t x3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+// a ^ (~b & c)
+__device__ __forceinline__ uint32_t chi3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0xD2);
+}
+
+// rotl64 on (lo, hi) by a compile-time r in [1, 63]
+template <int R>
+__device__ __forceinline__ void rot(uint32_t lo, uint32_t hi, uint32_t &olo, uint32_t &ohi) {
+    if constexpr (R == 0) {
+        olo = lo;
+        ohi = hi;
+    } else if constexpr (R < 32) {
+        ohi = __builtin_amdgcn_alignbit(hi, lo, 32 - R);
+        olo = __builtin_amdgcn_alignbit(lo, hi, 32 - R);
+    } else if constexpr (R == 32) {
+        olo = hi;
+        ohi = lo;
+    } else {
+        ohi = __builtin_amdgcn_alignbit(lo, hi, 64 - R);
+        olo = __builtin_amdgcn_alignbit(hi, lo, 64 - R);
+    }
+}
+
+__constant__ uint32_t KRC_LO[24] = {0x00000001u, 0x00008082u, 0x0000808au, 0x80008000u, 0x0000808bu, 0x80000001u,
+                                    0x80008081u, 0x00008009u, 0x0000008au, 0x00000088u, 0x80008009u, 0x8000000au,
+                                    0x8000808bu, 0x0000008bu, 0x00008089u, 0x00008003u, 0x00008002u, 0x00000080u,
+                                    0x0000800au, 0x8000000au, 0x80008081u, 0x00008080u, 0x80000001u, 0x80008008u};
+__constant__ uint32_t KRC_HI[24] = {0x00000000u, 0x00000000u, 0x80000000u, 0x80000000u, 0x00000000u, 0x00000000u,
+                                    0x80000000u, 0x80000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u,
+                                    0x00000000u, 0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u,
+                                    0x00000000u, 0x80000000u, 0x80000000u, 0x80000000u, 0x00000000u, 0x80000000u};
+
+// rho offsets r[x + 5y] (FIPS 202 Table 2)
+#define KR(i) ((i) == 0 ? 0 : (i) == 1 ? 1 : (i) == 2 ? 62 : (i) == 3 ? 28 : (i) == 4 ? 27 : (i) == 5 ? 36 \
+    : (i) == 6 ? 44 : (i) == 7 ? 6 : (i) == 8 ? 55 : (i) == 9 ? 20 : (i) == 10 ? 3 : (i) == 11 ? 10 : (i) == 12 ? 43 \
+    : (i) == 13 ? 25 : (i) == 14 ? 39 : (i) == 15 ? 41 : (i) == 16 ? 45 : (i) == 17 ? 15 : (i) == 18 ? 21 \
+    : (i) == 19 ? 8 : (i) == 20 ? 18 : (i) == 21 ? 2 : (i) == 22 ? 61 : (i) == 23 ? 56 : 14)
+
+// rho + pi for lane i = x + 5y: B[y + 5((2x + 3y) % 5)] = rot(A[i], r[i])
+template <int I>
+__device__ __forceinline__ void rho_pi(const uint32_t *lo, const uint32_t *hi, uint32_t *blo, uint32_t *bhi) {
+    constexpr int x = I % 5, y = I / 5, j = y + 5 * ((2 * x + 3 * y) % 5);
+    rot<KR(I)>(lo[I], hi[I], blo[j], bhi[j]);
+    if constexpr (I < 24) rho_pi<I + 1>(lo, hi, blo, bhi);
+}
+
+// Keccak-f[1600] on (lo[25], hi[25]), lanes A[x + 5y].  Fully unrolled: with the
+// rounds in a loop the B -> A renaming costs ~70 v_mov_b64 per round.
+__device__ __forceinline__ void keccak_f(uint32_t lo[25], uint32_t hi[25]) {
+#pragma unroll
+    for (int round = 0; round < 24; ++round) {
+        uint32_t clo[5], chi_[5], blo[25], bhi[25];
+#pragma unroll
+        for (int x = 0; x < 5; ++x) {
+            clo[x] = x3(x3(lo[x], lo[x + 5], lo[x + 10]), lo[x + 15], lo[x + 20]);
+            chi_[x] = x3(x3(hi[x], hi[x + 5], hi[x + 10]), hi[x + 15], hi[x + 20]);
+        }
+#pragma unroll
+        for (int x = 0; x < 5; ++x) {
+            uint32_t rlo, rhi;
+            rot<1>(clo[(x + 1) % 5], chi_[(x + 1) % 5], rlo, rhi);
+#pragma unroll
+            for (int y = 0; y < 5; ++y) {
+                lo[x + 5 * y] = x3(lo[x + 5 * y], clo[(x + 4) % 5], rlo);
+                hi[x + 5 * y] = x3(hi[x + 5 * y], chi_[(x + 4) % 5], rhi);
+            }
+        }
+        rho_pi<0>(lo, hi, blo, bhi);
+#pragma unroll
+        for (int y = 0; y < 5; ++y)
+#pragma unroll
+            for (int x = 0; x < 5; ++x) {
+                lo[x + 5 * y] = chi3(blo[x + 5 * y], blo[(x + 1) % 5 + 5 * y], blo[(x + 2) % 5 + 5 * y]);
+                hi[x + 5 * y] = chi3(bhi[x + 5 * y], bhi[(x + 1) % 5 + 5 * y], bhi[(x + 2) % 5 + 5 * y]);
+            }
+        lo[0] ^= KRC_LO[round];
+        hi[0] ^= KRC_HI[round];
+    }
+}
+
+constexpr uint32_t CAS_HDR = 26;   // "flakecache-cas" 0x00 kind u16le(1) u64le(len)
+constexpr uint32_t CAS_RATE = 136; // SHAKE256 rate in bytes (17 lanes)
+
+// Message byte m of a span's framed message (header, then payload); 0 past the end.
+__device__ __forceinline__ uint32_t msg_byte(const uint8_t *pay, uint64_t len, uint32_t kind, uint64_t m) {
+    if (m >= CAS_HDR) return m - CAS_HDR < len ? pay[m - CAS_HDR] : 0u;
+    constexpr char dom[15] = "flakecache-cas";
+    if (m < 14) return (uint8_t)dom[m];
+    if (m == 14) return 0u;
+    if (m == 15) return kind;
+    if (m == 16) return 1u;  // FORMAT_VERSION = 1, u16 little-endian
+    if (m == 17) return 0u;
+    return (uint32_t)(len >> (8 * (m - 18))) & 0xFFu;
+}
+
+// Block k (k >= 1) lies wholly inside the payload: its 136 bytes start at payload
+// byte 136k - 26.  The 35 aligned dwords covering them are loaded once and realigned
+// with v_alignbyte (the byte shift is the same for every block since 136 % 4 == 0).
+__device__ __forceinline__ bool whole_block(uint64_t k, uint64_t mlen) {
+    return k > 0 && (k + 1) * CAS_RATE <= mlen;
+}
+
+}  // namespace
+
+// Lanes take spans in the SHA-256 length order (longest first; `order` may be null).
+// Span g: bytes data[abs[g] .. abs[g] + desc[g].length); id -> ids + g * id_stride.
+__global__ __launch_bounds__(64) void k_cas_ids(const uint8_t *__restrict__ data, const uint64_t *__restrict__ abs,
+                                                const DescRaw *__restrict__ desc, const uint64_t *__restrict__ total_p,
+                                                uint64_t max_n, const uint32_t *__restrict__ order, uint32_t kind,
+                                                uint8_t *__restrict__ ids, uint64_t id_stride) {
+    uint64_t total = *total_p;
+    if (total > max_n) total = max_n;
+    const uint64_t slot = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+    if (slot >= total) return;
+    const uint64_t g = order ? (uint64_t)order[slot] : slot;
+    const uint64_t len = desc[g].length;
+    const uint8_t *pay = data + abs[g];
+    const uint64_t mlen = CAS_HDR + len;
+    const uint64_t nblk = mlen / CAS_RATE + 1;  // the pad block always exists (mlen % rate < rate)
+    const uint32_t shift = (uint32_t)((uintptr_t)pay & 3u);
+    const uint32_t *base0 = reinterpret_cast<const uint32_t *>(pay - shift);
+
+    const uint32_t sh = (shift + 2u) & 3u;
+    uint32_t lo[25], hi[25], dw[35];
+#pragma unroll
+    for (int i = 0; i < 25; ++i) lo[i] = hi[i] = 0;
+    // Aligned dwords of whole block k: payload bytes [136k - 26, 136k + 110) start
+    // at dword (136k - 26 + shift) / 4 of base0, byte sh = (shift + 2) & 3 of it (136k - 26
+    // is 2 mod 4); dword 34 is needed only when sh > 0 and then lies inside the payload,
+    // so no load leaves the span.
+    auto load_whole = [&](uint64_t k) {
+        const uint32_t *b = base0 + ((k * CAS_RATE - CAS_HDR + shift) >> 2);
+#pragma unroll
+        for (int i = 0; i < 34; ++i) dw[i] = __builtin_nontemporal_load(b + i);
+        dw[34] = sh ? __builtin_nontemporal_load(b + 34) : 0u;
+    };
+    if (whole_block(1, mlen)) load_whole(1);
+    for (uint64_t k = 0; k < nblk; ++k) {
+        if (whole_block(k, mlen)) {
+#pragma unroll
+            for (int i = 0; i < 17; ++i) {
+                lo[i] ^= __builtin_amdgcn_alignbyte(dw[2 * i + 1], dw[2 * i], sh);
+                hi[i] ^= __builtin_amdgcn_alignbyte(dw[2 * i + 2], dw[2 * i + 1], sh);
+            }
+        } else {  // header block, last partial block or the pad block: byte by byte
+            const uint64_t m0 = k * CAS_RATE;
+            for (uint32_t i = 0; i < CAS_RATE; ++i) {
+                const uint64_t m = m0 + i;
+                uint32_t v = m < mlen ? msg_byte(pay, len, kind, m) : 0u;
+                if (m == mlen) v ^= 0x1Fu;                          // SHAKE domain bits + first pad bit
+                if (k == nblk - 1 && i == CAS_RATE - 1) v ^= 0x80u;  // last pad bit
+                const uint32_t w = i >> 2, sb = 8 * (i & 3);
+                if (w & 1) hi[w >> 1] ^= v << sb;
+                else lo[w >> 1] ^= v << sb;
+            }
+        }
+        if (whole_block(k + 1, mlen)) load_whole(k + 1);  // in flight during the permutation
+        keccak_f(lo, hi);
+    }
+    uint4 *o = reinterpret_cast<uint4 *>(ids + id_stride * g);
+    o[0] = make_uint4(lo[0], hi[0], lo[1], hi[1]);
+    o[1] = make_uint4(lo[2], hi[2], lo[3], hi[3]);
+}
+
+void launch_cas_ids(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
+                    uint64_t max_n, const uint32_t *d_order, uint32_t kind, uint8_t *d_ids, size_t id_stride,
+                    hipStream_t st) {
+    if (max_n == 0) return;
+    hipLaunchKernelGGL(k_cas_ids, dim3((uint32_t)((max_n + 63) / 64)), dim3(64), 0, st, d_data, d_abs,
+                       (const DescRaw *)d_desc, d_total, max_n, d_order, kind, d_ids, (uint64_t)id_stride);
+}
+
+// Manifest spans (crates/node/src/lib.rs:124-129): NAR i's manifest is the
+// concatenation of its chunk ids, i.e. bytes [32 first[i], 32 first[i+1]) of the id
+// buffer.  Writes the (abs, desc.length) span view the CAS kernel reads.
+__global__ void k_manifest_spans(const uint64_t *__restrict__ first, uint64_t n_nars, uint64_t *__restrict__ abs,
+                                 DescRaw *__restrict__ desc, uint64_t *__restrict__ total) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0) *total = n_nars;
+    if (i >= n_nars) return;
+    abs[i] = 32 * first[i];
+    desc[i].offset = 32 * first[i];
+    desc[i].length = 32 * (first[i + 1] - first[i]);
+}
+
+void launch_manifest_spans(const uint64_t *d_first, uint64_t n_nars, uint64_t *d_abs, void *d_desc, uint64_t *d_total,
+                           hipStream_t st) {
+    hipLaunchKernelGGL(k_manifest_spans, dim3((uint32_t)(n_nars ? (n_nars + 255) / 256 : 1)), dim3(256), 0, st,
+                       d_first, n_nars, d_abs, (DescRaw *)d_desc, d_total);
+}
+
+}  // namespace cg

@@ -60,6 +60,23 @@ void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
                    uint8_t *d_hash_base, size_t hash_stride, hipStream_t st);
 size_t sha256_order_tmp_elems(uint64_t max_chunks);
 
+// Longest-first order of the first min(*d_total, max_chunks) descriptors (counting sort
+// on SHA-256 block count, max_len bounding every length); returns the order inside
+// d_order_tmp (sha256_order_tmp_elems(max_chunks) u32), or nullptr without a buffer.
+const uint32_t *launch_len_order(const void *d_desc, const uint64_t *d_total, uint64_t max_chunks, uint64_t max_len,
+                                 uint32_t *d_order_tmp, hipStream_t st);
+
+// K5: CAS content ids (cas.hip): SHAKE256-256 of the framed span, ContentId::compute
+// (crates/core/cas/src/lib.rs:53-69); id of span g -> d_ids + g * id_stride.
+void launch_cas_ids(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
+                    uint64_t max_n, const uint32_t *d_order, uint32_t kind, uint8_t *d_ids, size_t id_stride,
+                    hipStream_t st);
+
+// Manifest spans of a batch: span i = bytes [32 first[i], 32 first[i+1]) of the chunk-id
+// buffer (crates/node/src/lib.rs:124-129); *d_total = n_nars.
+void launch_manifest_spans(const uint64_t *d_first, uint64_t n_nars, uint64_t *d_abs, void *d_desc, uint64_t *d_total,
+                           hipStream_t st);
+
 void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
                    uint64_t max_chunks, uint64_t total_bytes, uint8_t *d_hash_base, size_t hash_stride,
                    uint32_t *d_gmap, uint64_t *d_group_base, uint32_t *d_gcount_u32,

@@ -124,13 +124,22 @@ struct Workspace {
     hipStream_t stream = nullptr;
     uint64_t gear_epoch = 0;
     DevBuf gear, seg_count, seg_cand, eoff, scan_tmp, entries, nar_off, cap_base, wchunk, nar_nchunks, nar_first,
-        chunk_abs, b3_gcount, b3_gbase, b3_gcv, b3_gmap, in, out, span_off, span_len, order;
+        chunk_abs, b3_gcount, b3_gbase, b3_gcv, b3_gmap, in, out, span_off, span_len, order, cas_order, ids,
+        man_abs, man_desc;
     PinBuf stage;
     hipEvent_t ev[EV_N] = {};
+    // CAS ids run on side_stream, concurrently with the digest: both stages are bound by
+    // their longest chunk's serial chain, not by the chip, so they overlap for free.
+    hipStream_t side_stream = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_cas = nullptr;
     int init(int dev) {
         device = dev;
         HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        HIP_TRY(hipStreamCreateWithFlags(&side_stream, hipStreamNonBlocking));
         for (auto &e : ev) HIP_TRY(hipEventCreate(&e));
+        HIP_TRY(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+        HIP_TRY(hipEventCreate(&ev_cas));
         return CG_OK;
     }
 };
@@ -255,8 +264,14 @@ uint32_t seg_slots(const CdcParams &p) {
 
 // The whole device pipeline for one batch.  d_out receives descriptors; the
 // digest of descriptor g is written in place at d_out[g].hash.
+//
+// Node::put mode (crates/node/src/lib.rs:114-132) when d_chunk_ids is set: every
+// chunk's ContentId(Chunk, payload) -> d_chunk_ids[32 g], and NAR i's manifest id
+// ContentId(Level1Manifest, its chunk ids in order) -> h_manifest_ids[32 i].  The CAS
+// stage forks onto ws->side_stream after descriptor assembly and joins before return.
 int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, size_t n_nars, const Opts &o,
-              int algo, cg_desc *d_out, size_t out_cap, uint64_t *h_nar_first, hipStream_t st) {
+              int algo, cg_desc *d_out, size_t out_cap, uint64_t *h_nar_first, hipStream_t st,
+              uint8_t *d_chunk_ids = nullptr, uint8_t *h_manifest_ids = nullptr) {
     if (algo != CG_BLAKE3 && algo != CG_SHA256) return fail(CG_E_INVALID_OPTIONS, "unknown hash algorithm");
     if (((uintptr_t)d_data & 15u) != 0) return fail(CG_E_IO, "device input must be 16-byte aligned");
     int rc;
@@ -333,6 +348,27 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
                         ws->nar_first.as<uint64_t>(), n_nars, d_out, out_cap, ws->chunk_abs.as<uint64_t>(), st);
     if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_ASSEMBLE], st));
     const uint64_t *d_total = ws->nar_first.as<uint64_t>() + n_nars;
+    uint8_t *d_man = nullptr;
+    if (d_chunk_ids) {
+        if ((rc = ws->cas_order.ensure(cg::sha256_order_tmp_elems(chunk_bound) * 4, "cas_order"))) return rc;
+        if ((rc = ws->ids.ensure((n_nars + 1) * 32, "manifest ids"))) return rc;
+        if ((rc = ws->man_abs.ensure((n_nars + 1) * 8, "manifest spans"))) return rc;
+        if ((rc = ws->man_desc.ensure((n_nars + 2) * sizeof(cg_desc), "manifest spans"))) return rc;
+        d_man = ws->ids.as<uint8_t>();
+        hipStream_t side = ws->side_stream;
+        HIP_TRY(hipEventRecord(ws->ev_fork, st));
+        HIP_TRY(hipStreamWaitEvent(side, ws->ev_fork, 0));
+        const uint32_t *ord = cg::launch_len_order(d_out, d_total, chunk_bound, o.max, ws->cas_order.as<uint32_t>(), side);
+        cg::launch_cas_ids(d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, ord, CG_KIND_CHUNK,
+                           d_chunk_ids, 32, side);
+        uint64_t *d_man_total = reinterpret_cast<uint64_t *>(ws->man_desc.as<cg_desc>() + n_nars);
+        cg::launch_manifest_spans(ws->nar_first.as<uint64_t>(), n_nars, ws->man_abs.as<uint64_t>(), ws->man_desc.p,
+                                  d_man_total, side);
+        cg::launch_cas_ids(d_chunk_ids, ws->man_abs.as<uint64_t>(), ws->man_desc.p, d_man_total, n_nars, nullptr,
+                           CG_KIND_LEVEL1_MANIFEST, d_man, 32, side);
+        HIP_TRY(hipEventRecord(ws->ev_cas, side));
+        HIP_TRY(hipEventRecord(ws->ev_join, side));
+    }
     uint8_t *hash_base = reinterpret_cast<uint8_t *>(d_out) + offsetof(cg_desc, hash);
     if (algo == CG_SHA256) {
         if ((rc = ws->order.ensure(cg::sha256_order_tmp_elems(chunk_bound) * 4, "order"))) return rc;
@@ -346,15 +382,23 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
                           ws->b3_gcount.as<uint32_t>(), ws->scan_tmp.as<uint64_t>(), ws->b3_gcv.as<uint32_t>(), st);
     }
     if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_DIGEST], st));
+    if (d_chunk_ids) HIP_TRY(hipStreamWaitEvent(st, ws->ev_join, 0));
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(s_first, ws->nar_first.p, (n_nars + 1) * 8, hipMemcpyDeviceToHost, st));
+    if (d_man && h_manifest_ids)
+        HIP_TRY(hipMemcpyAsync(h_manifest_ids, d_man, n_nars * 32, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     if (prof) {
-        t_stage_ms.assign(EV_N - 1, 0.0);
+        t_stage_ms.assign(EV_N - 1 + (d_chunk_ids ? 1 : 0), 0.0);
         for (int k = 1; k < EV_N; ++k) {
             float ms = 0;
             HIP_TRY(hipEventElapsedTime(&ms, ws->ev[k - 1], ws->ev[k]));
             t_stage_ms[k - 1] = ms;
+        }
+        if (d_chunk_ids) {  // CAS stage: from descriptor assembly to the last id
+            float ms = 0;
+            HIP_TRY(hipEventElapsedTime(&ms, ws->ev[EV_ASSEMBLE], ws->ev_cas));
+            t_stage_ms[EV_N - 1] = ms;
         }
     }
     if (h_nar_first) memcpy(h_nar_first, s_first, (n_nars + 1) * 8);
@@ -425,6 +469,29 @@ int hash_spans(Workspace *ws, const uint8_t *d_data, const uint64_t *d_offsets, 
     HIP_TRY(hipMemcpy2DAsync(d_digests, 32, hb, sizeof(cg_desc), 32, n, hipMemcpyDeviceToDevice, st));
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipStreamSynchronize(st));
+    return CG_OK;
+}
+
+// ContentId pipeline over n device spans on `st` (cg_cas_ids_device, cg_cas_id).
+int cas_spans(Workspace *ws, const uint8_t *d_data, const uint64_t *d_offsets, const uint64_t *d_lengths, size_t n,
+              uint32_t kind, uint8_t *d_ids, hipStream_t st) {
+    int rc;
+    if ((rc = ws->chunk_abs.ensure((n + 1) * 8, "chunk_abs"))) return rc;
+    if ((rc = ws->out.ensure((n + 1) * sizeof(cg_desc), "descriptors"))) return rc;
+    if ((rc = ws->nar_first.ensure(16, "total"))) return rc;
+    if ((rc = ws->cas_order.ensure(cg::sha256_order_tmp_elems(n) * 4, "cas_order"))) return rc;
+    uint64_t *d_total = ws->nar_first.as<uint64_t>();
+    cg::launch_spans_to_desc(d_offsets, d_lengths, n, ws->chunk_abs.as<uint64_t>(), ws->out.p, d_total, st);
+    const uint32_t *ord =
+        n > 64 ? cg::launch_len_order(ws->out.p, d_total, n, MAXIMUM_MAX, ws->cas_order.as<uint32_t>(), st) : nullptr;
+    cg::launch_cas_ids(d_data, ws->chunk_abs.as<uint64_t>(), ws->out.p, d_total, n, ord, kind, d_ids, 32, st);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(st));
+    return CG_OK;
+}
+
+int check_kind(uint32_t kind) {
+    if (kind < CG_KIND_CHUNK || kind > CG_KIND_COMMIT) return fail(CG_E_INVALID_OPTIONS, "unknown object kind");
     return CG_OK;
 }
 
@@ -544,6 +611,89 @@ int cg_hash_spans_device(const uint8_t *d_data, const uint64_t *d_offsets, const
     if (rc) return rc;
     WsGuard guard{ws};
     return hash_spans(ws, d_data, d_offsets, d_lengths, n, algo, d_digests, static_cast<hipStream_t>(stream));
+}
+
+int cg_cas_ids_device(const uint8_t *d_data, const uint64_t *d_offsets, const uint64_t *d_lengths, size_t n,
+                      uint32_t kind, uint8_t *d_ids, void *stream) {
+    t_err.clear();
+    int rc = check_kind(kind);
+    if (rc || n == 0) return rc;
+    Workspace *ws = nullptr;
+    if ((rc = acquire(&ws))) return rc;
+    WsGuard guard{ws};
+    return cas_spans(ws, d_data, d_offsets, d_lengths, n, kind, d_ids, static_cast<hipStream_t>(stream));
+}
+
+int cg_cas_id(const uint8_t *data, uint64_t len, uint32_t kind, uint8_t out[32]) {
+    t_err.clear();
+    int rc = check_kind(kind);
+    if (rc) return rc;
+    Workspace *ws = nullptr;
+    if ((rc = acquire(&ws))) return rc;
+    WsGuard guard{ws};
+    if ((rc = ws->in.ensure(len + 256, "input"))) return rc;
+    if ((rc = ws->span_off.ensure(64, "span"))) return rc;
+    if ((rc = ws->stage.ensure(64))) return rc;
+    uint64_t *s = ws->stage.as<uint64_t>();
+    s[0] = 0;
+    s[1] = len;
+    if (len) HIP_TRY(hipMemcpyAsync(ws->in.p, data, len, hipMemcpyHostToDevice, ws->stream));
+    HIP_TRY(hipMemcpyAsync(ws->span_off.p, s, 16, hipMemcpyHostToDevice, ws->stream));
+    const uint64_t *d_off = ws->span_off.as<uint64_t>();
+    uint8_t *d_id = reinterpret_cast<uint8_t *>(ws->span_off.as<uint64_t>() + 2);
+    if ((rc = cas_spans(ws, ws->in.as<uint8_t>(), d_off, d_off + 1, 1, kind, d_id, ws->stream))) return rc;
+    HIP_TRY(hipMemcpyAsync(s + 2, d_id, 32, hipMemcpyDeviceToHost, ws->stream));
+    HIP_TRY(hipStreamSynchronize(ws->stream));
+    memcpy(out, s + 2, 32);
+    return CG_OK;
+}
+
+int cg_node_put_batch_device(const uint8_t *d_data, const uint64_t *nar_offsets, size_t n_nars, uint64_t min_size,
+                             uint64_t avg_size, uint64_t max_size, cg_desc *d_out, size_t out_cap,
+                             uint64_t *nar_first, uint8_t *d_chunk_ids, uint8_t *manifest_ids, void *stream) {
+    t_err.clear();
+    Opts o;
+    int rc = resolve(min_size, avg_size, max_size, &o, nullptr, 0);
+    if (rc) return rc;
+    if (!d_chunk_ids) return fail(CG_E_IO, "node put: null chunk id buffer");
+    if (n_nars && nar_offsets[0] != 0) return fail(CG_E_BOUNDS, "device batch offsets must start at 0");
+    Workspace *ws = nullptr;
+    if ((rc = acquire(&ws))) return rc;
+    WsGuard guard{ws};
+    return run_batch(ws, d_data, nar_offsets, n_nars, o, CG_SHA256, d_out, out_cap, nar_first,
+                     static_cast<hipStream_t>(stream), d_chunk_ids, manifest_ids);
+}
+
+int cg_node_put(const uint8_t *data, uint64_t len, uint64_t min_size, uint64_t avg_size, uint64_t max_size,
+                cg_desc *out, size_t out_cap, size_t *n_out, uint8_t *chunk_ids, uint8_t manifest_id[32]) {
+    t_err.clear();
+    if (n_out) *n_out = 0;
+    Opts o;
+    int rc = resolve(min_size, avg_size, max_size, &o, nullptr, 0);
+    if (rc) return rc;
+    Workspace *ws = nullptr;
+    if ((rc = acquire(&ws))) return rc;
+    WsGuard guard{ws};
+    const uint64_t cap = capacity_of(len, o.min);
+    if ((rc = ws->in.ensure(len + 256, "input"))) return rc;
+    if ((rc = ws->out.ensure((cap + 1) * sizeof(cg_desc), "descriptors"))) return rc;
+    if ((rc = ws->span_len.ensure((cap + 1) * 32, "chunk ids"))) return rc;
+    if (len) HIP_TRY(hipMemcpyAsync(ws->in.p, data, len, hipMemcpyHostToDevice, ws->stream));
+    uint64_t offs[2] = {0, len}, first[2] = {0, 0};
+    uint8_t man[32];
+    rc = run_batch(ws, ws->in.as<uint8_t>(), offs, 1, o, CG_SHA256, ws->out.as<cg_desc>(), cap, first, ws->stream,
+                   ws->span_len.as<uint8_t>(), man);
+    if (rc) return rc;
+    const uint64_t total = first[1];
+    if (total > out_cap) return fail(CG_E_CAPACITY, "descriptor output array too small");
+    if (total) {
+        HIP_TRY(hipMemcpyAsync(out, ws->out.p, total * sizeof(cg_desc), hipMemcpyDeviceToHost, ws->stream));
+        if (chunk_ids) HIP_TRY(hipMemcpyAsync(chunk_ids, ws->span_len.p, total * 32, hipMemcpyDeviceToHost, ws->stream));
+        HIP_TRY(hipStreamSynchronize(ws->stream));
+    }
+    if (n_out) *n_out = total;
+    if (manifest_id) memcpy(manifest_id, man, 32);
+    return CG_OK;
 }
 
 int cg_hash(const uint8_t *data, uint64_t len, int algo, uint8_t out[32]) {

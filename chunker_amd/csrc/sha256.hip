@@ -755,6 +755,22 @@ __global__ __launch_bounds__(256) void k_len_scatter(const DescRaw *__restrict__
 
 size_t sha256_order_tmp_elems(uint64_t max_chunks) { return max_chunks + SHA_NBKT + 64; }
 
+const uint32_t *launch_len_order(const void *d_desc, const uint64_t *d_total, uint64_t max_chunks, uint64_t max_len,
+                                 uint32_t *d_order_tmp, hipStream_t st) {
+    if (!d_order_tmp || max_chunks == 0) return nullptr;
+    uint32_t shift = 0;
+    while ((((max_len + 72) >> 6) >> shift) >= SHA_NBKT - 1) ++shift;
+    uint32_t *bkt = d_order_tmp, *ord = d_order_tmp + SHA_NBKT;
+    const uint32_t nb = (uint32_t)((max_chunks + 255) / 256);
+    (void)hipMemsetAsync(bkt, 0, SHA_NBKT * sizeof(uint32_t), st);
+    hipLaunchKernelGGL(k_len_hist, dim3(nb), dim3(256), 0, st, (const DescRaw *)d_desc, d_total, max_chunks, shift,
+                       bkt);
+    hipLaunchKernelGGL(k_len_base, dim3(1), dim3(SHA_NBKT), 0, st, bkt);
+    hipLaunchKernelGGL(k_len_scatter, dim3(nb), dim3(256), 0, st, (const DescRaw *)d_desc, d_total, max_chunks,
+                       shift, bkt, ord);
+    return ord;
+}
+
 unsigned long long *g_sha_diag = nullptr;  // set by cg_diag_sha_stats (diagnostics only)
 uint32_t g_sha_mode = 0;                    // set by cg_diag_sha_mode (diagnostics only; 0 = product)
 // Split-lane workgroups per launch (32 longest chunks each): one per CU.  Set by
@@ -791,20 +807,9 @@ void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
     if (max_chunks == 0) return;
     uint32_t nquad = 0, npair = 0;
     const uint32_t nwg = sha256_grid(max_chunks, expected, &nquad, &npair);
-    const uint32_t *order = nullptr;
-    if (d_order_tmp && max_chunks > 8) {  // one workgroup has nothing to balance
-        uint32_t shift = 0;
-        while ((((max_len + 72) >> 6) >> shift) >= SHA_NBKT - 1) ++shift;
-        uint32_t *bkt = d_order_tmp, *ord = d_order_tmp + SHA_NBKT;
-        const uint32_t nb = (uint32_t)((max_chunks + 255) / 256);
-        (void)hipMemsetAsync(bkt, 0, SHA_NBKT * sizeof(uint32_t), st);
-        hipLaunchKernelGGL(k_len_hist, dim3(nb), dim3(256), 0, st, (const DescRaw *)d_desc, d_total, max_chunks,
-                           shift, bkt);
-        hipLaunchKernelGGL(k_len_base, dim3(1), dim3(SHA_NBKT), 0, st, bkt);
-        hipLaunchKernelGGL(k_len_scatter, dim3(nb), dim3(256), 0, st, (const DescRaw *)d_desc, d_total,
-                           max_chunks, shift, bkt, ord);
-        order = ord;
-    }
+    // one workgroup has nothing to balance
+    const uint32_t *order = max_chunks > 8 ? launch_len_order(d_desc, d_total, max_chunks, max_len, d_order_tmp, st)
+                                           : nullptr;
     // Latency-bound batches (no more workgroups than CUs): pad the LDS request past half
     // a CU's 160 KiB so no two workgroups share a CU, and a consumer wave never shares a
     // SIMD with another workgroup's wave (which costs it 20-90 % per round).

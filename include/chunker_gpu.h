@@ -108,6 +108,44 @@ int cg_hash_spans_device(const uint8_t *d_data, const uint64_t *d_offsets, const
  * blake3::hash, src/hashing.rs:36-53) into out[32].  len <= 16 MiB for BLAKE3. */
 int cg_hash(const uint8_t *data, uint64_t len, int algo, uint8_t out[32]);
 
+/* ---- CAS content ids and Node::put ---------------------- */
+
+/* ObjectKind (crates/core/cas/src/lib.rs:31-48), same discriminants. */
+typedef enum {
+    CG_KIND_CHUNK = 1,
+    CG_KIND_LEVEL0_MANIFEST = 2,
+    CG_KIND_LEVEL1_MANIFEST = 3,
+    CG_KIND_REFCOUNT = 4,
+    CG_KIND_WITNESS = 5,
+    CG_KIND_RECIPE = 6,
+    CG_KIND_COMMIT = 7
+} cg_object_kind;
+
+/* ContentId::compute(kind, payload) (crates/core/cas/src/lib.rs:53-69) over n
+ * device-resident spans: SHAKE256-256("flakecache-cas" || 0x00 || kind || u16le(1) ||
+ * u64le(len) || payload) (shake256_256, crates/core/crypto/src/hash.rs:34-41).
+ * d_ids receives n*32 bytes.  An unknown kind -> CG_E_INVALID_OPTIONS. */
+int cg_cas_ids_device(const uint8_t *d_data, const uint64_t *d_offsets, const uint64_t *d_lengths, size_t n,
+                      uint32_t kind, uint8_t *d_ids, void *stream);
+
+/* Host convenience: ContentId::compute of one host buffer into out[32]. */
+int cg_cas_id(const uint8_t *data, uint64_t len, uint32_t kind, uint8_t out[32]);
+
+/* Node::put (crates/node/src/lib.rs:114-132) over a device-resident batch of NARs:
+ * chunk_data with SHA-256 (:115, i.e. cg_chunk_batch_device with CG_SHA256) into
+ * d_out/nar_first; ContentId(Chunk, payload) of descriptor g -> d_chunk_ids[32 g]
+ * (:118-121); NAR i's manifest id ContentId(Level1Manifest, its chunk ids in order)
+ * -> manifest_ids[32 i] (host array, :124-129).  The CAS stage runs on a second
+ * stream concurrently with the SHA-256 digest. */
+int cg_node_put_batch_device(const uint8_t *d_data, const uint64_t *nar_offsets, size_t n_nars, uint64_t min_size,
+                             uint64_t avg_size, uint64_t max_size, cg_desc *d_out, size_t out_cap,
+                             uint64_t *nar_first, uint8_t *d_chunk_ids, uint8_t *manifest_ids, void *stream);
+
+/* Node::put on one host buffer: descriptors (out), chunk ids (chunk_ids, out_cap*32
+ * bytes) and the manifest id (manifest_id[32], the value Node::put returns). */
+int cg_node_put(const uint8_t *data, uint64_t len, uint64_t min_size, uint64_t avg_size, uint64_t max_size,
+                cg_desc *out, size_t out_cap, size_t *n_out, uint8_t *chunk_ids, uint8_t manifest_id[32]);
+
 /* FastCDC v2020 GEAR table plumbing.  The compiled-in table comes from
  * tables/fastcdc_v2020_gear.txt; cg_set_gear_table replaces it process-wide
  * (all devices) for later calls. */
@@ -117,7 +155,9 @@ int cg_gear_is_placeholder(void);
 
 /* Per-stage device times (ms) of the last batch call on this thread, measured with
  * HIP events on the stream the kernels ran on.  Order: scan, compact, walk,
- * assemble, digest.  Returns the number of stages written; 0 if profiling is off. */
+ * assemble, digest, and for the Node::put entries a sixth: cas (descriptor assembly
+ * to the last content id, on the side stream).  Returns the number of stages
+ * written; 0 if profiling is off. */
 void cg_set_profiling(int on);
 size_t cg_last_stage_times(double *ms, size_t n);
 

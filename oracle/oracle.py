@@ -10,6 +10,7 @@ FlakeCache/chunker snapshot); the restatements themselves live in oracle.c.
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
 import subprocess
 from pathlib import Path
@@ -163,6 +164,55 @@ def chunk_descriptors(data, mn=None, avg=None, mx=None, algo=SHA256, nthreads=No
 def hash_descs(data, descs: np.ndarray, algo=SHA256, nthreads=1) -> None:
     a = _buf(data)
     lib().or_hash_descs(a.ctypes.data, descs.ctypes.data, len(descs), algo, nthreads)
+
+
+# ---------------------------------------------------------------------------
+# CAS content ids and Node::put.  The Keccak sponge is
+# hashlib's SHAKE-256 (OpenSSL), an implementation independent of the GPU kernel,
+# pinned by the reference KAT (crates/core/crypto/src/hash.rs:46-57, test_oracle.py).
+# ---------------------------------------------------------------------------
+CAS_DOMAIN = b"flakecache-cas"  # crates/core/cas/src/lib.rs:23
+CAS_FORMAT_VERSION = 1          # crates/core/cas/src/lib.rs:25
+KIND_CHUNK = 0x01               # ObjectKind::Chunk, crates/core/cas/src/lib.rs:36
+KIND_LEVEL1_MANIFEST = 0x03     # ObjectKind::Level1Manifest, :40
+
+
+def shake256_256(data) -> bytes:
+    """shake256_256 (crates/core/crypto/src/hash.rs:34-41): first 32 bytes of SHAKE-256."""
+    return hashlib.shake_256(bytes(data)).digest(32)
+
+
+def content_id(kind: int, payload) -> bytes:
+    """ContentId::compute (crates/core/cas/src/lib.rs:59-69):
+    SHAKE256-256(domain || 0x00 || kind || u16le(version) || u64le(len) || payload)."""
+    payload = memoryview(_buf(payload))
+    h = hashlib.shake_256()
+    h.update(CAS_DOMAIN + b"\x00" + bytes([kind]) + CAS_FORMAT_VERSION.to_bytes(2, "little")
+             + len(payload).to_bytes(8, "little"))
+    h.update(payload)
+    return h.digest(32)
+
+
+def content_ids(data, descs: np.ndarray, kind: int = KIND_CHUNK, nthreads: int = 1) -> list[bytes]:
+    """One ContentId per descriptor span, in order (crates/node/src/lib.rs:118-121);
+    spans are hashed on a thread pool (hashlib drops the GIL for large updates)."""
+    buf = memoryview(_buf(data))
+    spans = [(int(d["offset"]), int(d["length"])) for d in descs]
+    one = lambda s: content_id(kind, buf[s[0]:s[0] + s[1]])  # noqa: E731
+    if nthreads <= 1 or len(spans) <= 1:
+        return [one(s) for s in spans]
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(nthreads) as ex:
+        return list(ex.map(one, spans))
+
+
+def node_put(data, mn=None, avg=None, mx=None, nthreads: int = 1):
+    """Node::put (crates/node/src/lib.rs:114-132) without the storage writes:
+    chunk_data (SHA-256) -> per-chunk ContentId(Chunk) -> manifest id
+    ContentId(Level1Manifest, concatenated chunk ids).  Returns (descs, ids, manifest)."""
+    descs = chunk_descriptors(data, mn, avg, mx, algo=SHA256, nthreads=nthreads)
+    ids = content_ids(data, descs, KIND_CHUNK, nthreads)
+    return descs, ids, content_id(KIND_LEVEL1_MANIFEST, b"".join(ids))
 
 
 class Push:

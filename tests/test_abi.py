@@ -135,3 +135,24 @@ def test_synthetic_nar_layout(ca):
         assert nar[-16:] == (1).to_bytes(8, "little") + b")" + bytes(7)
     z, _ = synth_nars([4096], zeros=True)
     assert not z[96:96 + 4096 - 112].any()
+
+
+def test_cas_entry_validation_without_gpu(ca):
+    """cg_cas_id / cg_cas_ids_device reject an unknown ObjectKind before touching a
+    device (crates/core/cas/src/lib.rs:31-48 has kinds 1..7); no CPU fallback."""
+    import torch
+
+    from chunker_amd import cas
+
+    buf = (ctypes.c_uint8 * 32)()
+    for bad in (0, 8, 255):
+        assert ca.lib.cg_cas_id(None, 0, bad, buf) == 4
+        assert "object kind" in ca._lib.last_error()
+        assert ca.lib.cg_cas_ids_device(None, None, None, 1, bad, None, None) == 4
+    assert ca.lib.cg_cas_ids_device(None, None, None, 0, 1, None, None) == 0
+    assert [int(k) for k in cas.ObjectKind] == list(range(1, 8))
+    if not torch.cuda.is_available():
+        with pytest.raises(ca.DeviceUnavailableError):
+            cas.ContentId.compute(cas.ObjectKind.Chunk, b"hello")
+        with pytest.raises(ca.DeviceUnavailableError):
+            cas.node_put(bytes(100_000), 4096, 16_384, 65_536)

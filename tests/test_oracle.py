@@ -195,3 +195,84 @@ def test_golden_fixtures_reproduce():
         data = make_input(case["input"])
         descs = O.chunk_descriptors(data, *case["params"], algo=case["algo"], nthreads=4)
         assert [[int(d["offset"]), int(d["length"]), bytes(d["hash"]).hex()] for d in descs] == case["chunks"]
+
+
+# --- CAS content ids -------------------------------------
+def _keccak_f(a):
+    """FIPS 202 Keccak-f[1600], pure Python (a second restatement to pin hashlib)."""
+    M = (1 << 64) - 1
+    R = [0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43, 25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14]
+    rot = lambda v, n: ((v << n) | (v >> (64 - n))) & M if n else v  # noqa: E731
+    rc = 1
+    for _ in range(24):
+        c = [a[x] ^ a[x + 5] ^ a[x + 10] ^ a[x + 15] ^ a[x + 20] for x in range(5)]
+        a = [a[i] ^ c[(i % 5 + 4) % 5] ^ rot(c[(i % 5 + 1) % 5], 1) for i in range(25)]
+        b = [0] * 25
+        for x in range(5):
+            for y in range(5):
+                b[y + 5 * ((2 * x + 3 * y) % 5)] = rot(a[x + 5 * y], R[x + 5 * y])
+        a = [b[i] ^ (~b[(i % 5 + 1) % 5 + 5 * (i // 5)] & b[(i % 5 + 2) % 5 + 5 * (i // 5)]) for i in range(25)]
+        # iota: round constant from the LFSR x^8 + x^6 + x^5 + x^4 + 1
+        v = 0
+        for j in range(7):
+            if rc & 1:
+                v |= 1 << ((1 << j) - 1)
+            rc = ((rc << 1) ^ (0x71 if rc & 0x80 else 0)) & 0xFF
+        a[0] ^= v
+    return a
+
+
+def _shake256_py(msg: bytes, n: int = 32) -> bytes:
+    rate = 136
+    m = bytearray(msg) + b"\x1f"
+    m += bytes(-len(m) % rate)
+    m[-1] |= 0x80
+    a = [0] * 25
+    for k in range(0, len(m), rate):
+        for i in range(rate // 8):
+            a[i] ^= int.from_bytes(m[k + 8 * i:k + 8 * i + 8], "little")
+        a = _keccak_f(a)
+    return b"".join(x.to_bytes(8, "little") for x in a)[:n]
+
+
+def test_shake256_kat_and_independent_keccak():
+    # crates/core/crypto/src/hash.rs:46-57 (NIST empty-input vector)
+    kat = "46b9dd2b0ba88d13233b3feb743eeb243fcd52ea62b81b82b50c27646ed5762f"
+    assert O.shake256_256(b"").hex() == kat and _shake256_py(b"").hex() == kat
+    # short_digest_is_long_digest_prefix (:59-65)
+    assert hashlib.shake_256(b"flakecache").digest(16) == O.shake256_256(b"flakecache")[:16]
+    rng = np.random.default_rng(1)
+    for n in (1, 109, 110, 111, 135, 136, 137, 271, 272, 273, 1000):
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert O.shake256_256(d) == _shake256_py(d), n
+
+
+def test_content_id_framing_and_golden():
+    """ContentId::compute framing (crates/core/cas/src/lib.rs:59-69) and the committed
+    vectors (tests/golden/cas_vectors.json, made by tests/golden/make_cas_vectors.py)."""
+    p = b"hello"
+    framed = b"flakecache-cas" + b"\x00" + b"\x01" + b"\x01\x00" + (5).to_bytes(8, "little") + p
+    assert len(framed) - len(p) == 26
+    assert O.content_id(O.KIND_CHUNK, p) == _shake256_py(framed)
+    # id_is_deterministic_and_kind_separated (crates/core/cas/src/lib.rs:254-261)
+    assert O.content_id(1, p) == O.content_id(1, p) != O.content_id(4, p)
+    g = json.loads((GOLDEN / "cas_vectors.json").read_text())
+    import sys
+    sys.path.insert(0, str(GOLDEN))
+    from make_cas_vectors import payload
+    for case in g["cases"]:
+        assert O.content_id(case["kind"], payload(case["len"], case["seed"])).hex() == case["id"], case
+
+
+def test_node_put_oracle_structure():
+    """Node::put (crates/node/src/lib.rs:114-132): the manifest is the Level1Manifest id of
+    the concatenated chunk ids; identical input -> identical manifest (:226-239)."""
+    rng = np.random.default_rng(2)
+    data = rng.integers(0, 256, 300_000, dtype=np.uint8)
+    descs, ids, man = O.node_put(data, 4096, 16_384, 65_536, nthreads=4)
+    assert len(ids) == len(descs) > 3
+    assert ids == [O.content_id(O.KIND_CHUNK, data[int(d["offset"]):int(d["offset"] + d["length"])])
+                   for d in descs]
+    assert man == O.content_id(O.KIND_LEVEL1_MANIFEST, b"".join(ids))
+    assert O.node_put(data, 4096, 16_384, 65_536)[2] == man
+    assert O.node_put(b"", 4096, 16_384, 65_536)[2] == O.content_id(O.KIND_LEVEL1_MANIFEST, b"")
