@@ -102,6 +102,63 @@ __device__ __forceinline__ void keccak_f(uint32_t lo[25], uint32_t hi[25]) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Pair tier: one span on a lane pair, lane h = 0 holding the low dwords of the 25
+// state lanes and h = 1 the high dwords.  Every 64-bit rotation is then the same
+// instruction on both lanes, new_own = alignbit(own, other) (r < 32) or
+// alignbit(other, own) (r > 32), with `other` the partner's half through one DPP
+// quad_perm swap; theta's parities, the a ^= d fold and chi touch only the lane's own
+// half.  ~120 VALU per round instead of ~180, so the longest span's chain is ~1.5x
+// shorter.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t partner(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
+}
+
+template <int R>
+__device__ __forceinline__ uint32_t rot_pair(uint32_t own) {
+    if constexpr (R == 0) {
+        return own;
+    } else if constexpr (R < 32) {
+        return __builtin_amdgcn_alignbit(own, partner(own), 32 - R);
+    } else if constexpr (R == 32) {
+        return partner(own);
+    } else {
+        return __builtin_amdgcn_alignbit(partner(own), own, 64 - R);
+    }
+}
+
+template <int I>
+__device__ __forceinline__ void rho_pi_pair(const uint32_t *a, uint32_t *b) {
+    constexpr int x = I % 5, y = I / 5, j = y + 5 * ((2 * x + 3 * y) % 5);
+    b[j] = rot_pair<KR(I)>(a[I]);
+    if constexpr (I < 24) rho_pi_pair<I + 1>(a, b);
+}
+
+// hmask = 0 on the low lane, ~0 on the high lane
+__device__ __forceinline__ void keccak_f_pair(uint32_t a[25], uint32_t hmask) {
+#pragma unroll
+    for (int round = 0; round < 24; ++round) {
+        uint32_t c[5], b[25];
+#pragma unroll
+        for (int x = 0; x < 5; ++x) c[x] = x3(x3(a[x], a[x + 5], a[x + 10]), a[x + 15], a[x + 20]);
+#pragma unroll
+        for (int x = 0; x < 5; ++x) {
+            const uint32_t d = rot_pair<1>(c[(x + 1) % 5]);
+#pragma unroll
+            for (int y = 0; y < 5; ++y) a[x + 5 * y] = x3(a[x + 5 * y], c[(x + 4) % 5], d);
+        }
+        rho_pi_pair<0>(a, b);
+#pragma unroll
+        for (int y = 0; y < 5; ++y)
+#pragma unroll
+            for (int x = 0; x < 5; ++x)
+                a[x + 5 * y] = chi3(b[x + 5 * y], b[(x + 1) % 5 + 5 * y], b[(x + 2) % 5 + 5 * y]);
+        // iota: own half of RC = lo ^ ((lo ^ hi) & hmask)
+        a[0] ^= KRC_LO[round] ^ ((KRC_LO[round] ^ KRC_HI[round]) & hmask);
+    }
+}
+
 constexpr uint32_t CAS_HDR = 26;   // "flakecache-cas" 0x00 kind u16le(1) u64le(len)
 constexpr uint32_t CAS_RATE = 136; // SHAKE256 rate in bytes (17 lanes)
 
@@ -126,72 +183,132 @@ __device__ __forceinline__ bool whole_block(uint64_t k, uint64_t mlen) {
 
 }  // namespace
 
-// Lanes take spans in the SHA-256 length order (longest first; `order` may be null).
-// Span g: bytes data[abs[g] .. abs[g] + desc[g].length); id -> ids + g * id_stride.
-__global__ __launch_bounds__(64) void k_cas_ids(const uint8_t *__restrict__ data, const uint64_t *__restrict__ abs,
-                                                const DescRaw *__restrict__ desc, const uint64_t *__restrict__ total_p,
-                                                uint64_t max_n, const uint32_t *__restrict__ order, uint32_t kind,
-                                                uint8_t *__restrict__ ids, uint64_t id_stride) {
-    uint64_t total = *total_p;
-    if (total > max_n) total = max_n;
-    const uint64_t slot = (uint64_t)blockIdx.x * 64 + threadIdx.x;
-    if (slot >= total) return;
-    const uint64_t g = order ? (uint64_t)order[slot] : slot;
-    const uint64_t len = desc[g].length;
-    const uint8_t *pay = data + abs[g];
+// Absorb-and-permute of one span.  PAIR: the calling lane holds half `h` of the
+// state (see keccak_f_pair); otherwise the whole state.  Writes the 32-byte id.
+template <bool PAIR>
+__device__ __forceinline__ void cas_span(const uint8_t *pay, uint64_t len, uint32_t kind, uint32_t h, uint8_t *id) {
     const uint64_t mlen = CAS_HDR + len;
     const uint64_t nblk = mlen / CAS_RATE + 1;  // the pad block always exists (mlen % rate < rate)
     const uint32_t shift = (uint32_t)((uintptr_t)pay & 3u);
     const uint32_t *base0 = reinterpret_cast<const uint32_t *>(pay - shift);
-
     const uint32_t sh = (shift + 2u) & 3u;
-    uint32_t lo[25], hi[25], dw[35];
+    constexpr int NW = PAIR ? 25 : 50;  // state dwords held by this lane
+    constexpr int ND = PAIR ? 34 : 35;  // block dwords loaded by this lane
+    uint32_t a[NW], dw[ND];
 #pragma unroll
-    for (int i = 0; i < 25; ++i) lo[i] = hi[i] = 0;
+    for (int i = 0; i < NW; ++i) a[i] = 0;
     // Aligned dwords of whole block k: payload bytes [136k - 26, 136k + 110) start
     // at dword (136k - 26 + shift) / 4 of base0, byte sh = (shift + 2) & 3 of it (136k - 26
-    // is 2 mod 4); dword 34 is needed only when sh > 0 and then lies inside the payload,
-    // so no load leaves the span.
+    // is 2 mod 4).  The last dword is needed only when sh > 0 and then lies inside the
+    // payload, so no load leaves the span.  A pair lane reads its stream one dword later
+    // on the high lane, so its halves are dw[2i], dw[2i + 1] on both lanes.
     auto load_whole = [&](uint64_t k) {
-        const uint32_t *b = base0 + ((k * CAS_RATE - CAS_HDR + shift) >> 2);
+        const uint32_t *b = base0 + ((k * CAS_RATE - CAS_HDR + shift) >> 2) + h;
 #pragma unroll
-        for (int i = 0; i < 34; ++i) dw[i] = __builtin_nontemporal_load(b + i);
-        dw[34] = sh ? __builtin_nontemporal_load(b + 34) : 0u;
+        for (int i = 0; i < ND - 1; ++i) dw[i] = __builtin_nontemporal_load(b + i);
+        dw[ND - 1] = (sh || (PAIR && !h)) ? __builtin_nontemporal_load(b + ND - 1) : 0u;
     };
     if (whole_block(1, mlen)) load_whole(1);
     for (uint64_t k = 0; k < nblk; ++k) {
         if (whole_block(k, mlen)) {
 #pragma unroll
             for (int i = 0; i < 17; ++i) {
-                lo[i] ^= __builtin_amdgcn_alignbyte(dw[2 * i + 1], dw[2 * i], sh);
-                hi[i] ^= __builtin_amdgcn_alignbyte(dw[2 * i + 2], dw[2 * i + 1], sh);
+                if constexpr (PAIR) {
+                    a[i] ^= __builtin_amdgcn_alignbyte(dw[2 * i + 1], dw[2 * i], sh);
+                } else {
+                    a[2 * i] ^= __builtin_amdgcn_alignbyte(dw[2 * i + 1], dw[2 * i], sh);
+                    a[2 * i + 1] ^= __builtin_amdgcn_alignbyte(dw[2 * i + 2], dw[2 * i + 1], sh);
+                }
             }
         } else {  // header block, last partial block or the pad block: byte by byte
             const uint64_t m0 = k * CAS_RATE;
             for (uint32_t i = 0; i < CAS_RATE; ++i) {
+                const uint32_t w = i >> 2;  // message dword; state dword w = half (w & 1) of lane w / 2
+                if (PAIR && (w & 1u) != h) continue;
                 const uint64_t m = m0 + i;
                 uint32_t v = m < mlen ? msg_byte(pay, len, kind, m) : 0u;
                 if (m == mlen) v ^= 0x1Fu;                          // SHAKE domain bits + first pad bit
                 if (k == nblk - 1 && i == CAS_RATE - 1) v ^= 0x80u;  // last pad bit
-                const uint32_t w = i >> 2, sb = 8 * (i & 3);
-                if (w & 1) hi[w >> 1] ^= v << sb;
-                else lo[w >> 1] ^= v << sb;
+                const uint32_t sb = 8 * (i & 3);
+                if constexpr (PAIR) {
+#pragma unroll
+                    for (int j = 0; j < 17; ++j)
+                        if ((uint32_t)j == (w >> 1)) a[j] ^= v << sb;
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 34; ++j)
+                        if ((uint32_t)j == w) a[j] ^= v << sb;
+                }
             }
         }
         if (whole_block(k + 1, mlen)) load_whole(k + 1);  // in flight during the permutation
-        keccak_f(lo, hi);
+        if constexpr (PAIR) {
+            keccak_f_pair(a, h ? ~0u : 0u);
+        } else {
+            uint32_t lo[25], hi[25];
+#pragma unroll
+            for (int i = 0; i < 25; ++i) {
+                lo[i] = a[2 * i];
+                hi[i] = a[2 * i + 1];
+            }
+            keccak_f(lo, hi);
+#pragma unroll
+            for (int i = 0; i < 25; ++i) {
+                a[2 * i] = lo[i];
+                a[2 * i + 1] = hi[i];
+            }
+        }
     }
-    uint4 *o = reinterpret_cast<uint4 *>(ids + id_stride * g);
-    o[0] = make_uint4(lo[0], hi[0], lo[1], hi[1]);
-    o[1] = make_uint4(lo[2], hi[2], lo[3], hi[3]);
+    uint32_t *o = reinterpret_cast<uint32_t *>(id);
+    if constexpr (PAIR) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[2 * i + h] = a[i];
+    } else {
+        reinterpret_cast<uint4 *>(id)[0] = make_uint4(a[0], a[1], a[2], a[3]);
+        reinterpret_cast<uint4 *>(id)[1] = make_uint4(a[4], a[5], a[6], a[7]);
+    }
 }
+
+// Slots take spans in the SHA-256 length order (longest first; `order` may be null).
+// Workgroups [0, npair_wg) run the pair tier on slots [0, 32 npair_wg), the rest one
+// lane per span.  Span g: bytes data[abs[g] .. abs[g] + desc[g].length); its id ->
+// ids + g * id_stride.
+__global__ __launch_bounds__(64) void k_cas_ids(const uint8_t *__restrict__ data, const uint64_t *__restrict__ abs,
+                                                const DescRaw *__restrict__ desc, const uint64_t *__restrict__ total_p,
+                                                uint64_t max_n, const uint32_t *__restrict__ order, uint32_t kind,
+                                                uint8_t *__restrict__ ids, uint64_t id_stride, uint32_t npair_wg) {
+    uint64_t total = *total_p;
+    if (total > max_n) total = max_n;
+    const bool pair = blockIdx.x < npair_wg;
+    const uint64_t slot = pair ? (uint64_t)blockIdx.x * 32 + (threadIdx.x >> 1)
+                               : (uint64_t)npair_wg * 32 + (uint64_t)(blockIdx.x - npair_wg) * 64 + threadIdx.x;
+    if (slot >= total) return;  // pair lanes leave together: both halves share the slot
+    const uint64_t g = order ? (uint64_t)order[slot] : slot;
+    const uint8_t *pay = data + abs[g];
+    if (pair)
+        cas_span<true>(pay, desc[g].length, kind, threadIdx.x & 1u, ids + id_stride * g);
+    else
+        cas_span<false>(pay, desc[g].length, kind, 0, ids + id_stride * g);
+}
+
+uint64_t g_cas_wave_budget = 1024;  // SIMDs of the chip
+int64_t g_cas_pair_max = -1;        // diagnostics/tests: cap on pair-tier spans (-1 = none)
 
 void launch_cas_ids(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
                     uint64_t max_n, const uint32_t *d_order, uint32_t kind, uint8_t *d_ids, size_t id_stride,
                     hipStream_t st) {
     if (max_n == 0) return;
-    hipLaunchKernelGGL(k_cas_ids, dim3((uint32_t)((max_n + 63) / 64)), dim3(64), 0, st, d_data, d_abs,
-                       (const DescRaw *)d_desc, d_total, max_n, d_order, kind, d_ids, (uint64_t)id_stride);
+    // Pair tier for the longest spans while the whole grid still fits one wave per SIMD
+    // (256 CUs x 4): npair spans cost npair / 64 extra waves over the one-lane grid.
+    const uint64_t single_waves = (max_n + 63) / 64;
+    uint64_t npair = single_waves < g_cas_wave_budget ? 64 * (g_cas_wave_budget - single_waves) : 0;
+    if (npair > max_n) npair = max_n;
+    if (g_cas_pair_max >= 0 && npair > (uint64_t)g_cas_pair_max) npair = (uint64_t)g_cas_pair_max;
+    const uint32_t npair_wg = (uint32_t)((npair + 31) / 32);
+    const uint64_t rest = max_n > 32 * (uint64_t)npair_wg ? max_n - 32 * (uint64_t)npair_wg : 0;
+    const uint32_t nwg = npair_wg + (uint32_t)((rest + 63) / 64);
+    hipLaunchKernelGGL(k_cas_ids, dim3(nwg), dim3(64), 0, st, d_data, d_abs, (const DescRaw *)d_desc, d_total, max_n,
+                       d_order, kind, d_ids, (uint64_t)id_stride, npair_wg);
 }
 
 // Manifest spans (crates/node/src/lib.rs:124-129): NAR i's manifest is the
@@ -214,3 +331,11 @@ void launch_manifest_spans(const uint64_t *d_first, uint64_t n_nars, uint64_t *d
 }
 
 }  // namespace cg
+
+// Diagnostics / tests: cap the pair tier (-1 = budget only, 0 = one lane per span
+// everywhere); returns the previous cap.
+extern "C" int64_t cg_diag_cas_pair_max(int64_t v) {
+    const int64_t old = cg::g_cas_pair_max;
+    cg::g_cas_pair_max = v;
+    return old;
+}

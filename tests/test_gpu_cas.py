@@ -58,8 +58,26 @@ def test_shake_kat_and_reference_cas_cases(cas, O):
     assert a == b and a != c and len(a.to_hex()) == 64
 
 
-def test_cas_ids_all_lengths_and_alignments(cas, O):
+def _pair_max(v):
+    """Cap the CAS pair tier (cg_diag_cas_pair_max): -1 = wave budget only, 0 = one lane
+    per span everywhere, k = the k longest spans on lane pairs; returns the old cap."""
+    import ctypes
+
+    from chunker_amd import lib
+
+    f = lib.cg_diag_cas_pair_max
+    f.argtypes, f.restype = [ctypes.c_int64], ctypes.c_int64
+    return f(v)
+
+
+TIERS = pytest.mark.parametrize("pair_max", [-1, 0, 37], ids=["pairs", "single", "mixed"])
+
+
+@TIERS
+def test_cas_ids_all_lengths_and_alignments(cas, O, pair_max):
     import torch
+
+    old = _pair_max(pair_max)
 
     rng = np.random.default_rng(17)
     data = rng.integers(0, 256, 4 << 20, dtype=np.uint8)
@@ -75,6 +93,7 @@ def test_cas_ids_all_lengths_and_alignments(cas, O):
         ids = ids.cpu().numpy().reshape(-1, 32)
         for k, (a, n) in enumerate(zip(offs, lens)):
             assert bytes(ids[k]) == O.content_id(int(kind), data[a:a + n]), (int(kind), n, a)
+    _pair_max(old)
 
 
 def test_node_put_matches_oracle(cas, O):
@@ -134,9 +153,12 @@ def test_node_put_batch_device(cas, O, params):
         assert bytes(man[i]) == rman, i
 
 
-def test_cas_many_spans_ordered(cas, O):
+@TIERS
+def test_cas_many_spans_ordered(cas, O, pair_max):
     """> 64 spans of mixed lengths: the longest-first order path."""
     import torch
+
+    old = _pair_max(pair_max)
 
     rng = np.random.default_rng(23)
     data = rng.integers(0, 256, 8 << 20, dtype=np.uint8)
@@ -150,4 +172,5 @@ def test_cas_many_spans_ordered(cas, O):
     ids = ids.cpu().numpy().reshape(-1, 32)
     want = O.content_ids(data, np.array(list(zip(offs, lens)), dtype=[("offset", "<u8"), ("length", "<u8")]),
                          O.KIND_CHUNK, nthreads=8)
+    _pair_max(old)
     assert [bytes(x) for x in ids] == want
