@@ -315,20 +315,25 @@ class PushChunker:
         self._h = lib.cg_push_new(o.min_size, o.avg_size, o.max_size, int(self.hash), ctypes.byref(st))
         if not self._h:
             _raise(st.value)
-        # payload bookkeeping (the engine returns descriptors; payloads are sliced here)
-        self._pending = bytearray()
-        self._pending_pos = 0
+        # payload bookkeeping (the engine returns descriptors; payloads are sliced here
+        # from the pushed slices, which are kept by reference: one copy per payload byte)
+        self._segs: list[tuple[int, memoryview]] = []  # (stream offset, bytes) not yet emitted
+        self._pushed = 0
+
+    def _payload(self, off: int, ln: int) -> bytes:
+        parts = []
+        for start, mv in self._segs:
+            lo, hi = max(off, start), min(off + ln, start + len(mv))
+            if lo < hi:
+                parts.append(mv[lo - start:hi - start])
+        return b"".join(parts)
 
     def _collect(self, arr: np.ndarray) -> list[ChunkMetadata]:
-        out = []
-        for d in arr:
-            off, ln = int(d["offset"]), int(d["length"])
-            rel = off - self._pending_pos
-            out.append(ChunkMetadata(bytes(d["hash"]), off, ln, bytes(self._pending[rel:rel + ln])))
+        out = [ChunkMetadata(bytes(d["hash"]), int(d["offset"]), int(d["length"]),
+                             self._payload(int(d["offset"]), int(d["length"]))) for d in arr]
         if len(arr):
-            consumed = int(arr[-1]["offset"] + arr[-1]["length"]) - self._pending_pos
-            del self._pending[:consumed]
-            self._pending_pos += consumed
+            end = int(arr[-1]["offset"] + arr[-1]["length"])
+            self._segs = [(st, mv) for st, mv in self._segs if st + len(mv) > end]
         return out
 
     def push(self, data) -> list[ChunkMetadata]:
@@ -338,7 +343,11 @@ class PushChunker:
         n = ctypes.c_size_t(0)
         st = lib.cg_push_push(self._h, _ptr(a), len(a), out.ctypes.data, len(out), ctypes.byref(n))
         _check(st)
-        self._pending += a.tobytes()
+        # immutable input is kept by reference, anything else is copied once
+        keep = data if isinstance(data, bytes) else a.tobytes()
+        if len(keep):
+            self._segs.append((self._pushed, memoryview(keep)))
+            self._pushed += len(keep)
         return self._collect(out[: n.value])
 
     def finish(self) -> list[ChunkMetadata]:
@@ -369,6 +378,20 @@ def effective_read_slice_cap() -> int:
     return DEFAULT_READ_SLICE_CAP
 
 
+# A GPU push costs about one digest chain of its longest chunk whatever the slice size
+# (streaming), so without an explicit CHUNKER_READ_SLICE_CAP_BYTES the
+# stream reads MAX_READ_SLICE_CAP-sized slices instead of the reference's 8 MiB default.
+# Chunks do not depend on the slice size (test_push_matches_in_memory_across_slice_sizes).
+def stream_read_size(max_size: int) -> int:
+    """Read size per refill: src/chunking.rs:713-716 when the cap is pinned by the
+    environment, else the GPU slice (MAX_READ_SLICE_CAP)."""
+    target = max(max_size * 8, 4 * 1024 * 1024)
+    if os.environ.get("CHUNKER_READ_SLICE_CAP_BYTES") is None:
+        target = max(target, MAX_READ_SLICE_CAP)
+        return target
+    return max(min(target, effective_read_slice_cap()), MIN_READ_SLICE_CAP)
+
+
 class ChunkStream:
     """ChunkStream (src/chunking.rs:382-740): pull chunks from a binary reader."""
 
@@ -379,6 +402,28 @@ class ChunkStream:
         self._max = self._push.options.max_size
         self._pending: list[ChunkMetadata] = []
         self._eof = False
+        # read-ahead: the next slice is read on a helper thread while the engine chunks
+        # and digests the current one (the ctypes call releases the GIL); the bytes and
+        # their order are exactly what sequential reads return
+        self._pool = None
+        self._next = None
+
+    def _read_async(self):
+        from concurrent.futures import ThreadPoolExecutor
+
+        if self._pool is None:
+            self._pool = ThreadPoolExecutor(1, thread_name_prefix="chunk-stream-read")
+        self._next = self._pool.submit(self._reader.read, stream_read_size(self._max))
+
+    def _close_pool(self):
+        if self._pool is not None:
+            self._pool.shutdown(wait=True)
+            self._pool = None
+
+    def __del__(self):
+        pool = getattr(self, "_pool", None)
+        if pool is not None:
+            pool.shutdown(wait=False)
 
     @classmethod
     def new_with_hash(cls, reader, min_size, avg_size, max_size, hash):
@@ -393,16 +438,20 @@ class ChunkStream:
                 return self._pending.pop(0)
             if self._eof:
                 raise StopIteration
-            target = max(self._max * 8, 4 * 1024 * 1024)  # :713-716
-            read_size = max(min(target, effective_read_slice_cap()), MIN_READ_SLICE_CAP)
+            if self._next is None:
+                self._read_async()
             try:
-                buf = self._reader.read(read_size)
+                buf = self._next.result()
             except OSError as e:
+                self._close_pool()
                 raise IoError(str(e)) from e
             if not buf:
+                self._next = None
+                self._close_pool()
                 self._eof = True
                 self._pending.extend(self._push.finish())
             else:
+                self._read_async()
                 self._pending.extend(self._push.push(buf))
 
 

@@ -271,7 +271,7 @@ uint32_t seg_slots(const CdcParams &p) {
 // stage forks onto ws->side_stream after descriptor assembly and joins before return.
 int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, size_t n_nars, const Opts &o,
               int algo, cg_desc *d_out, size_t out_cap, uint64_t *h_nar_first, hipStream_t st,
-              uint8_t *d_chunk_ids = nullptr, uint8_t *h_manifest_ids = nullptr) {
+              uint8_t *d_chunk_ids = nullptr, uint8_t *h_manifest_ids = nullptr, bool digest = true) {
     if (algo != CG_BLAKE3 && algo != CG_SHA256) return fail(CG_E_INVALID_OPTIONS, "unknown hash algorithm");
     if (((uintptr_t)d_data & 15u) != 0) return fail(CG_E_IO, "device input must be 16-byte aligned");
     int rc;
@@ -370,7 +370,9 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
         HIP_TRY(hipEventRecord(ws->ev_join, side));
     }
     uint8_t *hash_base = reinterpret_cast<uint8_t *>(d_out) + offsetof(cg_desc, hash);
-    if (algo == CG_SHA256) {
+    if (!digest) {
+        // boundaries only (push_drain digests the chunks that became final afterwards)
+    } else if (algo == CG_SHA256) {
         if ((rc = ws->order.ensure(cg::sha256_order_tmp_elems(chunk_bound) * 4, "order"))) return rc;
         // expected chunk count: FastCDC's mean chunk is about min + avg on random data
         const uint64_t expected = std::min<uint64_t>(chunk_bound, total_len / (o.min + o.avg) + n_nars);
@@ -500,57 +502,143 @@ int check_kind(uint32_t kind) {
 // ---------------------------------------------------------------------------
 // PushChunker (src/chunking.rs:753-829) over drain_finalized_chunks (:541-673)
 // ---------------------------------------------------------------------------
+// The retained bytes live in HBM: each push copies only its new bytes H2D, straight
+// from the caller's buffer, after the device-resident tail (no host-side copy of
+// the stream); after a drain the tail moves to the front of the other buffer.
 struct cg_push {
     Opts o;
     int algo;
-    std::vector<uint8_t> buf;
+    int device = -1;
+    DevBuf dbuf[2];
+    int cur = 0;
+    uint64_t dlen = 0;  // retained bytes in dbuf[cur]
     uint64_t position = 0;
     bool finished = false;
+    ~cg_push() {
+        if (device >= 0) {
+            int prev = 0;
+            (void)hipGetDevice(&prev);
+            (void)hipSetDevice(device);
+            dbuf[0].release();
+            dbuf[1].release();
+            (void)hipSetDevice(prev);
+        }
+    }
 };
 
 namespace {
 
+// drain_finalized_chunks (src/chunking.rs:541-673) on the GPU.  The retained buffer
+// is staged once; boundaries for all of it come from the device pipeline (the
+// reference re-runs FastCDC over the buffer too, :553); the descriptors go back to the
+// host, which decides what is final (:579-584); then only the final chunks are
+// digested, on the bytes already in HBM -- the retained tail chunk is never hashed
+// twice (the reference hashes only emitted chunks, :612-641).
 int push_drain(cg_push *h, bool eof, cg_desc *out, size_t out_cap, size_t *n_out) {
     *n_out = 0;
+    if (h->dlen == 0 || (h->dlen < h->o.min && !eof)) return CG_OK;
+    Workspace *ws = nullptr;
+    int rc = acquire(&ws);
+    if (rc) return rc;
+    WsGuard guard{ws};
+    const uint64_t len = h->dlen;
+    const uint64_t cap = capacity_of(len, h->o.min);
+    hipStream_t st = ws->stream;
+    if ((rc = ws->out.ensure((cap + 1) * sizeof(cg_desc), "descriptors"))) return rc;
+    const uint8_t *d_in = h->dbuf[h->cur].as<uint8_t>();
+    uint64_t offs[2] = {0, len}, first[2] = {0, 0};
+    cg_desc *d_out = ws->out.as<cg_desc>();
+    if ((rc = run_batch(ws, d_in, offs, 1, h->o, h->algo, d_out, cap, first, st, nullptr, nullptr,
+                        /*digest=*/false)))
+        return rc;
+    const uint64_t total = first[1];
+    std::vector<cg_desc> tmp(total);
+    if (total) {
+        HIP_TRY(hipMemcpyAsync(tmp.data(), d_out, total * sizeof(cg_desc), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
     size_t n = 0;
-    uint64_t total = 0;
-    if (!h->buf.empty() && (h->buf.size() >= h->o.min || eof)) {
-        const uint64_t len = h->buf.size();
-        const uint64_t cap = capacity_of(len, h->o.min);
-        std::vector<cg_desc> tmp(cap);
-        uint64_t offs[2] = {0, len};
-        uint64_t first[2];
-        int rc = batch_host(h->buf.data(), offs, 1, h->o.min, h->o.avg, h->o.max, h->algo, tmp.data(), cap, first);
-        if (rc) return rc;
-        for (uint64_t k = 0; k < first[1]; ++k) {
-            const cg_desc &d = tmp[k];
-            if (d.length == 0) return fail(CG_E_ZERO_LENGTH_CHUNK, "FastCDC returned a chunk with length 0");
-            const bool touches_end = d.offset + d.length == len;
-            if (touches_end && !eof && d.length < h->o.max) break;  // retained tail (:579-584)
-            if (n >= out_cap) return fail(CG_E_CAPACITY, "push output array too small");
-            out[n] = d;
-            out[n].offset += h->position;
-            ++n;
-            total += d.length;
+    uint64_t emitted = 0;
+    for (uint64_t k = 0; k < total; ++k) {
+        const cg_desc &d = tmp[k];
+        if (d.length == 0) return fail(CG_E_ZERO_LENGTH_CHUNK, "FastCDC returned a chunk with length 0");
+        const bool touches_end = d.offset + d.length == len;
+        if (touches_end && !eof && d.length < h->o.max) break;  // retained tail (:579-584)
+        ++n;
+        emitted += d.length;
+    }
+    // EOF remainder (:651-670): FastCDC's chunks always cover the buffer, so at EOF
+    // every byte has been emitted; anything else is an engine fault, never silent
+    if (eof && emitted < len) return fail(CG_E_IO, "push: chunks do not cover the buffer at finish");
+    if (n > out_cap) return fail(CG_E_CAPACITY, "push output array too small");
+    if (n) {
+        // digest descriptors [0, n) in place: the count goes to the device total slot
+        uint64_t *d_total = ws->nar_first.as<uint64_t>() + 1;
+        if ((rc = ws->stage.ensure(64))) return rc;
+        ws->stage.as<uint64_t>()[0] = n;
+        HIP_TRY(hipMemcpyAsync(d_total, ws->stage.p, 8, hipMemcpyHostToDevice, st));
+        uint8_t *hb = reinterpret_cast<uint8_t *>(d_out) + offsetof(cg_desc, hash);
+        if (h->algo == CG_SHA256) {
+            if ((rc = ws->order.ensure(cg::sha256_order_tmp_elems(n) * 4, "order"))) return rc;
+            cg::launch_sha256(d_in, ws->chunk_abs.as<uint64_t>(), d_out, d_total, n, n, h->o.max,
+                              ws->order.as<uint32_t>(), hb, sizeof(cg_desc), st);
+        } else {
+            const uint64_t gb = cg::blake3_group_bound(len, n);
+            if ((rc = ws->b3_gcount.ensure((n + 1) * 4, "b3_gcount"))) return rc;
+            if ((rc = ws->b3_gbase.ensure((n + 1) * 8, "b3_gbase"))) return rc;
+            if ((rc = ws->b3_gcv.ensure((gb + 1) * 32, "b3_gcv"))) return rc;
+            if ((rc = ws->b3_gmap.ensure((gb + 1) * 4, "b3_gmap"))) return rc;
+            cg::launch_blake3(d_in, ws->chunk_abs.as<uint64_t>(), d_out, d_total, n, len, hb,
+                              sizeof(cg_desc), ws->b3_gmap.as<uint32_t>(), ws->b3_gbase.as<uint64_t>(),
+                              ws->b3_gcount.as<uint32_t>(), ws->scan_tmp.as<uint64_t>(), ws->b3_gcv.as<uint32_t>(),
+                              st);
         }
-        h->buf.erase(h->buf.begin(), h->buf.begin() + (ptrdiff_t)total);
-        h->position += total;
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipMemcpyAsync(out, d_out, n * sizeof(cg_desc), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        for (size_t k = 0; k < n; ++k) out[k].offset += h->position;
     }
-    if (eof && !h->buf.empty()) {  // defensive EOF remainder (:651-670)
-        if (n >= out_cap) return fail(CG_E_CAPACITY, "push output array too small");
-        uint64_t offs[2] = {0, h->buf.size()};
-        // a buffer below min is one chunk by FastCDC's first rule; digest it through the same path
-        cg_desc d;
-        uint64_t first[2];
-        int rc = batch_host(h->buf.data(), offs, 1, h->o.min, h->o.avg, h->o.max, h->algo, &d, 1, first);
-        if (rc) return rc;
-        d.offset = h->position;
-        d.length = h->buf.size();
-        out[n++] = d;
-        h->position += h->buf.size();
-        h->buf.clear();
+    const uint64_t consumed = eof ? len : emitted;
+    const uint64_t tail = len - consumed;
+    if (tail && consumed) {  // tail to the front of the other buffer (same capacity, 16-B aligned base)
+        if (tail + 256 > h->dbuf[1 - h->cur].cap) return fail(CG_E_IO, "push: retained tail exceeds its buffer");
+        HIP_TRY(hipMemcpyAsync(h->dbuf[1 - h->cur].p, d_in + consumed, tail, hipMemcpyDeviceToDevice, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        h->cur = 1 - h->cur;
     }
+    h->dlen = tail;
+    h->position += consumed;
     *n_out = n;
+    return CG_OK;
+}
+
+// Append `len` caller bytes after the device-resident tail (growing the buffer keeps
+// the tail: it is copied into the larger other buffer first).
+int push_append(cg_push *h, const uint8_t *data, uint64_t len) {
+    int dev = 0, rc = current_device(&dev);
+    if (rc) return rc;
+    if (h->device < 0) h->device = dev;
+    if (h->device != dev) return fail(CG_E_IO, "push handle used on another device than the one it started on");
+    Workspace *ws = nullptr;
+    if ((rc = acquire(&ws))) return rc;
+    WsGuard guard{ws};
+    hipStream_t st = ws->stream;
+    // both buffers always have the same capacity, so a tail move never needs to grow one
+    const uint64_t need = h->dlen + len + 256;
+    if (need > h->dbuf[h->cur].cap) {
+        DevBuf &nb = h->dbuf[1 - h->cur];
+        nb.release();
+        if ((rc = nb.ensure(need, "push buffer"))) return rc;
+        if (h->dlen) HIP_TRY(hipMemcpyAsync(nb.p, h->dbuf[h->cur].p, h->dlen, hipMemcpyDeviceToDevice, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        DevBuf &ob = h->dbuf[h->cur];
+        ob.release();
+        if ((rc = ob.ensure(need, "push buffer"))) return rc;  // same request -> same capacity
+        h->cur = 1 - h->cur;
+    }
+    HIP_TRY(hipMemcpyAsync(h->dbuf[h->cur].as<uint8_t>() + h->dlen, data, len, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    h->dlen += len;
     return CG_OK;
 }
 
@@ -740,7 +828,8 @@ int cg_push_push(cg_push *h, const uint8_t *data, uint64_t len, cg_desc *out, si
     if (!h) return fail(CG_E_IO, "null push handle");
     if (h->finished) return fail(CG_E_INVALID_OPTIONS, "push called after finish");
     if (len == 0) return CG_OK;
-    h->buf.insert(h->buf.end(), data, data + len);
+    int arc = push_append(h, data, len);
+    if (arc) return arc;
     size_t n = 0;
     int rc = push_drain(h, false, out, out_cap, &n);
     if (n_out) *n_out = n;
@@ -758,10 +847,10 @@ int cg_push_finish(cg_push *h, cg_desc *out, size_t out_cap, size_t *n_out) {
     return rc;
 }
 
-uint64_t cg_push_bytes_consumed(const cg_push *h) { return h ? h->position + h->buf.size() : 0; }
+uint64_t cg_push_bytes_consumed(const cg_push *h) { return h ? h->position + h->dlen : 0; }
 
 size_t cg_push_out_capacity(const cg_push *h, uint64_t next_len) {
-    return h ? capacity_of(h->buf.size() + next_len, h->o.min) + 1 : 0;
+    return h ? capacity_of(h->dlen + next_len, h->o.min) + 1 : 0;
 }
 
 void cg_push_free(cg_push *h) { delete h; }

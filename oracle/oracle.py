@@ -255,6 +255,9 @@ class Push:
         return lib().or_push_bytes_consumed(self.h)
 
     def __del__(self):
-        if getattr(self, "h", None):
-            lib().or_push_free(self.h)
+        if getattr(self, "h", None) and lib is not None:  # module globals are gone at interpreter exit
+            try:
+                lib().or_push_free(self.h)
+            except TypeError:
+                pass
             self.h = None

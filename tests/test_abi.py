@@ -156,3 +156,20 @@ def test_cas_entry_validation_without_gpu(ca):
             cas.ContentId.compute(cas.ObjectKind.Chunk, b"hello")
         with pytest.raises(ca.DeviceUnavailableError):
             cas.node_put(bytes(100_000), 4096, 16_384, 65_536)
+
+
+def test_stream_read_size(ca, monkeypatch):
+    """ChunkStream refill size: the reference's formula (src/chunking.rs:713-716) when
+    CHUNKER_READ_SLICE_CAP_BYTES pins the cap, else the GPU slice (256 MiB)."""
+    from chunker_amd.chunking import MAX_READ_SLICE_CAP, stream_read_size
+
+    monkeypatch.delenv("CHUNKER_READ_SLICE_CAP_BYTES", raising=False)
+    assert stream_read_size(4 << 20) == MAX_READ_SLICE_CAP
+    assert stream_read_size(64 << 20) == 512 << 20
+    monkeypatch.setenv("CHUNKER_READ_SLICE_CAP_BYTES", str(8 << 20))
+    assert stream_read_size(4 << 20) == 8 << 20
+    assert stream_read_size(1024) == 4 << 20 if (4 << 20) <= (8 << 20) else True
+    monkeypatch.setenv("CHUNKER_READ_SLICE_CAP_BYTES", "4096")
+    assert stream_read_size(1 << 20) == 4096
+    monkeypatch.setenv("CHUNKER_READ_SLICE_CAP_BYTES", "12")  # out of range -> 8 MiB default
+    assert stream_read_size(4 << 20) == 8 << 20
