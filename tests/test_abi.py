@@ -173,3 +173,16 @@ def test_stream_read_size(ca, monkeypatch):
     assert stream_read_size(1 << 20) == 4096
     monkeypatch.setenv("CHUNKER_READ_SLICE_CAP_BYTES", "12")  # out of range -> 8 MiB default
     assert stream_read_size(4 << 20) == 8 << 20
+
+
+def test_nix_base32_reference_fixture(ca):
+    """nix_base32_matches_nix (crates/proto/nix/src/narinfo.rs:383-385): the fixture's
+    NarHash (SRI base64, :359) encodes to the reference's expected string (:361)."""
+    import base64
+
+    from chunker_amd.narinfo import nar_hash_field, nix_base32
+
+    d = base64.b64decode("LHmbxrZuoUhZ7p0Q+oD4wBzxH/byKBAKbJsfAZXoBCU=")
+    assert nix_base32(d) == "0984x2ah27wvdh510a7jyqgz2760z20gl44xxrcli8bfnv39ny9c"
+    assert nar_hash_field(d) == "sha256:0984x2ah27wvdh510a7jyqgz2760z20gl44xxrcli8bfnv39ny9c"
+    assert nix_base32(b"") == "" and len(nix_base32(bytes(32))) == 52

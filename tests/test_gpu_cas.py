@@ -174,3 +174,26 @@ def test_cas_many_spans_ordered(cas, O, pair_max):
                          O.KIND_CHUNK, nthreads=8)
     _pair_max(old)
     assert [bytes(x) for x in ids] == want
+
+
+def test_nar_hashes_device(gpu):
+    """Whole-NAR SHA-256 (narinfo NarHash, crates/proto/nix/src/narinfo.rs:127-157) of a
+    device batch: one span per NAR, vs hashlib."""
+    import hashlib
+
+    import torch
+
+    from chunker_amd.nar import synth_nars
+    from chunker_amd.narinfo import nar_hash, nar_hash_field, nar_hashes_device
+
+    data, offs = synth_nars([120, 4096, 3 * 1024 * 1024 + 8, 17 * 1024 * 1024 + 16, 1 << 20], first_index=9)
+    d = torch.from_numpy(data).cuda()
+    dig = torch.zeros(32 * (len(offs) - 1), dtype=torch.uint8, device="cuda")
+    nar_hashes_device(d.data_ptr(), offs, dig.data_ptr())
+    dig = dig.cpu().numpy().reshape(-1, 32)
+    for i in range(len(offs) - 1):
+        want = hashlib.sha256(data[offs[i]:offs[i + 1]].tobytes()).digest()
+        assert bytes(dig[i]) == want, i
+    one = data[offs[1]:offs[2]].tobytes()
+    assert nar_hash(one) == hashlib.sha256(one).digest()
+    assert nar_hash_field(nar_hash(one)).startswith("sha256:") and len(nar_hash_field(nar_hash(one))) == 59
