@@ -1,27 +1,33 @@
 """bench.py -- device-resident FastCDC + per-chunk digest throughput on MI355X.
 
-Metric (BASELINE.json): "device-resident GiB/s FastCDC+SHA-256 over synthetic NARs".
-A step is one pass of the hot path (candidate scan -> cut walk -> descriptor
-assembly -> per-chunk digest) over one batch of synthetic NARs already resident in
-HBM, through the C ABI entry cg_chunk_batch_device.  Default workload = BASELINE
-config 2: 256 x 4 MiB NARs, 256K/1M/4M, SHA-256, per GPU.
+Metric (BASELINE.json): "device-resident GiB/s FastCDC+SHA-256 over synthetic NARs,
+1/2/4/8 MI355X".  A step is one pass of the hot path (candidate scan -> cut walk ->
+descriptor assembly -> per-chunk digest) over one batch of synthetic NARs already
+resident in HBM, through the C ABI entry cg_chunk_batch_device.  Default workload =
+BASELINE config 2: 256 x 4 MiB NARs per GPU, 256K/1M/4M, SHA-256.
 
-Multi-GPU (torchrun, one rank per GPU): every rank owns its own batch of NARs
-(NAR indices rank*n .. rank*n+n-1: one-file-per-GPU sharding, weak scaling); after
-each step the per-NAR descriptor counts and the descriptor arrays are gathered to
-rank 0 over RCCL (the only exchange the path has).  value = all ranks' bytes /
-max-over-ranks time.
+Multi-GPU: `--gpus N` with no torchrun environment starts N ranks itself (a child
+`python -m torch.distributed.run`; this parent never touches a GPU); under the
+driver's torchrun each process is one rank.  NARs are sharded one-file-per-GPU with
+chunker_amd.dist.shard_nars over n_per_gpu x N NARs (weak scaling; config c5 = 16 x
+1 GiB per GPU, i.e. BASELINE config 5's 128 x 1 GiB at N = 8); every step ends with
+the descriptors gathered to rank 0 over RCCL, the path's only exchange.  value = all
+ranks' bytes / max-over-ranks time.
 
-Extra JSON keys: roofline (dominant kernel, HIP-event timed on the stream the
-kernels run on), cpu_baseline (the oracle's restatement of chunk_data, rank 0),
-stages_ms (per-stage device times), chunks.
+Extra JSON keys: roofline (dominant kernel, HIP events on the stream the kernels run
+on), cpu_baseline (the oracle's restatement of chunk_data, rank 0 at N = 1 only),
+stages_ms, chunks, gear_table, and at N = 1 `concurrent`: K independent batches in
+flight on K streams from K host threads (the reference's callers are concurrent).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
+import threading
 import time
 from pathlib import Path
 
@@ -32,21 +38,23 @@ sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak, /opt/skills/guides/MI355X_MICROARCH.md
 GIB = 1024 ** 3
+PUBLISHED_CHUNK_DATA_ZEROS = 1.055  # GiB/s, chunk_data_eager_10mb_sha256 (benchmarks/latest.md:12)
 
 CONFIGS = {
-    # name: (n_nars, nar_bytes, (min, avg, max), algo, description)
+    # name: (nars per GPU, nar_bytes, (min, avg, max), algo, description)
     "c2": (256, 4 << 20, (256 << 10, 1 << 20, 4 << 20), 1,
-           "256x4MiB synthetic NARs, 256K/1M/4M, SHA-256 (BASELINE config 2)"),
+           "256x4MiB synthetic NARs per GPU, 256K/1M/4M, SHA-256 (BASELINE config 2)"),
     "c3": (256, 4 << 20, (256 << 10, 1 << 20, 4 << 20), 0,
-           "256x4MiB synthetic NARs, 256K/1M/4M, BLAKE3 (BASELINE config 3)"),
+           "256x4MiB synthetic NARs per GPU, 256K/1M/4M, BLAKE3 (BASELINE config 3)"),
     "c4": (16, 1 << 30, (64 << 10, 256 << 10, 1 << 20), 1,
-           "16x1GiB synthetic NARs, 64K/256K/1M, SHA-256 (BASELINE config 4)"),
+           "16x1GiB synthetic NARs per GPU, 64K/256K/1M, SHA-256 (BASELINE config 4)"),
     "c5": (16, 1 << 30, (256 << 10, 1 << 20, 4 << 20), 1,
-           "16x1GiB synthetic NARs per GPU, 256K/1M/4M, SHA-256 (BASELINE config 5 shard)"),
+           "16x1GiB synthetic NARs per GPU (128x1GiB at 8 GPUs), 256K/1M/4M, SHA-256, RCCL gather "
+           "(BASELINE config 5)"),
 }
 
 
-def main():
+def parse_args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -54,8 +62,31 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--zeros", action="store_true", help="all-zero payloads (the reference's bench data)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-nars", type=int, default=0, help="0 = whole batch (config c2/c3)")
-    args = ap.parse_args()
+    ap.add_argument("--cpu-sample-nars", type=int, default=0, help="0 = whole batch for c2/c3, 1 NAR for c4/c5")
+    ap.add_argument("--no-concurrent", action="store_true", help="skip the K-batches-in-flight measurement")
+    ap.add_argument("--concurrent", default="8,32", help="K values of the in-flight measurement")
+    ap.add_argument("--concurrent-only", action="store_true", help="only the in-flight measurement (profiling)")
+    return ap.parse_args()
+
+
+def launch_ranks(n: int) -> int:
+    """Start n ranks as one child torchrun process (127.0.0.1 rendezvous) and return
+    its exit code.  Nothing here initialises HIP: the GPUs belong to the children."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *sys.argv[1:]]
+    return subprocess.call(cmd)
+
+
+def main():
+    args = parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    # The installed GEAR table is the labelled placeholder (tables/README.md) and the
+    # engine refuses to chunk with it unless opted in; the JSON says which table ran.
+    os.environ.setdefault("CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR", "1")
 
     import torch
     import torch.distributed as dist
@@ -70,26 +101,27 @@ def main():
         torch.cuda.set_device(0)
 
     import chunker_amd as ca
-    from chunker_amd.nar import synth_nars
+    from chunker_amd.dist import gather_batch, shard_nars
+    from chunker_amd.nar import synth_nars_device
 
-    n_nars, nar_bytes, params, algo, desc = CONFIGS[args.config]
-    sizes = np.full(n_nars, nar_bytes, np.uint64)
-    host, offs = synth_nars(sizes, zeros=args.zeros, first_index=rank * n_nars)
+    n_per, nar_bytes, params, algo, desc = CONFIGS[args.config]
+    if args.concurrent_only:
+        print(json.dumps({"concurrent": concurrent_rates(ca, torch, args, n_per, nar_bytes, params, algo)}))
+        return
+    mine = shard_nars(n_per * world, world, rank)
+    sizes = np.full(len(mine), nar_bytes, np.uint64)
+    d_data, offs = synth_nars_device(sizes, zeros=args.zeros, first_index=mine.start)
     total_bytes = int(offs[-1])
-    d_data = torch.empty(total_bytes + 256, dtype=torch.uint8, device="cuda")
-    d_data[:total_bytes].copy_(torch.from_numpy(host))
     cap = ca.chunking.batch_capacity(offs, params[0])
     d_out = torch.empty(cap * 48, dtype=torch.uint8, device="cuda")
     stream = torch.cuda.current_stream()
     sptr = stream.cuda_stream
 
-    from chunker_amd.dist import gather_descriptors
-
     def step():
         first = ca.chunk_batch_device(d_data.data_ptr(), offs, d_out.data_ptr(), cap, *params, hash=algo,
                                       stream=sptr)
-        if world > 1:  # descriptors to rank 0 over RCCL (the path's only exchange)
-            gather_descriptors(d_out, int(first[-1]))
+        if world > 1:  # descriptors + NAR index to rank 0 over RCCL (the path's only exchange)
+            gather_batch(d_out, first)
         return first
 
     for _ in range(args.warmup):
@@ -121,9 +153,9 @@ def main():
     stages_ms = dict(zip(["scan", "compact", "walk", "assemble", "digest"],
                          stage[: max(args.steps, 1)].mean(axis=0).round(4)))
 
-    # parity spot check on the last step (rank 0): descriptors cover every NAR exactly
+    # parity spot check on the last step: descriptors cover every NAR exactly
     descs = d_out[: n_chunks * 48].cpu().numpy().view(ca.DESC_DTYPE)
-    for i in range(n_nars):
+    for i in range(len(mine)):
         a, b = int(first[i]), int(first[i + 1])
         assert b > a and descs["offset"][a] == 0
         assert int(descs["offset"][b - 1] + descs["length"][b - 1]) == nar_bytes
@@ -147,7 +179,7 @@ def main():
                         "traffic": None},
     }
     if algo == 1:
-        roofline["latency_floor"] = sha_chain_floor(descs, n_nars, total_bytes, params, dig_ms)
+        roofline["latency_floor"] = sha_chain_floor(descs, len(mine), total_bytes, params, dig_ms)
     dig_kernels = ["k_sha256"] if algo == 1 else ["k_b3_groups", "k_b3_top"]
     traffic, src = pmc_traffic(args.config, dig_kernels)
     if traffic is not None:
@@ -156,10 +188,17 @@ def main():
         roofline["traffic_source"] = src
 
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(host, offs, params, algo, args.cpu_sample_nars or n_nars)
+    conc = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, n_per, nar_bytes, params, algo)
+    if world == 1 and not args.no_concurrent:
+        del d_out, d_data
+        torch.cuda.empty_cache()
+        conc = concurrent_rates(ca, torch, args, n_per, nar_bytes, params, algo)
 
     if rank == 0:
+        gear = "placeholder" if ca.lib.cg_gear_is_placeholder() else (
+            "fastcdc-4.0.1 (selftest passed)" if ca.tables_verified() else "installed, unverified")
         line = {
             "metric": "device-resident GiB/s FastCDC+SHA-256 over synthetic NARs, 1/2/4/8 MI355X"
             if algo == 1 else "device-resident GiB/s FastCDC+BLAKE3 over synthetic NARs",
@@ -174,16 +213,68 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (xorshift64 NAR payloads)" if not args.zeros else "synthetic (all-zero NAR payloads)",
-            "config": {"workload": desc, "nars_per_gpu": n_nars, "nar_bytes": nar_bytes,
+            "config": {"workload": desc, "nars_per_gpu": len(mine), "nar_bytes": nar_bytes,
                        "params": list(params), "parallelism": f"nar-shard x{world}"},
+            "gear_table": gear,
             "chunks": n_chunks,
             "stages_ms": stages_ms,
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "concurrent": conc,
         }
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
+
+
+def concurrent_rates(ca, torch, args, n_per, nar_bytes, params, algo):
+    """K independent config batches in flight: K host threads, each with its own input
+    batch, output array and HIP stream, calling cg_chunk_batch_device `reps` times.
+    Aggregate GiB/s = K x reps x batch bytes / wall time (after one untimed round that
+    sizes every workspace).  The headline `value` stays the single-batch rate."""
+    from chunker_amd.nar import synth_nars_device
+
+    ks = sorted({int(k) for k in args.concurrent.split(",") if k})
+    kmax = max(ks)
+    sizes = np.full(n_per, nar_bytes, np.uint64)
+    jobs = []
+    for k in range(kmax):
+        d, offs = synth_nars_device(sizes, zeros=args.zeros, first_index=(k + 1) * 1000 * n_per)
+        cap = ca.chunking.batch_capacity(offs, params[0])
+        out = torch.empty(cap * 48, dtype=torch.uint8, device="cuda")
+        jobs.append((d, offs, out, cap, torch.cuda.Stream()))
+    torch.cuda.synchronize()
+    batch_bytes = int(jobs[0][1][-1])
+    res = {"unit": "GiB/s", "batch": f"{n_per}x{nar_bytes >> 20}MiB", "reps": 3,
+           "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default (4)")}
+    for K in ks:
+        for timed in (False, True):
+            reps = res["reps"] if timed else 1
+            bar = threading.Barrier(K + 1)
+            errs = []
+
+            def work(k):
+                d, offs, out, cap, s = jobs[k]
+                bar.wait()
+                try:
+                    for _ in range(reps):
+                        ca.chunk_batch_device(d.data_ptr(), offs, out.data_ptr(), cap, *params, hash=algo,
+                                              stream=s.cuda_stream)
+                except Exception as e:  # noqa: BLE001
+                    errs.append(repr(e))
+
+            th = [threading.Thread(target=work, args=(k,)) for k in range(K)]
+            for x in th:
+                x.start()
+            bar.wait()
+            t0 = time.perf_counter()
+            for x in th:
+                x.join()
+            dt = time.perf_counter() - t0
+            if errs:
+                raise RuntimeError(errs[0])
+        res[f"K{K}"] = round(K * reps * batch_bytes / dt / GIB, 3)
+    return res
 
 
 def sha_chain_floor(descs, n_nars, total_bytes, params, dig_ms):
@@ -221,25 +312,72 @@ def pmc_traffic(config, kernels):
     return (round(total), str(files[-1].relative_to(ROOT))) if hit else (None, None)
 
 
-def cpu_baseline(host, offs, params, algo, sample_nars):
-    """The oracle's restatement of chunk_data (one call per NAR: serial FastCDC scan,
-    then per-chunk digests on a thread pool, as rayon does), timed on this host."""
+def cpu_baseline(args, n_per, nar_bytes, params, algo):
+    """The oracle's restatement of the reference's CPU path, timed on this host:
+
+    * value: chunk_descriptors (src/chunking.rs:323-374) one call per NAR -- serial
+      FastCDC scan, then per-chunk digests on a pool of `cores` threads (rayon's role)
+      -- over the whole 1 GiB batch (c2/c3) or one 1 GiB NAR (c4/c5);
+    * nar_parallel: the CPU upper bound, NARs spread over the same pool, one
+      single-threaded chunk_descriptors per NAR;
+    * config1: BASELINE config 1 (benches/throughput.rs:39-43), chunk_data on 10 MiB
+      with payload copies (:265-296), D params, SHA-256, median of 7 runs, on zeros
+      (the published bench's data, 1.055 GiB/s in benchmarks/latest.md:12) and on
+      xorshift64 bytes."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from chunker_amd.nar import synth_nars
     from oracle import oracle as O
 
     nt = min(os.cpu_count() or 1, 16)
     O.lib()
-    nars = [host[int(offs[i]):int(offs[i + 1])] for i in range(min(sample_nars, len(offs) - 1))]
-    O.chunk_descriptors(nars[0], *params, algo=algo, nthreads=nt)  # warm
+    k = args.cpu_sample_nars or (n_per if nar_bytes <= (64 << 20) else 1)
+    host, offs = synth_nars(np.full(k, nar_bytes, np.uint64), zeros=args.zeros, first_index=0)
+    nars = [host[int(offs[i]):int(offs[i + 1])] for i in range(k)]
+    O.chunk_descriptors(nars[0][: 8 << 20], *params, algo=algo, nthreads=nt)  # warm
     t0 = time.perf_counter()
-    nbytes = 0
     for nar in nars:
         O.chunk_descriptors(nar, *params, algo=algo, nthreads=nt)
-        nbytes += len(nar)
     dt = time.perf_counter() - t0
+    nbytes = int(offs[-1])
+    with ThreadPoolExecutor(nt) as ex:
+        t1 = time.perf_counter()
+        list(ex.map(lambda a: O.chunk_descriptors(a, *params, algo=algo, nthreads=1), nars))
+        dt_par = time.perf_counter() - t1
+
+    def chunk_data(buf):  # chunk_data_with_hash: descriptors + an owned payload copy per chunk
+        return [(bytes(buf[int(d["offset"]):int(d["offset"] + d["length"])]), d)
+                for d in O.chunk_descriptors(buf, 256 << 10, 1 << 20, 4 << 20, algo=1, nthreads=nt)]
+
+    c1 = {}
+    ten = 10 * 1024 * 1024
+    for name, buf in (("zeros", np.zeros(ten, np.uint8)),
+                      ("random", synth_nars([ten], first_index=7)[0])):
+        chunk_data(buf)
+        ts = []
+        for _ in range(7):
+            t = time.perf_counter()
+            chunk_data(buf)
+            ts.append(time.perf_counter() - t)
+        c1[name] = round(ten / float(np.median(ts)) / GIB, 3)
+    c1["published_zeros"] = PUBLISHED_CHUNK_DATA_ZEROS
     return {"value": round(nbytes / dt / GIB, 4), "unit": "GiB/s", "cores": nt, "kind": "port",
-            "sample": f"{len(nars)} NARs ({nbytes / GIB:.3f} GiB) of the same batch, one chunk_descriptors call "
+            "sample": f"{k} NAR(s) ({nbytes / GIB:.3f} GiB) of the same workload, one chunk_descriptors call "
                       f"per NAR, SHA-NI={'yes' if O.lib().or_sha256_uses_shani() else 'no'}",
-            "seconds": round(dt, 3)}
+            "seconds": round(dt, 3),
+            "nar_parallel": round(nbytes / dt_par / GIB, 4),
+            "config1_chunk_data_10MiB_D_sha256": c1,
+            "cpu_model": cpu_model()}
+
+
+def cpu_model() -> str:
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 if __name__ == "__main__":

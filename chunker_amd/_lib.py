@@ -12,6 +12,13 @@ from pathlib import Path
 import numpy as np
 
 LIB_PATH = Path(__file__).resolve().parent / "libchunker_amd.so"
+# diagnostics build (make -C chunker_amd/csrc diag): same ABI plus cg_diag_* kernels
+DIAG_LIB_PATH = Path(__file__).resolve().parent / "libchunker_amd_diag.so"
+ABI_VERSION = 2
+
+# Opt-in that lifts the engine's fail-closed FastCDC table gate (include/chunker_gpu.h):
+# with the placeholder GEAR installed every chunking call refuses to run unless it is "1".
+ALLOW_PLACEHOLDER_ENV = "CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR"
 
 CG_OK = 0
 CG_E_BOUNDS = 1
@@ -21,6 +28,7 @@ CG_E_INVALID_OPTIONS = 4
 CG_E_BUFFER_LIMIT = 5
 CG_E_CAPACITY = 6
 CG_E_NO_DEVICE = 7
+CG_E_TABLES = 8
 
 # cg_desc (48 bytes): ChunkDescriptor {offset, length, hash[32]}
 DESC_DTYPE = np.dtype([("offset", "<u8"), ("length", "<u8"), ("hash", "u1", (32,))])
@@ -28,16 +36,18 @@ assert DESC_DTYPE.itemsize == 48
 
 # every exported symbol declared in include/chunker_gpu.h
 EXPORTS = (
-    "cg_abi_version", "cg_last_error_message", "cg_validate", "cg_capacity", "cg_chunk_descriptors",
-    "cg_chunk_batch", "cg_chunk_batch_device", "cg_push_new", "cg_push_push", "cg_push_finish",
-    "cg_push_bytes_consumed", "cg_push_out_capacity", "cg_push_free", "cg_hash_spans_device",
-    "cg_set_gear_table", "cg_get_gear_table", "cg_gear_is_placeholder", "cg_set_profiling",
-    "cg_last_stage_times", "cg_synth_nars", "cg_hash", "cg_cas_ids_device", "cg_cas_id",
-    "cg_node_put_batch_device", "cg_node_put",
+    "cg_abi_version", "cg_last_error_message", "cg_last_error_detail", "cg_validate", "cg_capacity",
+    "cg_chunk_descriptors", "cg_chunk_batch", "cg_chunk_batch_device", "cg_push_new", "cg_push_push",
+    "cg_push_finish", "cg_push_bytes_consumed", "cg_push_out_capacity", "cg_push_free", "cg_hash_spans_device",
+    "cg_set_cdc_tables", "cg_get_cdc_tables", "cg_set_gear_table", "cg_get_gear_table", "cg_gear_is_placeholder",
+    "cg_selftest", "cg_tables_verified", "cg_set_profiling", "cg_last_stage_times", "cg_synth_nars", "cg_hash",
+    "cg_cas_ids_device", "cg_cas_id", "cg_node_put_batch_device", "cg_node_put",
 )
+# test hooks the product library exports beyond the header (tier caps, spin-guard limit)
+TEST_HOOKS = ("cg_test_sha_quad_max", "cg_test_sha_split_max", "cg_test_sha_spin_limit", "cg_test_cas_pair_max")
 
 
-def _load() -> ctypes.CDLL:
+def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
     # PyTorch-ROCm ships its own libamdhip64 (SONAME libamdhip64.so.7) and links it as
     # "libamdhip64.so".  Loading torch first makes our DT_NEEDED libamdhip64.so.7
     # resolve to that same copy, so one process never holds two HIP runtimes.
@@ -45,15 +55,17 @@ def _load() -> ctypes.CDLL:
         import torch  # noqa: F401
     except ImportError:
         pass
-    if not LIB_PATH.exists():
+    if not path.exists():
         raise ImportError(
-            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(hipcc --offload-arch=gfx950). chunker_amd has no CPU fallback.")
-    L = ctypes.CDLL(str(LIB_PATH))
+    L = ctypes.CDLL(str(path))
     u64, sz, p, i = ctypes.c_uint64, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int
     psz = ctypes.POINTER(sz)
     L.cg_abi_version.restype = ctypes.c_uint32
     L.cg_last_error_message.restype = ctypes.c_char_p
+    L.cg_last_error_detail.argtypes = [p]
+    L.cg_last_error_detail.restype = i
     L.cg_validate.argtypes = [u64, u64, u64, ctypes.c_char_p, sz]
     L.cg_validate.restype = i
     L.cg_capacity.argtypes = [u64, u64]
@@ -88,11 +100,23 @@ def _load() -> ctypes.CDLL:
     L.cg_node_put_batch_device.restype = i
     L.cg_node_put.argtypes = [p, u64, u64, u64, u64, p, sz, psz, p, p]
     L.cg_node_put.restype = i
+    L.cg_set_cdc_tables.argtypes = [p, p]
+    L.cg_set_cdc_tables.restype = i
+    L.cg_get_cdc_tables.argtypes = [p, p]
+    L.cg_get_cdc_tables.restype = None
     L.cg_set_gear_table.argtypes = [p]
     L.cg_set_gear_table.restype = i
     L.cg_get_gear_table.argtypes = [p]
     L.cg_get_gear_table.restype = None
     L.cg_gear_is_placeholder.restype = i
+    L.cg_selftest.restype = i
+    L.cg_tables_verified.restype = i
+    u32 = ctypes.c_uint32
+    for name in ("cg_test_sha_quad_max", "cg_test_sha_split_max", "cg_test_sha_spin_limit"):
+        getattr(L, name).argtypes = [u32]
+        getattr(L, name).restype = u32
+    L.cg_test_cas_pair_max.argtypes = [ctypes.c_int64]
+    L.cg_test_cas_pair_max.restype = ctypes.c_int64
     L.cg_set_profiling.argtypes = [i]
     L.cg_set_profiling.restype = None
     L.cg_last_stage_times.argtypes = [p, sz]
@@ -102,10 +126,33 @@ def _load() -> ctypes.CDLL:
     return L
 
 
-lib = _load()
-assert lib.cg_abi_version() == 1
+# CHUNKER_AMD_DIAG=1 (scripts/diag_*.py only) loads the diagnostics build in its place
+lib = _load(DIAG_LIB_PATH if __import__("os").environ.get("CHUNKER_AMD_DIAG") == "1" else LIB_PATH)
+assert lib.cg_abi_version() == ABI_VERSION
+
+_diag = None
+
+
+def diag_lib() -> ctypes.CDLL:
+    """The diagnostics build (scripts/diag_*.py): built on demand, never used by the
+    product path."""
+    global _diag
+    if _diag is None:
+        if not DIAG_LIB_PATH.exists():
+            import subprocess
+            subprocess.run(["make", "-s", "-C", str(Path(__file__).resolve().parent / "csrc"), "diag"], check=True)
+        _diag = _load(DIAG_LIB_PATH)
+    return _diag
 
 
 def last_error() -> str:
     msg = lib.cg_last_error_message()
     return msg.decode() if msg else ""
+
+
+def last_error_detail() -> tuple[int, int, int, int]:
+    """(status, a, b, c) of this thread's last failure: Bounds -> (data_len, offset,
+    length), BufferLimitExceeded -> (attempted, limit, 0)."""
+    out = (ctypes.c_uint64 * 3)()
+    st = lib.cg_last_error_detail(out)
+    return st, int(out[0]), int(out[1]), int(out[2])

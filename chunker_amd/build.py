@@ -11,7 +11,8 @@ CSRC = Path(__file__).resolve().parent / "csrc"
 def build(jobs: int = 8) -> Path:
     env = dict(os.environ)
     env.setdefault("ARCH", "gfx950")
-    subprocess.run(["make", "-s", "-C", str(CSRC), f"-j{jobs}"], check=True, env=env)
+    # the product library and the diagnostics build (scripts/diag_*.py, the DPP probe test)
+    subprocess.run(["make", "-s", "-C", str(CSRC), f"-j{jobs}", "all", "diag"], check=True, env=env)
     return CSRC.parent / "libchunker_amd.so"
 
 

@@ -41,7 +41,7 @@ class ContentId:
         """ContentId::compute (:59-69) on the GPU (cg_cas_id)."""
         a = _as_u8(payload)
         out = (ctypes.c_uint8 * 32)()
-        _check(lib.cg_cas_id(_ptr(a), len(a), int(ObjectKind(kind)), out), len(a))
+        _check(lib.cg_cas_id(_ptr(a), len(a), int(ObjectKind(kind)), out))
         return cls(bytes(out))
 
     @classmethod
@@ -85,7 +85,7 @@ def node_put(data, min_size=None, avg_size=None, max_size=None) -> PutResult:
     man = (ctypes.c_uint8 * 32)()
     n = ctypes.c_size_t(0)
     _check(lib.cg_node_put(_ptr(a), len(a), o.min_size, o.avg_size, o.max_size, out.ctypes.data, cap,
-                           ctypes.byref(n), ids.ctypes.data, man), len(a))
+                           ctypes.byref(n), ids.ctypes.data, man))
     descs = descriptors_to_list(out[:n.value])
     raw = bytes(a)
     chunks = [ChunkMetadata(d.hash, d.offset, d.length, raw[d.offset:d.offset + d.length]) for d in descs]

@@ -88,24 +88,66 @@ class DeviceUnavailableError(IoError):
     """No gfx950 device: the engine has no CPU fallback (ABI status CG_E_NO_DEVICE)."""
 
 
-def _raise(status: int, data_len: int = 0) -> None:
+class TablesError(IoError):
+    """FastCDC tables refused (ABI status CG_E_TABLES): the placeholder GEAR is installed
+    or the installed set failed the reference-fixture selftest (include/chunker_gpu.h)."""
+
+
+def _raise(status: int) -> None:
+    """Rebuild the reference's ChunkingError variant from the ABI status and the
+    failure's fields (cg_last_error_detail), as the Rust shim does."""
     msg = _lib.last_error()
+    _, a, b, c = _lib.last_error_detail()
     if status == _lib.CG_E_INVALID_OPTIONS:
         raise InvalidOptionsError(msg)
     if status == _lib.CG_E_BOUNDS:
-        raise BoundsError(data_len, 0, 0)
+        raise BoundsError(a, b, c)
     if status == _lib.CG_E_ZERO_LENGTH_CHUNK:
         raise ZeroLengthChunkError()
     if status == _lib.CG_E_BUFFER_LIMIT:
-        raise BufferLimitExceededError(0, 0)
+        raise BufferLimitExceededError(a, b)
     if status == _lib.CG_E_NO_DEVICE:
         raise DeviceUnavailableError(msg)
+    if status == _lib.CG_E_TABLES:
+        raise TablesError(msg)
     raise IoError(msg or f"engine status {status}")
 
 
-def _check(status: int, data_len: int = 0) -> None:
+def _check(status: int) -> None:
     if status != _lib.CG_OK:
-        _raise(status, data_len)
+        _raise(status)
+
+
+# ---------------------------------------------------------------------------
+# FastCDC tables (fastcdc 4.0.1 v2020 GEAR / MASKS): install, inspect, verify
+# ---------------------------------------------------------------------------
+def set_cdc_tables(gear, masks=None) -> None:
+    """Install GEAR[256] (and MASKS[26], or keep the current ones) process-wide.  The
+    engine runs the new set only after it reproduces the reference fixture
+    (src/chunking.rs:1266-1297) on the GPU -- see selftest()."""
+    g = np.ascontiguousarray(gear, dtype=np.uint64)
+    if g.shape != (256,):
+        raise InvalidOptionsError("GEAR must have 256 entries")
+    m = None if masks is None else np.ascontiguousarray(masks, dtype=np.uint64)
+    if m is not None and m.shape != (26,):
+        raise InvalidOptionsError("MASKS must have 26 entries")
+    _check(lib.cg_set_cdc_tables(g.ctypes.data, None if m is None else m.ctypes.data))
+
+
+def get_cdc_tables() -> tuple[np.ndarray, np.ndarray]:
+    g, m = np.zeros(256, np.uint64), np.zeros(26, np.uint64)
+    lib.cg_get_cdc_tables(g.ctypes.data, m.ctypes.data)
+    return g, m
+
+
+def selftest() -> None:
+    """Run the reference's golden boundary fixture through the GPU pipeline with the
+    installed tables; raises TablesError (with the boundaries found) on a mismatch."""
+    _check(lib.cg_selftest())
+
+
+def tables_verified() -> bool:
+    return bool(lib.cg_tables_verified())
 
 
 # ---------------------------------------------------------------------------
@@ -208,7 +250,7 @@ def chunk_descriptors_array(data, min_size=None, avg_size=None, max_size=None,
     out = np.zeros(cap, DESC_DTYPE)
     n = ctypes.c_size_t(0)
     _check(lib.cg_chunk_descriptors(_ptr(a), len(a), o.min_size, o.avg_size, o.max_size, int(hash),
-                                    out.ctypes.data, cap, ctypes.byref(n)), len(a))
+                                    out.ctypes.data, cap, ctypes.byref(n)))
     return out[: n.value]
 
 
@@ -257,7 +299,7 @@ def chunk_batch(nars: Sequence, min_size=None, avg_size=None, max_size=None,
     out = np.zeros(cap, DESC_DTYPE)
     first = np.zeros(len(arrs) + 1, np.uint64)
     _check(lib.cg_chunk_batch(_ptr(flat), offs.ctypes.data, len(arrs), o.min_size, o.avg_size, o.max_size,
-                              int(hash), out.ctypes.data, cap, first.ctypes.data), len(flat))
+                              int(hash), out.ctypes.data, cap, first.ctypes.data))
     return [out[int(first[i]):int(first[i + 1])] for i in range(len(arrs))]
 
 
@@ -274,7 +316,7 @@ def chunk_batch_flat(flat, nar_offsets, min_size=None, avg_size=None, max_size=N
         out = np.zeros(cap, DESC_DTYPE)
     first = np.zeros(n + 1, np.uint64)
     _check(lib.cg_chunk_batch(_ptr(a), offs.ctypes.data, n, o.min_size, o.avg_size, o.max_size, int(hash),
-                              out.ctypes.data, len(out), first.ctypes.data), len(a))
+                              out.ctypes.data, len(out), first.ctypes.data))
     return out[: int(first[-1])], first
 
 
@@ -443,7 +485,9 @@ class ChunkStream:
             try:
                 buf = self._next.result()
             except OSError as e:
-                self._close_pool()
+                # the failed read is consumed: a later next() reads again (as the
+                # reference's ChunkStream::next does after an Io error)
+                self._next = None
                 raise IoError(str(e)) from e
             if not buf:
                 self._next = None

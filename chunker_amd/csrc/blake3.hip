@@ -324,7 +324,9 @@ __global__ __launch_bounds__(64) void k_b3_top(const DescRaw *__restrict__ desc,
     if (lane == 0) store_digest(hash_base + c * stride, cv);
 }
 
-uint32_t g_b3_diag = 0;  // set by cg_diag_b3_mode (diagnostics only; 0 = product)
+#ifdef CG_DIAG
+uint32_t g_b3_diag = 0;  // set by cg_diag_b3_mode (diagnostics build only)
+#endif
 
 size_t blake3_group_bound(uint64_t total_bytes, uint64_t max_chunks) { return total_bytes / 65536 + max_chunks + 1; }
 
@@ -339,7 +341,12 @@ void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
     launch_exclusive_scan_u32(d_gcount_u32, d_group_base, max_chunks, 0, d_scan_tmp, st);
     hipLaunchKernelGGL(k_b3_map, dim3(cblocks), dim3(256), 0, st, d_group_base, d_total, max_chunks, d_gmap);
     const uint64_t gbound = blake3_group_bound(total_bytes, max_chunks);
-    hipLaunchKernelGGL(g_b3_diag ? k_b3_groups<true> : k_b3_groups<false>,
+#ifdef CG_DIAG
+    auto groups = g_b3_diag ? k_b3_groups<true> : k_b3_groups<false>;
+#else
+    auto groups = k_b3_groups<false>;
+#endif
+    hipLaunchKernelGGL(groups,
                        dim3((uint32_t)((gbound + B3_WAVES - 1) / B3_WAVES)), dim3(64 * B3_WAVES), 0, st, d_data, d_abs, desc, d_total, max_chunks, d_group_base, d_gmap, d_hash_base, hash_stride,
                        d_gcv);
     hipLaunchKernelGGL(k_b3_top, dim3((uint32_t)max_chunks), dim3(64), 0, st, desc, d_total, max_chunks,

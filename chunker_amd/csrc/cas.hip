@@ -332,9 +332,9 @@ void launch_manifest_spans(const uint64_t *d_first, uint64_t n_nars, uint64_t *d
 
 }  // namespace cg
 
-// Diagnostics / tests: cap the pair tier (-1 = budget only, 0 = one lane per span
-// everywhere); returns the previous cap.
-extern "C" int64_t cg_diag_cas_pair_max(int64_t v) {
+// Test hook: cap the pair tier (-1 = budget only, 0 = one lane per span everywhere) so
+// the parity tests can force every tier mix; returns the previous cap.
+extern "C" int64_t cg_test_cas_pair_max(int64_t v) {
     const int64_t old = cg::g_cas_pair_max;
     cg::g_cas_pair_max = v;
     return old;

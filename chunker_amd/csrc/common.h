@@ -54,10 +54,11 @@ void launch_assemble(const uint64_t *d_nar_off, const uint64_t *d_cap_base, cons
 
 // d_order_tmp (sha256_order_tmp_elems(max_chunks) u32, or nullptr = identity order) holds
 // the longest-first lane order; max_len bounds every chunk length (bucket width);
-// `expected` estimates the chunk count (sizes the workgroup tiers).
+// `expected` estimates the chunk count (sizes the workgroup tiers).  d_err (one u32, zeroed
+// by the caller) becomes nonzero if a producer/consumer hand-off hit its spin guard.
 void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
                    uint64_t max_chunks, uint64_t expected, uint64_t max_len, uint32_t *d_order_tmp,
-                   uint8_t *d_hash_base, size_t hash_stride, hipStream_t st);
+                   uint8_t *d_hash_base, size_t hash_stride, uint32_t *d_err, hipStream_t st);
 size_t sha256_order_tmp_elems(uint64_t max_chunks);
 
 // Longest-first order of the first min(*d_total, max_chunks) descriptors (counting sort

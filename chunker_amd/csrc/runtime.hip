@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -31,26 +32,90 @@ constexpr uint64_t MINIMUM_MIN = 64, MINIMUM_MAX = 1048576, AVERAGE_MIN = 256, A
                    MAXIMUM_MIN = 1024, MAXIMUM_MAX = 16777216;
 
 thread_local std::string t_err;
+thread_local uint64_t t_detail[3];  // ChunkingError fields of the last failure (cg_last_error_detail)
+thread_local int t_status = CG_OK;
 thread_local std::vector<double> t_stage_ms;
 std::atomic<int> g_profiling{0};
 
-std::mutex g_gear_mu;
-uint64_t g_gear[256];
-bool g_gear_init = false;
-std::atomic<uint64_t> g_gear_epoch{1};
-std::atomic<int> g_gear_placeholder{CG_GEAR_IS_PLACEHOLDER};
-
 int fail(int code, const std::string &msg) {
     t_err = msg;
+    t_status = code;
+    t_detail[0] = t_detail[1] = t_detail[2] = 0;
     return code;
 }
 
-int hip_fail(hipError_t e, const char *what) {
-    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation)
-        return fail(CG_E_BUFFER_LIMIT, std::string("device allocation failed: ") + what);
+void clear_error() {
+    t_err.clear();
+    t_status = CG_OK;
+    t_detail[0] = t_detail[1] = t_detail[2] = 0;
+}
+
+// ChunkingError::Bounds { data_len, offset, length } (src/chunking.rs:38-42)
+int fail_bounds(uint64_t data_len, uint64_t offset, uint64_t length, const std::string &what) {
+    fail(CG_E_BOUNDS, what);
+    t_detail[0] = data_len;
+    t_detail[1] = offset;
+    t_detail[2] = length;
+    return CG_E_BOUNDS;
+}
+
+// ChunkingError::BufferLimitExceeded { attempted, limit } (src/chunking.rs:49-50): a device
+// allocation of `attempted` bytes failed with `limit` bytes of device memory free.
+int fail_limit(uint64_t attempted, const std::string &what) {
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) free_b = 0;
+    fail(CG_E_BUFFER_LIMIT, what);
+    t_detail[0] = attempted;
+    t_detail[1] = free_b;
+    return CG_E_BUFFER_LIMIT;
+}
+
+int hip_fail(hipError_t e, const char *what, uint64_t attempted = 0) {
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) {
+        (void)hipGetLastError();  // clear the sticky allocation error
+        return fail_limit(attempted, std::string("device allocation failed: ") + what);
+    }
     if (e == hipErrorNoDevice || e == hipErrorNoBinaryForGpu || e == hipErrorInvalidDevice)
         return fail(CG_E_NO_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
     return fail(CG_E_IO, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// ---------------------------------------------------------------------------
+// FastCDC v2020 tables [ext fastcdc 4.0.1]: GEAR[256] and MASKS[26].  The compiled-in
+// set comes from tables/*.txt; cg_set_cdc_tables installs another one process-wide.
+// Fail closed: a chunking call refuses to run while the placeholder GEAR is installed,
+// and any other table set must first reproduce the reference's golden fixture
+// (src/chunking.rs:1266-1297) on the GPU (cg_selftest, run lazily on first use), unless
+// CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR=1 -- the test / bench opt-in -- is set.
+// ---------------------------------------------------------------------------
+struct Tables {
+    uint64_t gear[256];
+    uint64_t masks[26];
+    uint64_t epoch;
+    bool placeholder;
+};
+
+std::mutex g_tab_mu;
+std::shared_ptr<const Tables> g_tab;
+std::atomic<uint64_t> g_tab_epoch{1};
+std::atomic<uint64_t> g_verified_epoch{0};  // epoch whose tables passed the selftest
+
+std::shared_ptr<const Tables> tables() {
+    std::lock_guard<std::mutex> g(g_tab_mu);
+    if (!g_tab) {
+        auto t = std::make_shared<Tables>();
+        memcpy(t->gear, CG_DEFAULT_GEAR, sizeof t->gear);
+        memcpy(t->masks, CG_MASKS, sizeof t->masks);
+        t->epoch = g_tab_epoch.load();
+        t->placeholder = CG_GEAR_IS_PLACEHOLDER != 0;
+        g_tab = t;
+    }
+    return g_tab;
+}
+
+bool allow_unverified_tables() {
+    const char *v = getenv("CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR");
+    return v && v[0] == '1' && v[1] == 0;
 }
 
 #define HIP_TRY(expr)                                   \
@@ -58,15 +123,6 @@ int hip_fail(hipError_t e, const char *what) {
         hipError_t _e = (expr);                         \
         if (_e != hipSuccess) return hip_fail(_e, #expr); \
     } while (0)
-
-void gear_snapshot(uint64_t out[256]) {
-    std::lock_guard<std::mutex> g(g_gear_mu);
-    if (!g_gear_init) {
-        memcpy(g_gear, CG_DEFAULT_GEAR, sizeof g_gear);
-        g_gear_init = true;
-    }
-    memcpy(out, g_gear, sizeof g_gear);
-}
 
 uint32_t logarithm2(uint32_t v) { return (uint32_t)std::round(std::log2((double)v)); }
 
@@ -82,7 +138,7 @@ struct DevBuf {
         hipError_t e = hipMalloc(&p, want);
         if (e != hipSuccess) {
             p = nullptr;
-            return hip_fail(e, name);
+            return hip_fail(e, name, want);
         }
         cap = want;
         return CG_OK;
@@ -108,7 +164,7 @@ struct PinBuf {
         hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
         if (e != hipSuccess) {
             p = nullptr;
-            return hip_fail(e, "hipHostMalloc");
+            return hip_fail(e, "hipHostMalloc", want);
         }
         cap = want;
         return CG_OK;
@@ -125,8 +181,8 @@ struct Workspace {
     uint64_t gear_epoch = 0;
     DevBuf gear, seg_count, seg_cand, eoff, scan_tmp, entries, nar_off, cap_base, wchunk, nar_nchunks, nar_first,
         chunk_abs, b3_gcount, b3_gbase, b3_gcv, b3_gmap, in, out, span_off, span_len, order, cas_order, ids,
-        man_abs, man_desc;
-    PinBuf stage;
+        man_abs, man_desc, sha_err;
+    PinBuf stage, err_stage;
     hipEvent_t ev[EV_N] = {};
     // CAS ids run on side_stream, concurrently with the digest: both stages are bound by
     // their longest chunk's serial chain, not by the chip, so they overlap for free.
@@ -196,21 +252,40 @@ struct WsGuard {
     }
 };
 
-int ensure_gear(Workspace *ws) {
-    const uint64_t epoch = g_gear_epoch.load();
-    if (ws->gear_epoch == epoch && ws->gear.p) return CG_OK;
+// Upload the snapshot's GEAR table to this workspace (once per table epoch).
+int ensure_gear(Workspace *ws, const Tables &t) {
+    if (ws->gear_epoch == t.epoch && ws->gear.p) return CG_OK;
     int st = ws->gear.ensure(256 * sizeof(uint64_t), "gear");
     if (st) return st;
-    uint64_t g[256];
-    gear_snapshot(g);
-    HIP_TRY(hipMemcpy(ws->gear.p, g, sizeof g, hipMemcpyHostToDevice));
-    ws->gear_epoch = epoch;
+    HIP_TRY(hipMemcpy(ws->gear.p, t.gear, sizeof t.gear, hipMemcpyHostToDevice));
+    ws->gear_epoch = t.epoch;
     return CG_OK;
 }
 
 struct Opts {
     uint64_t min, avg, max;
 };
+
+// The SHA-256 kernel's spin-guard word (launch_sha256 d_err): zeroed before a digest
+// launch, copied back with the call's other results, checked after the stream sync.
+int sha_err_arm(Workspace *ws, hipStream_t st) {
+    int rc;
+    if ((rc = ws->sha_err.ensure(64, "sha err"))) return rc;
+    if ((rc = ws->err_stage.ensure(64))) return rc;
+    ws->err_stage.as<uint32_t>()[0] = 0;
+    HIP_TRY(hipMemsetAsync(ws->sha_err.p, 0, 4, st));
+    return CG_OK;
+}
+int sha_err_fetch(Workspace *ws, hipStream_t st) {
+    HIP_TRY(hipMemcpyAsync(ws->err_stage.p, ws->sha_err.p, 4, hipMemcpyDeviceToHost, st));
+    return CG_OK;
+}
+int sha_err_check(Workspace *ws) {  // after the stream sync
+    if (ws->err_stage.p && ws->err_stage.as<uint32_t>()[0])
+        return fail(CG_E_IO, "SHA-256 digest: a producer/consumer hand-off hit the kernel's spin guard; "
+                             "the digests of this call are invalid");
+    return CG_OK;
+}
 
 int resolve(uint64_t mn, uint64_t avg, uint64_t mx, Opts *o, char *msg, size_t cap) {
     o->min = mn ? mn : DEF_MIN;
@@ -277,17 +352,20 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
     int rc;
     const uint64_t base0 = n_nars ? h_nar_off[0] : 0;
     const uint64_t total_len = n_nars ? h_nar_off[n_nars] : 0;
-    for (size_t i = 0; i < n_nars; ++i)
-        if (h_nar_off[i + 1] < h_nar_off[i]) return fail(CG_E_BOUNDS, "nar offsets must be non-decreasing");
+    for (size_t i = 0; i < n_nars; ++i)  // NAR i = [off[i], off[i+1]) must lie inside the batch
+        if (h_nar_off[i + 1] < h_nar_off[i])
+            return fail_bounds(h_nar_off[i + 1], h_nar_off[i], 0, "nar offsets must be non-decreasing");
     (void)base0;
 
+    // one table snapshot for the whole call: GEAR on the device and MASKS in P agree
+    const std::shared_ptr<const Tables> tab = tables();
     CdcParams P;
     const uint32_t bits = logarithm2((uint32_t)o.avg);
     P.min = o.min;
     P.avg = o.avg;
     P.max = o.max;
-    P.mask_s = CG_MASKS[bits + 1];
-    P.mask_l = CG_MASKS[bits - 1];
+    P.mask_s = tab->masks[bits + 1];
+    P.mask_l = tab->masks[bits - 1];
 
     // host staging: nar_off (n+1), cap_base (n+1), nar_first (n+1)
     if ((rc = ws->stage.ensure(3 * (n_nars + 1) * sizeof(uint64_t)))) return rc;
@@ -305,7 +383,7 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
     const uint64_t nseg = (total_len + CG_SEG - 1) / CG_SEG;
     const uint32_t slots = seg_slots(P);
     const uint64_t chunk_bound = std::min<uint64_t>(total_cap, out_cap);
-    if ((rc = ensure_gear(ws))) return rc;
+    if ((rc = ensure_gear(ws, *tab))) return rc;
     if ((rc = ws->seg_count.ensure((nseg + 1) * 4, "seg_count"))) return rc;
     if ((rc = ws->seg_cand.ensure((nseg * slots + 1) * 4, "seg_cand"))) return rc;
     if ((rc = ws->eoff.ensure((nseg + 1) * 8, "eoff"))) return rc;
@@ -370,14 +448,17 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
         HIP_TRY(hipEventRecord(ws->ev_join, side));
     }
     uint8_t *hash_base = reinterpret_cast<uint8_t *>(d_out) + offsetof(cg_desc, hash);
+    bool sha_armed = false;
     if (!digest) {
         // boundaries only (push_drain digests the chunks that became final afterwards)
     } else if (algo == CG_SHA256) {
         if ((rc = ws->order.ensure(cg::sha256_order_tmp_elems(chunk_bound) * 4, "order"))) return rc;
         // expected chunk count: FastCDC's mean chunk is about min + avg on random data
         const uint64_t expected = std::min<uint64_t>(chunk_bound, total_len / (o.min + o.avg) + n_nars);
+        if ((rc = sha_err_arm(ws, st))) return rc;
+        sha_armed = true;
         cg::launch_sha256(d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, expected, o.max,
-                          ws->order.as<uint32_t>(), hash_base, sizeof(cg_desc), st);
+                          ws->order.as<uint32_t>(), hash_base, sizeof(cg_desc), ws->sha_err.as<uint32_t>(), st);
     } else {
         cg::launch_blake3(d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, total_len, hash_base,
                           sizeof(cg_desc), ws->b3_gmap.as<uint32_t>(), ws->b3_gbase.as<uint64_t>(),
@@ -389,7 +470,9 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
     HIP_TRY(hipMemcpyAsync(s_first, ws->nar_first.p, (n_nars + 1) * 8, hipMemcpyDeviceToHost, st));
     if (d_man && h_manifest_ids)
         HIP_TRY(hipMemcpyAsync(h_manifest_ids, d_man, n_nars * 32, hipMemcpyDeviceToHost, st));
+    if (sha_armed && (rc = sha_err_fetch(ws, st))) return rc;
     HIP_TRY(hipStreamSynchronize(st));
+    if (sha_armed && (rc = sha_err_check(ws))) return rc;
     if (prof) {
         t_stage_ms.assign(EV_N - 1 + (d_chunk_ids ? 1 : 0), 0.0);
         for (int k = 1; k < EV_N; ++k) {
@@ -408,11 +491,89 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
     return CG_OK;
 }
 
+// The reference's golden boundary fixture, fastcdc_boundaries_match_v3_golden_fixture
+// (src/chunking.rs:1266-1297): b[i] = (i*31 + i/7) % 251 for 65,659 bytes, chunked at
+// (1024, 6000, 16384) -- bits = 13, so it exercises MASKS[14] / MASKS[12] and GEAR[0..250].
+constexpr uint64_t FIX_LEN = 64 * 1024 + 123;
+constexpr uint64_t FIX_CUTS[10][2] = {{0, 6162},     {6162, 7028},  {13190, 7028}, {20218, 7028}, {27246, 7028},
+                                      {34274, 7028}, {41302, 7028}, {48330, 7028}, {55358, 7028}, {62386, 3273}};
+
+// Run the fixture through the GPU pipeline (scan, walk, assembly) with the installed
+// tables and compare with the reference's ten boundaries.  On a match the table epoch
+// the pipeline used is marked verified.
+int selftest_gpu() {
+    Workspace *ws = nullptr;
+    int rc = acquire(&ws);
+    if (rc) return rc;
+    WsGuard guard{ws};
+    Opts o{1024, 6000, 16384};
+    std::vector<uint8_t> fx(FIX_LEN);
+    for (uint64_t i = 0; i < FIX_LEN; ++i) fx[i] = (uint8_t)((i * 31 + i / 7) % 251);
+    const uint64_t cap = capacity_of(FIX_LEN, o.min);
+    if ((rc = ws->in.ensure(FIX_LEN + 256, "input"))) return rc;
+    if ((rc = ws->out.ensure((cap + 1) * sizeof(cg_desc), "descriptors"))) return rc;
+    HIP_TRY(hipMemcpyAsync(ws->in.p, fx.data(), FIX_LEN, hipMemcpyHostToDevice, ws->stream));
+    uint64_t offs[2] = {0, FIX_LEN}, first[2] = {0, 0};
+    if ((rc = run_batch(ws, ws->in.as<uint8_t>(), offs, 1, o, CG_SHA256, ws->out.as<cg_desc>(), cap, first,
+                        ws->stream, nullptr, nullptr, /*digest=*/false)))
+        return rc;
+    const uint64_t used_epoch = ws->gear_epoch;
+    std::vector<cg_desc> got(first[1]);
+    if (first[1]) {
+        HIP_TRY(hipMemcpyAsync(got.data(), ws->out.p, first[1] * sizeof(cg_desc), hipMemcpyDeviceToHost, ws->stream));
+        HIP_TRY(hipStreamSynchronize(ws->stream));
+    }
+    bool ok = got.size() == 10;
+    for (size_t k = 0; ok && k < 10; ++k) ok = got[k].offset == FIX_CUTS[k][0] && got[k].length == FIX_CUTS[k][1];
+    if (ok) {
+        g_verified_epoch.store(used_epoch);
+        return CG_OK;
+    }
+    std::string msg = "FastCDC selftest failed: the reference fixture (src/chunking.rs:1266-1297) gave " +
+                      std::to_string(got.size()) + " chunks [";
+    for (size_t k = 0; k < got.size() && k < 4; ++k)
+        msg += (k ? ", (" : "(") + std::to_string(got[k].offset) + "," + std::to_string(got[k].length) + ")";
+    msg += got.size() > 4 ? ", ...]" : "]";
+    msg += " where fastcdc gives 10 [(0,6162), (6162,7028), ...]";
+    if (tables()->placeholder) msg += "; the installed GEAR table is the build's placeholder, not fastcdc 4.0.1's";
+    return fail(CG_E_TABLES, msg);
+}
+
+// Fail-closed gate in front of every chunking entry point (see Tables above).
+int check_tables() {
+    if (allow_unverified_tables()) return CG_OK;
+    const std::shared_ptr<const Tables> t = tables();
+    if (t->placeholder)
+        return fail(CG_E_TABLES,
+                    "FastCDC GEAR table is the build's placeholder (tables/fastcdc_v2020_gear.txt), not fastcdc "
+                    "4.0.1's: chunk boundaries would differ from the reference. Install the crate's GEAR/MASKS with "
+                    "cg_set_cdc_tables(), or set CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR=1 to run anyway");
+    if (g_verified_epoch.load() == t->epoch) return CG_OK;
+    return selftest_gpu();
+}
+
+// The reference's own checks on the descriptor list before it is handed out:
+// ZeroLengthChunk (src/chunking.rs:567-570) and the bounds check of every
+// (offset, length) against the input (:346-356); a GPU list that fails them is an
+// engine fault and surfaces as the same errors, never as silently bad chunks.
+int check_descriptors(const cg_desc *out, const uint64_t *first, const uint64_t *off, size_t n_nars) {
+    for (size_t i = 0; i < n_nars; ++i) {
+        const uint64_t len = off[i + 1] - off[i];
+        for (uint64_t g = first[i]; g < first[i + 1]; ++g) {
+            if (out[g].length == 0) return fail(CG_E_ZERO_LENGTH_CHUNK, "FastCDC returned a chunk with length 0");
+            if (out[g].offset > len || out[g].length > len - out[g].offset)
+                return fail_bounds(len, out[g].offset, out[g].length, "descriptor outside its input");
+        }
+    }
+    return CG_OK;
+}
+
 int batch_host(const uint8_t *data, const uint64_t *nar_offsets, size_t n_nars, uint64_t mn, uint64_t avg,
                uint64_t mx, int algo, cg_desc *out, size_t out_cap, uint64_t *nar_first) {
     Opts o;
     int rc = resolve(mn, avg, mx, &o, nullptr, 0);
     if (rc) return rc;
+    if ((rc = check_tables())) return rc;
     Workspace *ws = nullptr;
     if ((rc = acquire(&ws))) return rc;
     WsGuard guard{ws};
@@ -437,7 +598,7 @@ int batch_host(const uint8_t *data, const uint64_t *nar_offsets, size_t n_nars, 
         HIP_TRY(hipMemcpyAsync(out, ws->out.p, total * sizeof(cg_desc), hipMemcpyDeviceToHost, ws->stream));
         HIP_TRY(hipStreamSynchronize(ws->stream));
     }
-    return CG_OK;
+    return check_descriptors(out, first.data(), off.data(), n_nars);
 }
 
 // Digest-only pipeline over n device spans on `st` (shared by cg_hash_spans_device and cg_hash).
@@ -451,11 +612,14 @@ int hash_spans(Workspace *ws, const uint8_t *d_data, const uint64_t *d_offsets, 
     uint64_t *d_total = ws->nar_first.as<uint64_t>();
     cg::launch_spans_to_desc(d_offsets, d_lengths, n, ws->chunk_abs.as<uint64_t>(), ws->out.p, d_total, st);
     uint8_t *hb = ws->out.as<uint8_t>() + offsetof(cg_desc, hash);
+    bool sha_armed = false;
     if (algo == CG_SHA256) {
         // spans are not bounded by a max_size: bucket for the ABI's 16 MiB span cap
         if ((rc = ws->order.ensure(cg::sha256_order_tmp_elems(n) * 4, "order"))) return rc;
+        if ((rc = sha_err_arm(ws, st))) return rc;
+        sha_armed = true;
         cg::launch_sha256(d_data, ws->chunk_abs.as<uint64_t>(), ws->out.p, d_total, n, n, MAXIMUM_MAX,
-                          ws->order.as<uint32_t>(), hb, sizeof(cg_desc), st);
+                          ws->order.as<uint32_t>(), hb, sizeof(cg_desc), ws->sha_err.as<uint32_t>(), st);
     } else {
         // group-grid bound without reading lengths back: spans are capped at 16 MiB each
         const uint64_t tb = (uint64_t)n * MAXIMUM_MAX;
@@ -470,7 +634,9 @@ int hash_spans(Workspace *ws, const uint8_t *d_data, const uint64_t *d_offsets, 
     }
     HIP_TRY(hipMemcpy2DAsync(d_digests, 32, hb, sizeof(cg_desc), 32, n, hipMemcpyDeviceToDevice, st));
     HIP_TRY(hipGetLastError());
+    if (sha_armed && (rc = sha_err_fetch(ws, st))) return rc;
     HIP_TRY(hipStreamSynchronize(st));
+    if (sha_armed && (rc = sha_err_check(ws))) return rc;
     return CG_OK;
 }
 
@@ -578,10 +744,13 @@ int push_drain(cg_push *h, bool eof, cg_desc *out, size_t out_cap, size_t *n_out
         ws->stage.as<uint64_t>()[0] = n;
         HIP_TRY(hipMemcpyAsync(d_total, ws->stage.p, 8, hipMemcpyHostToDevice, st));
         uint8_t *hb = reinterpret_cast<uint8_t *>(d_out) + offsetof(cg_desc, hash);
+        bool sha_armed = false;
         if (h->algo == CG_SHA256) {
             if ((rc = ws->order.ensure(cg::sha256_order_tmp_elems(n) * 4, "order"))) return rc;
+            if ((rc = sha_err_arm(ws, st))) return rc;
+            sha_armed = true;
             cg::launch_sha256(d_in, ws->chunk_abs.as<uint64_t>(), d_out, d_total, n, n, h->o.max,
-                              ws->order.as<uint32_t>(), hb, sizeof(cg_desc), st);
+                              ws->order.as<uint32_t>(), hb, sizeof(cg_desc), ws->sha_err.as<uint32_t>(), st);
         } else {
             const uint64_t gb = cg::blake3_group_bound(len, n);
             if ((rc = ws->b3_gcount.ensure((n + 1) * 4, "b3_gcount"))) return rc;
@@ -595,13 +764,15 @@ int push_drain(cg_push *h, bool eof, cg_desc *out, size_t out_cap, size_t *n_out
         }
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(out, d_out, n * sizeof(cg_desc), hipMemcpyDeviceToHost, st));
+        if (sha_armed && (rc = sha_err_fetch(ws, st))) return rc;
         HIP_TRY(hipStreamSynchronize(st));
+        if (sha_armed && (rc = sha_err_check(ws))) return rc;
         for (size_t k = 0; k < n; ++k) out[k].offset += h->position;
     }
     const uint64_t consumed = eof ? len : emitted;
     const uint64_t tail = len - consumed;
-    if (tail && consumed) {  // tail to the front of the other buffer (same capacity, 16-B aligned base)
-        if (tail + 256 > h->dbuf[1 - h->cur].cap) return fail(CG_E_IO, "push: retained tail exceeds its buffer");
+    if (tail && consumed) {  // tail to the front of the other buffer (16-B aligned base)
+        if ((rc = h->dbuf[1 - h->cur].ensure(std::max(h->dbuf[h->cur].cap, tail + 256), "push buffer"))) return rc;
         HIP_TRY(hipMemcpyAsync(h->dbuf[1 - h->cur].p, d_in + consumed, tail, hipMemcpyDeviceToDevice, st));
         HIP_TRY(hipStreamSynchronize(st));
         h->cur = 1 - h->cur;
@@ -626,15 +797,17 @@ int push_append(cg_push *h, const uint8_t *data, uint64_t len) {
     // both buffers always have the same capacity, so a tail move never needs to grow one
     const uint64_t need = h->dlen + len + 256;
     if (need > h->dbuf[h->cur].cap) {
+        // grow: the tail moves into the (larger) other buffer, which becomes current as
+        // soon as it holds the only copy; a failed allocation leaves a usable handle
         DevBuf &nb = h->dbuf[1 - h->cur];
         nb.release();
         if ((rc = nb.ensure(need, "push buffer"))) return rc;
         if (h->dlen) HIP_TRY(hipMemcpyAsync(nb.p, h->dbuf[h->cur].p, h->dlen, hipMemcpyDeviceToDevice, st));
         HIP_TRY(hipStreamSynchronize(st));
-        DevBuf &ob = h->dbuf[h->cur];
+        h->cur = 1 - h->cur;
+        DevBuf &ob = h->dbuf[1 - h->cur];
         ob.release();
         if ((rc = ob.ensure(need, "push buffer"))) return rc;  // same request -> same capacity
-        h->cur = 1 - h->cur;
     }
     HIP_TRY(hipMemcpyAsync(h->dbuf[h->cur].as<uint8_t>() + h->dlen, data, len, hipMemcpyHostToDevice, st));
     HIP_TRY(hipStreamSynchronize(st));
@@ -651,6 +824,7 @@ uint32_t cg_abi_version(void) { return CG_ABI_VERSION; }
 const char *cg_last_error_message(void) { return t_err.c_str(); }
 
 int cg_validate(uint64_t min_size, uint64_t avg_size, uint64_t max_size, char *msg, size_t msg_cap) {
+    clear_error();
     Opts o;
     return resolve(min_size, avg_size, max_size, &o, msg, msg_cap);
 }
@@ -660,13 +834,13 @@ size_t cg_capacity(uint64_t len, uint64_t min_size) { return capacity_of(len, mi
 int cg_chunk_batch(const uint8_t *data, const uint64_t *nar_offsets, size_t n_nars, uint64_t min_size,
                    uint64_t avg_size, uint64_t max_size, int algo, cg_desc *out, size_t out_cap,
                    uint64_t *nar_first) {
-    t_err.clear();
+    clear_error();
     return batch_host(data, nar_offsets, n_nars, min_size, avg_size, max_size, algo, out, out_cap, nar_first);
 }
 
 int cg_chunk_descriptors(const uint8_t *data, uint64_t len, uint64_t min_size, uint64_t avg_size,
                          uint64_t max_size, int algo, cg_desc *out, size_t out_cap, size_t *n_out) {
-    t_err.clear();
+    clear_error();
     uint64_t offs[2] = {0, len};
     uint64_t first[2] = {0, 0};
     int rc = batch_host(data, offs, 1, min_size, avg_size, max_size, algo, out, out_cap, first);
@@ -677,11 +851,13 @@ int cg_chunk_descriptors(const uint8_t *data, uint64_t len, uint64_t min_size, u
 int cg_chunk_batch_device(const uint8_t *d_data, const uint64_t *nar_offsets, size_t n_nars, uint64_t min_size,
                           uint64_t avg_size, uint64_t max_size, int algo, cg_desc *d_out, size_t out_cap,
                           uint64_t *nar_first, void *stream) {
-    t_err.clear();
+    clear_error();
     Opts o;
     int rc = resolve(min_size, avg_size, max_size, &o, nullptr, 0);
     if (rc) return rc;
-    if (n_nars && nar_offsets[0] != 0) return fail(CG_E_BOUNDS, "device batch offsets must start at 0");
+    if (n_nars && nar_offsets[0] != 0)
+        return fail_bounds(nar_offsets[n_nars], nar_offsets[0], 0, "device batch offsets must start at 0");
+    if ((rc = check_tables())) return rc;
     Workspace *ws = nullptr;
     if ((rc = acquire(&ws))) return rc;
     WsGuard guard{ws};
@@ -691,7 +867,7 @@ int cg_chunk_batch_device(const uint8_t *d_data, const uint64_t *nar_offsets, si
 
 int cg_hash_spans_device(const uint8_t *d_data, const uint64_t *d_offsets, const uint64_t *d_lengths, size_t n,
                          int algo, uint8_t *d_digests, void *stream) {
-    t_err.clear();
+    clear_error();
     if (algo != CG_BLAKE3 && algo != CG_SHA256) return fail(CG_E_INVALID_OPTIONS, "unknown hash algorithm");
     if (n == 0) return CG_OK;
     Workspace *ws = nullptr;
@@ -703,7 +879,7 @@ int cg_hash_spans_device(const uint8_t *d_data, const uint64_t *d_offsets, const
 
 int cg_cas_ids_device(const uint8_t *d_data, const uint64_t *d_offsets, const uint64_t *d_lengths, size_t n,
                       uint32_t kind, uint8_t *d_ids, void *stream) {
-    t_err.clear();
+    clear_error();
     int rc = check_kind(kind);
     if (rc || n == 0) return rc;
     Workspace *ws = nullptr;
@@ -713,7 +889,7 @@ int cg_cas_ids_device(const uint8_t *d_data, const uint64_t *d_offsets, const ui
 }
 
 int cg_cas_id(const uint8_t *data, uint64_t len, uint32_t kind, uint8_t out[32]) {
-    t_err.clear();
+    clear_error();
     int rc = check_kind(kind);
     if (rc) return rc;
     Workspace *ws = nullptr;
@@ -739,12 +915,14 @@ int cg_cas_id(const uint8_t *data, uint64_t len, uint32_t kind, uint8_t out[32])
 int cg_node_put_batch_device(const uint8_t *d_data, const uint64_t *nar_offsets, size_t n_nars, uint64_t min_size,
                              uint64_t avg_size, uint64_t max_size, cg_desc *d_out, size_t out_cap,
                              uint64_t *nar_first, uint8_t *d_chunk_ids, uint8_t *manifest_ids, void *stream) {
-    t_err.clear();
+    clear_error();
     Opts o;
     int rc = resolve(min_size, avg_size, max_size, &o, nullptr, 0);
     if (rc) return rc;
     if (!d_chunk_ids) return fail(CG_E_IO, "node put: null chunk id buffer");
-    if (n_nars && nar_offsets[0] != 0) return fail(CG_E_BOUNDS, "device batch offsets must start at 0");
+    if (n_nars && nar_offsets[0] != 0)
+        return fail_bounds(nar_offsets[n_nars], nar_offsets[0], 0, "device batch offsets must start at 0");
+    if ((rc = check_tables())) return rc;
     Workspace *ws = nullptr;
     if ((rc = acquire(&ws))) return rc;
     WsGuard guard{ws};
@@ -754,11 +932,12 @@ int cg_node_put_batch_device(const uint8_t *d_data, const uint64_t *nar_offsets,
 
 int cg_node_put(const uint8_t *data, uint64_t len, uint64_t min_size, uint64_t avg_size, uint64_t max_size,
                 cg_desc *out, size_t out_cap, size_t *n_out, uint8_t *chunk_ids, uint8_t manifest_id[32]) {
-    t_err.clear();
+    clear_error();
     if (n_out) *n_out = 0;
     Opts o;
     int rc = resolve(min_size, avg_size, max_size, &o, nullptr, 0);
     if (rc) return rc;
+    if ((rc = check_tables())) return rc;
     Workspace *ws = nullptr;
     if ((rc = acquire(&ws))) return rc;
     WsGuard guard{ws};
@@ -785,7 +964,7 @@ int cg_node_put(const uint8_t *data, uint64_t len, uint64_t min_size, uint64_t a
 }
 
 int cg_hash(const uint8_t *data, uint64_t len, int algo, uint8_t out[32]) {
-    t_err.clear();
+    clear_error();
     if (algo != CG_BLAKE3 && algo != CG_SHA256) return fail(CG_E_INVALID_OPTIONS, "unknown hash algorithm");
     if (algo == CG_BLAKE3 && len > MAXIMUM_MAX) return fail(CG_E_BOUNDS, "cg_hash: BLAKE3 input above 16 MiB");
     Workspace *ws = nullptr;
@@ -810,7 +989,7 @@ int cg_hash(const uint8_t *data, uint64_t len, int algo, uint8_t out[32]) {
 }
 
 cg_push *cg_push_new(uint64_t min_size, uint64_t avg_size, uint64_t max_size, int algo, int *status) {
-    t_err.clear();
+    clear_error();
     Opts o;
     int rc = resolve(min_size, avg_size, max_size, &o, nullptr, 0);
     if (!rc && algo != CG_BLAKE3 && algo != CG_SHA256) rc = fail(CG_E_INVALID_OPTIONS, "unknown hash algorithm");
@@ -823,23 +1002,32 @@ cg_push *cg_push_new(uint64_t min_size, uint64_t avg_size, uint64_t max_size, in
 }
 
 int cg_push_push(cg_push *h, const uint8_t *data, uint64_t len, cg_desc *out, size_t out_cap, size_t *n_out) {
-    t_err.clear();
+    clear_error();
     if (n_out) *n_out = 0;
     if (!h) return fail(CG_E_IO, "null push handle");
     if (h->finished) return fail(CG_E_INVALID_OPTIONS, "push called after finish");
     if (len == 0) return CG_OK;
-    int arc = push_append(h, data, len);
-    if (arc) return arc;
+    int rc = check_tables();
+    if (rc) return rc;
+    const uint64_t dlen0 = h->dlen;
+    if ((rc = push_append(h, data, len))) return rc;
     size_t n = 0;
-    int rc = push_drain(h, false, out, out_cap, &n);
+    if ((rc = push_drain(h, false, out, out_cap, &n))) {
+        // push_drain changes the handle only on success: dropping the appended bytes
+        // leaves it exactly as before this call, so a caller may retry the same slice
+        h->dlen = dlen0;
+        return rc;
+    }
     if (n_out) *n_out = n;
-    return rc;
+    return CG_OK;
 }
 
 int cg_push_finish(cg_push *h, cg_desc *out, size_t out_cap, size_t *n_out) {
-    t_err.clear();
+    clear_error();
     if (n_out) *n_out = 0;
     if (!h) return fail(CG_E_IO, "null push handle");
+    int rc0 = check_tables();
+    if (rc0) return rc0;
     h->finished = true;
     size_t n = 0;
     int rc = push_drain(h, true, out, out_cap, &n);
@@ -855,20 +1043,51 @@ size_t cg_push_out_capacity(const cg_push *h, uint64_t next_len) {
 
 void cg_push_free(cg_push *h) { delete h; }
 
-int cg_set_gear_table(const uint64_t gear[256]) {
-    {
-        std::lock_guard<std::mutex> g(g_gear_mu);
-        memcpy(g_gear, gear, sizeof g_gear);
-        g_gear_init = true;
+int cg_set_cdc_tables(const uint64_t gear[256], const uint64_t masks[26]) {
+    clear_error();
+    if (!gear) return fail(CG_E_INVALID_OPTIONS, "null GEAR table");
+    auto t = std::make_shared<Tables>();
+    memcpy(t->gear, gear, sizeof t->gear);
+    if (masks) {
+        // the candidate scan's 48-byte window is exact only for masks within bits 0..47
+        for (int i = 0; i < 26; ++i)
+            if (masks[i] >> 48)
+                return fail(CG_E_INVALID_OPTIONS, "MASKS[" + std::to_string(i) +
+                                                      "] has bits above 47: unsupported by the windowed GPU scan");
+        memcpy(t->masks, masks, sizeof t->masks);
+    } else {
+        memcpy(t->masks, tables()->masks, sizeof t->masks);
     }
-    g_gear_placeholder.store(memcmp(gear, CG_DEFAULT_GEAR, sizeof g_gear) == 0 ? CG_GEAR_IS_PLACEHOLDER : 0);
-    g_gear_epoch.fetch_add(1);
+    t->placeholder = CG_GEAR_IS_PLACEHOLDER && memcmp(gear, CG_DEFAULT_GEAR, sizeof t->gear) == 0;
+    std::lock_guard<std::mutex> g(g_tab_mu);
+    t->epoch = g_tab_epoch.fetch_add(1) + 1;
+    g_tab = t;
     return CG_OK;
 }
 
-void cg_get_gear_table(uint64_t gear[256]) { gear_snapshot(gear); }
+int cg_set_gear_table(const uint64_t gear[256]) { return cg_set_cdc_tables(gear, nullptr); }
 
-int cg_gear_is_placeholder(void) { return g_gear_placeholder.load(); }
+void cg_get_cdc_tables(uint64_t gear[256], uint64_t masks[26]) {
+    const std::shared_ptr<const Tables> t = tables();
+    if (gear) memcpy(gear, t->gear, sizeof t->gear);
+    if (masks) memcpy(masks, t->masks, sizeof t->masks);
+}
+
+void cg_get_gear_table(uint64_t gear[256]) { cg_get_cdc_tables(gear, nullptr); }
+
+int cg_gear_is_placeholder(void) { return tables()->placeholder ? 1 : 0; }
+
+int cg_selftest(void) {
+    clear_error();
+    return selftest_gpu();
+}
+
+int cg_tables_verified(void) { return g_verified_epoch.load() == tables()->epoch ? 1 : 0; }
+
+int cg_last_error_detail(uint64_t out[3]) {
+    if (out) memcpy(out, t_detail, sizeof t_detail);
+    return t_status;
+}
 
 void cg_set_profiling(int on) { g_profiling.store(on ? 1 : 0); }
 

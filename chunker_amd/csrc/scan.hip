@@ -81,7 +81,7 @@ __device__ __forceinline__ void quad_transpose(uint4 v[4], uint32_t lane) {
 // running min (5 VALU + 1 LDS read per byte); a piece whose min hits 0 in some lane
 // is re-walked exactly for that lane.  Used when mask_s & mask_l has >= 15 bits
 // (hits are rarer than ~1 per 32 KiB); otherwise every byte is tested exactly.
-// DIAG (diagnostics only, 0 = product): 1 = loads only, 2 = loads + transpose,
+// DIAG (diagnostics build only, 0 = product): 1 = loads only, 2 = loads + transpose,
 // 3 = hashing on register-resident bytes without loads, 4 = as 3 without LDS reads;
 // + 8 = non-temporal loads.
 template <bool PRE, int DIAG = 0>
@@ -306,12 +306,15 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan(const uint8_t *__restrict__ da
     seg_count[seg] = count;
 }
 
-uint32_t g_scan_diag = 0;  // set by cg_diag_scan_mode (diagnostics only; 0 = product)
+#ifdef CG_DIAG
+uint32_t g_scan_diag = 0;  // set by cg_diag_scan_mode (diagnostics build only)
+#endif
 
 void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint64_t mask_s, uint64_t mask_l,
                  uint32_t cap, uint32_t *d_seg_count, uint32_t *d_seg_cand, uint64_t nseg, hipStream_t st) {
     if (nseg == 0) return;
     const uint64_t blocks = (nseg + SCAN2_T - 1) / SCAN2_T;
+#ifdef CG_DIAG
     if (g_scan_diag && __builtin_popcountll(mask_s & mask_l) >= 15) {
         auto k = g_scan_diag == 1   ? k_scan<true, 1>
                  : g_scan_diag == 2 ? k_scan<true, 2>
@@ -321,7 +324,10 @@ void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint
                                     : k_scan<true, 9>;
         hipLaunchKernelGGL(k, dim3((uint32_t)blocks), dim3(SCAN2_T), 0, st, d_data, n, d_gear, mask_s, mask_l, cap,
                            d_seg_count, d_seg_cand, nseg);
-    } else if (__builtin_popcountll(mask_s & mask_l) >= 15)
+        return;
+    }
+#endif
+    if (__builtin_popcountll(mask_s & mask_l) >= 15)
         hipLaunchKernelGGL(k_scan<true>, dim3((uint32_t)blocks), dim3(SCAN2_T), 0, st, d_data, n, d_gear, mask_s,
                            mask_l, cap, d_seg_count, d_seg_cand, nseg);
     else

@@ -155,22 +155,42 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 #define PC_RING 4u  // LDS schedule slots: the producer runs up to 4 blocks ahead
 
 // Spin guard: no legitimate wait for a ring slot lasts more than a few blocks
-// (~10^4 clocks); 2^26 sleeps (~2 s) ends a wait that would otherwise hang the GPU.
-#define SHA_SPIN_LIMIT (1u << 26)
+// (~10^4 clocks); after `limit` sleeps (2^26 by default, ~2 s) a wait gives up so a
+// broken hand-off cannot hang the GPU, and raises the workgroup's timeout flag: the
+// kernel then reports the launch as failed (k_sha256 -> *err) and the host returns
+// CG_E_IO instead of digests computed from a stale ring slot.
+// The workgroup's hand-off words live in LDS in this order; the waits find the flag
+// and the limit from the counter they poll.
+enum { SY_READY = 0, SY_DONE = 1, SY_TIMEOUT = 2, SY_LIMIT = 3, SY_N = 4 };
+
+__device__ __forceinline__ bool spin_expired(const uint32_t *sync, uint32_t &it) {
+    if (++it <= sync[SY_LIMIT]) {
+        __builtin_amdgcn_s_sleep(1);
+        return false;
+    }
+    __hip_atomic_store(const_cast<uint32_t *>(sync) + SY_TIMEOUT, 1u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_WORKGROUP);
+    return true;
+}
 
 // Wait until `*ctr` moved past `k` (consumer: producer filled slot k) -- `ready`
 // form -- or until slot k is free (producer: consumer released k - PC_RING).
 __device__ __forceinline__ unsigned long long wait_ready(const uint32_t *ctr, uint32_t k, bool timed) {
     if (lds_load_acquire(ctr) > k) return 0;
     const unsigned long long t0 = timed ? __builtin_amdgcn_s_memtime() : 0ull;
-    for (uint32_t it = 0; lds_load_acquire(ctr) <= k && it < SHA_SPIN_LIMIT; ++it) __builtin_amdgcn_s_sleep(1);
+    const uint32_t *sync = ctr - SY_READY;
+    uint32_t it = 0;
+    while (lds_load_acquire(ctr) <= k && !spin_expired(sync, it)) {
+    }
     return timed ? __builtin_amdgcn_s_memtime() - t0 : 0ull;
 }
 __device__ __forceinline__ unsigned long long wait_slot(const uint32_t *done, uint32_t k, bool timed) {
     if ((int)(k - lds_load_acquire(done)) < (int)PC_RING) return 0;
     const unsigned long long t0 = timed ? __builtin_amdgcn_s_memtime() : 0ull;
-    for (uint32_t it = 0; (int)(k - lds_load_acquire(done)) >= (int)PC_RING && it < SHA_SPIN_LIMIT; ++it)
-        __builtin_amdgcn_s_sleep(1);
+    const uint32_t *sync = done - SY_DONE;
+    uint32_t it = 0;
+    while ((int)(k - lds_load_acquire(done)) >= (int)PC_RING && !spin_expired(sync, it)) {
+    }
     return timed ? __builtin_amdgcn_s_memtime() - t0 : 0ull;
 }
 // This wave's schedule writes for block k have landed: publish k + 1.
@@ -578,10 +598,14 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
                                                uint64_t max_chunks, const uint32_t *__restrict__ order,
                                                uint8_t *__restrict__ hash_base, size_t stride,
                                                unsigned long long *__restrict__ diag, uint32_t mode,
-                                               uint32_t nquad, uint32_t npair) {
+                                               uint32_t nquad, uint32_t npair, uint32_t spin_limit,
+                                               uint32_t *__restrict__ err) {
     unsigned long long t_start = diag ? __builtin_amdgcn_s_memtime() : 0ull, t_spin = 0;
     __shared__ __attribute__((aligned(16))) uint32_t sW[PC_RING][64 * PC_ROW];
-    __shared__ uint32_t s_ready, s_done;  // blocks filled by the producer / consumed by the consumer
+    // hand-off words (SY_*): blocks filled by the producer / consumed by the consumer,
+    // the spin guard's timeout flag and limit
+    __shared__ uint32_t s_sync[SY_N];
+    uint32_t &s_ready = s_sync[SY_READY], &s_done = s_sync[SY_DONE];
     const uint32_t lane = threadIdx.x & 63u;
     const bool producer = threadIdx.x < 64;
     const uint32_t b = blockIdx.x;
@@ -605,6 +629,8 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
     if (threadIdx.x == 0) {
         s_ready = 0;
         s_done = 0;
+        s_sync[SY_TIMEOUT] = 0;
+        s_sync[SY_LIMIT] = spin_limit;
     }
     __syncthreads();
     const uint64_t g = wg_base + slot;
@@ -680,6 +706,10 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
                               __builtin_bswap32(st[7]));
         }
     }
+    // both waves are past their last wait: report an expired spin guard (vector store)
+    __syncthreads();
+    if (threadIdx.x == 0 && __hip_atomic_load(&s_sync[SY_TIMEOUT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------------------
@@ -771,13 +801,21 @@ const uint32_t *launch_len_order(const void *d_desc, const uint64_t *d_total, ui
     return ord;
 }
 
-unsigned long long *g_sha_diag = nullptr;  // set by cg_diag_sha_stats (diagnostics only)
-uint32_t g_sha_mode = 0;                    // set by cg_diag_sha_mode (diagnostics only; 0 = product)
-// Split-lane workgroups per launch (32 longest chunks each): one per CU.  Set by
-// cg_diag_sha_split_max (diagnostics; 0 = one lane per chunk everywhere).
+#ifdef CG_DIAG
+unsigned long long *g_sha_diag = nullptr;  // set by cg_diag_sha_stats (diagnostics build only)
+uint32_t g_sha_mode = 0;                    // set by cg_diag_sha_mode (diagnostics build only)
+#else
+constexpr unsigned long long *g_sha_diag = nullptr;
+constexpr uint32_t g_sha_mode = 0;
+#endif
+// Split-lane workgroups per launch (32 longest chunks each): one per CU.  Test hook
+// cg_test_sha_split_max (0 = one lane per chunk everywhere).
 uint32_t g_sha_split_max = 256;
-// Quad workgroups per launch (8 longest chunks each).  cg_diag_sha_quad_max.
+// Quad workgroups per launch (8 longest chunks each).  Test hook cg_test_sha_quad_max.
 uint32_t g_sha_quad_max = 256;
+// Spin-guard limit (sleeps per wait) of the producer/consumer hand-off: test hook
+// cg_test_sha_spin_limit.
+uint32_t g_sha_spin_limit = 1u << 26;
 
 // Workgroup tiers for a launch of up to max_chunks chunks, `expected` of them
 // likely (total bytes / (min + avg)).  A quad workgroup holds a whole workgroup's
@@ -803,7 +841,7 @@ uint32_t sha256_grid(uint64_t max_chunks, uint64_t expected, uint32_t *nquad_out
 
 void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
                    uint64_t max_chunks, uint64_t expected, uint64_t max_len, uint32_t *d_order_tmp,
-                   uint8_t *d_hash_base, size_t hash_stride, hipStream_t st) {
+                   uint8_t *d_hash_base, size_t hash_stride, uint32_t *d_err, hipStream_t st) {
     if (max_chunks == 0) return;
     uint32_t nquad = 0, npair = 0;
     const uint32_t nwg = sha256_grid(max_chunks, expected, &nquad, &npair);
@@ -816,9 +854,10 @@ void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
     const size_t pad = nwg <= 256 ? 16384 : 0;
     hipLaunchKernelGGL(k_sha256, dim3(nwg), dim3(128), pad, st, d_data, d_abs,
                        (const DescRaw *)d_desc, d_total, max_chunks, order, d_hash_base, hash_stride, g_sha_diag,
-                       g_sha_mode, nquad, npair);
+                       g_sha_mode, nquad, npair, g_sha_spin_limit, d_err);
 }
 
+#ifdef CG_DIAG
 // ---------------------------------------------------------------------------
 // Diagnostics: cycles per split round for a lone wave (the same round code the
 // split consumer runs, schedule words held in registers).
@@ -865,8 +904,10 @@ __global__ void k_diag_dpp_probe(uint32_t *out) {
     out[lane] = b;
 }
 
+#endif  // CG_DIAG
 }  // namespace cg
 
+#ifdef CG_DIAG
 // quad != 0: the 9-VALU quad round; else the 10-VALU pair round
 extern "C" int cg_diag_sha_rounds_split(uint32_t iters, uint32_t blocks, uint32_t threads, int quad,
                                         unsigned long long *h_cycles) {
@@ -894,23 +935,29 @@ extern "C" int cg_diag_dpp_probe(uint32_t *h_out) {
     return e == hipSuccess ? 0 : 2;
 }
 
-extern "C" uint32_t cg_diag_sha_split_max(uint32_t v) {
+// workgroups the digest launch uses for `max_chunks` (diagnostics: sizes cg_diag_sha_stats)
+extern "C" uint32_t cg_diag_sha_grid(uint64_t max_chunks, uint64_t expected) {
+    return cg::sha256_grid(max_chunks, expected, nullptr, nullptr);
+}
+#endif  // CG_DIAG
+
+// Test hooks: tier caps of the digest launch (the parity tests force every tier mix)
+// and the spin-guard limit (a test drives the timeout path); each returns the old value.
+extern "C" uint32_t cg_test_sha_split_max(uint32_t v) {
     const uint32_t old = cg::g_sha_split_max;
     cg::g_sha_split_max = v;
     return old;
 }
 
-// workgroups the digest launch uses for `max_chunks` (diagnostics: sizes cg_diag_sha_stats)
-extern "C" uint32_t cg_diag_sha_grid(uint64_t max_chunks, uint64_t expected) {
-    return cg::sha256_grid(max_chunks, expected, nullptr, nullptr);
+extern "C" uint32_t cg_test_sha_spin_limit(uint32_t v) {
+    const uint32_t old = cg::g_sha_spin_limit;
+    cg::g_sha_spin_limit = v;
+    return old;
 }
 
-extern "C" uint32_t cg_diag_sha_quad_max(uint32_t v) {
+extern "C" uint32_t cg_test_sha_quad_max(uint32_t v) {
     const uint32_t old = cg::g_sha_quad_max;
     cg::g_sha_quad_max = v;
     return old;
 }
 
-namespace cg {
-
-}  // namespace cg

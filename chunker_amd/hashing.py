@@ -12,7 +12,7 @@ from .chunking import HashAlgorithm, _as_u8, _check, _ptr
 def _digest(data, algo: HashAlgorithm) -> bytes:
     a = _as_u8(data)
     out = (ctypes.c_uint8 * 32)()
-    _check(lib.cg_hash(_ptr(a), len(a), int(algo), out), len(a))
+    _check(lib.cg_hash(_ptr(a), len(a), int(algo), out))
     return bytes(out)
 
 

@@ -33,6 +33,34 @@ def synth_nars(sizes, zeros: bool = False, first_index: int = 0, out: np.ndarray
     return out[:total], offs
 
 
+def synth_nars_device(sizes, zeros: bool = False, first_index: int = 0, pad: int = 256,
+                      host_chunk: int = 2 << 30):
+    """The same batch written straight into one device buffer (a torch uint8 CUDA
+    tensor of total + pad bytes), synthesised NAR group by NAR group through a host
+    buffer of at most max(host_chunk, largest NAR) bytes: 16 GiB batches (BASELINE
+    configs 4 and 5) need no 16 GiB host copy.  Returns (device tensor, offsets[n+1])."""
+    import torch
+
+    sizes = np.ascontiguousarray(sizes, dtype=np.uint64)
+    offs = np.zeros(len(sizes) + 1, np.uint64)
+    np.cumsum(sizes, out=offs[1:])
+    total = int(offs[-1])
+    dev = torch.empty(total + pad, dtype=torch.uint8, device="cuda")
+    cap = max(host_chunk, int(sizes.max()) if len(sizes) else 0)
+    host = torch.empty(cap, dtype=torch.uint8).pin_memory()
+    hnp = host.numpy()
+    i = 0
+    while i < len(sizes):
+        j, acc = i, 0
+        while j < len(sizes) and acc + int(sizes[j]) <= cap:
+            acc += int(sizes[j])
+            j += 1
+        synth_nars(sizes[i:j], zeros=zeros, first_index=first_index + i, out=hnp)
+        dev[int(offs[i]):int(offs[j])].copy_(host[:acc])  # synchronous: the host buffer is reused
+        i = j
+    return dev, offs
+
+
 def xorshift_bytes_py(seed: int, n: int) -> bytes:
     """Pure-Python xorshift64 stream (crates/node/src/lib.rs:192-203), for tests."""
     m = (1 << 64) - 1

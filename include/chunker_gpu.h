@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CG_ABI_VERSION 1u
+#define CG_ABI_VERSION 2u
 
 /* Status codes.  1..5 map 1:1 onto ChunkingError (src/chunking.rs:33-51) so the
  * host shim can rebuild the exact Display strings. */
@@ -38,6 +38,8 @@ typedef enum {
     CG_E_BUFFER_LIMIT = 5,       /* ChunkingError::BufferLimitExceeded (device OOM) */
     CG_E_CAPACITY = 6,           /* ABI only: caller's output array too small */
     CG_E_NO_DEVICE = 7,          /* ABI only: no gfx950 device; there is no CPU fallback */
+    CG_E_TABLES = 8,             /* ABI only: FastCDC tables are the placeholder or failed the selftest
+                                    (the shim maps it to ChunkingError::Io with the message) */
 } cg_status;
 
 /* HashAlgorithm (src/chunking.rs:53-58), same declaration order. */
@@ -56,6 +58,13 @@ uint32_t cg_abi_version(void);
  * CG_E_INVALID_OPTIONS it is exactly the InvalidOptions payload of
  * ChunkingOptions::validate (src/chunking.rs:190-231). */
 const char *cg_last_error_message(void);
+
+/* Fields of the last failure on this thread, so the shim can rebuild the reference's
+ * variants exactly (src/chunking.rs:35-50): CG_E_BOUNDS -> out = {data_len, offset,
+ * length} (ChunkingError::Bounds); CG_E_BUFFER_LIMIT -> out = {attempted, limit, 0}
+ * (BufferLimitExceeded: bytes of the failed device allocation, device bytes free);
+ * zeros otherwise.  Returns that failure's status (CG_OK if the last call succeeded). */
+int cg_last_error_detail(uint64_t out[3]);
 
 /* ChunkingOptions::resolve/validate (src/chunking.rs:173-231).  Pass 0 for a size to
  * take the reference default (256 KiB / 1 MiB / 4 MiB, :179-181).  `msg` may be NULL. */
@@ -146,12 +155,30 @@ int cg_node_put_batch_device(const uint8_t *d_data, const uint64_t *nar_offsets,
 int cg_node_put(const uint8_t *data, uint64_t len, uint64_t min_size, uint64_t avg_size, uint64_t max_size,
                 cg_desc *out, size_t out_cap, size_t *n_out, uint8_t *chunk_ids, uint8_t manifest_id[32]);
 
-/* FastCDC v2020 GEAR table plumbing.  The compiled-in table comes from
- * tables/fastcdc_v2020_gear.txt; cg_set_gear_table replaces it process-wide
- * (all devices) for later calls. */
-int cg_set_gear_table(const uint64_t gear[256]);
+/* FastCDC v2020 tables [ext fastcdc 4.0.1 src/v2020]: GEAR[256] and MASKS[26], used by
+ * FastCDC::new at src/chunking.rs:334, :553, :893.  The compiled-in set comes from
+ * the tables/ text files; its GEAR is a PLACEHOLDER (the crate is not vendored in the reference),
+ * so the engine FAILS CLOSED: every chunking entry point (cg_chunk_*, cg_push_push /
+ * _finish, cg_node_put*) returns CG_E_TABLES while the placeholder is installed, and
+ * runs any other table set only after it reproduced the reference's golden fixture
+ * (src/chunking.rs:1266-1297) on the GPU (cg_selftest, run once per installed set on
+ * first use).  CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR=1 in the environment lifts the gate
+ * (tests and benchmarks; boundaries are then self-consistent, not the reference's).
+ * Digest-only entries (cg_hash*, cg_cas_*) do not use the tables and are never gated.
+ *
+ * cg_set_cdc_tables installs a set process-wide (all devices) for later calls; masks
+ * may be NULL to keep the current MASKS; a mask with bits above 47 -> CG_E_INVALID_OPTIONS
+ * (the windowed GPU scan needs every tested bit within 48 bytes of history). */
+int cg_set_cdc_tables(const uint64_t gear[256], const uint64_t masks[26]);
+void cg_get_cdc_tables(uint64_t gear[256], uint64_t masks[26]);
+int cg_set_gear_table(const uint64_t gear[256]); /* = cg_set_cdc_tables(gear, NULL) */
 void cg_get_gear_table(uint64_t gear[256]);
 int cg_gear_is_placeholder(void);
+/* Run the reference fixture through the GPU pipeline (scan, walk, assembly) with the
+ * installed tables: CG_OK if it gives fastcdc's 10 boundaries (the set is then marked
+ * verified), CG_E_TABLES with the boundaries found otherwise.  Needs a device. */
+int cg_selftest(void);
+int cg_tables_verified(void); /* 1 once the installed set passed cg_selftest */
 
 /* Per-stage device times (ms) of the last batch call on this thread, measured with
  * HIP events on the stream the kernels ran on.  Order: scan, compact, walk,

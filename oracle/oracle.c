@@ -18,8 +18,9 @@
  *   - blake3::hash                             src/chunking.rs:68-71 (BLAKE3 spec)
  *
  * Parity status: SHA-256 is pinned by hashlib (independent) and the KAT at
- * src/lib.rs:54-69; BLAKE3 by the KAT at src/hashing.rs:173-182 (<=1 KiB only --
- * tree mode is parity-unpinned); FastCDC is table-parametric: with the crate's
+ * src/lib.rs:54-69; BLAKE3 by the KAT at src/hashing.rs:173-182 and, for tree mode
+ * (multi-leaf inputs), by the published BLAKE3 test vectors for 0..102400 bytes
+ * (tests/golden/blake3_vectors.json); FastCDC is table-parametric: with the crate's
  * GEAR table it is pinned by src/chunking.rs:1266-1297, with the placeholder
  * table shipped in tables/ it is "parity unpinned" (see DESIGN.md).
  */

@@ -1,6 +1,9 @@
 """Diagnostic: BLAKE3 digest stage on config 3 with and without leaf loads
 (cg_diag_b3_mode 1 compresses register words instead: digests garbage), so the
 compression's own time and the load path's share can be read apart."""
+import os
+os.environ["CHUNKER_AMD_DIAG"] = "1"  # load libchunker_amd_diag.so (make -C chunker_amd/csrc diag)
+os.environ.setdefault("CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR", "1")
 import ctypes
 import json
 import sys

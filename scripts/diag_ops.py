@@ -1,6 +1,9 @@
 """Diagnostic: issue cost (cycles per instruction per wave) of the integer VALU
 instructions the scan / SHA-256 / BLAKE3 kernels are built from, for 1, 4, 8 and 16
 waves in one workgroup (s_memtime, shader clocks)."""
+import os
+os.environ["CHUNKER_AMD_DIAG"] = "1"  # load libchunker_amd_diag.so (make -C chunker_amd/csrc diag)
+os.environ.setdefault("CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR", "1")
 import ctypes
 import json
 import sys

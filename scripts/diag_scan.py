@@ -1,5 +1,8 @@
 """Diagnostic: k_scan stage time by diag mode (0 product, 1 loads only, 2 loads +
 transpose, 3 hashing without loads) on config-2 and config-4 shaped batches."""
+import os
+os.environ["CHUNKER_AMD_DIAG"] = "1"  # load libchunker_amd_diag.so (make -C chunker_amd/csrc diag)
+os.environ.setdefault("CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR", "1")
 import ctypes
 import json
 import sys

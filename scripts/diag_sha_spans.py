@@ -1,5 +1,8 @@
 """Diagnostic: cycles per SHA-256 round of k_sha256 on controlled span layouts
 (one long span per workgroup vs full workgroups), product mode and diag modes."""
+import os
+os.environ["CHUNKER_AMD_DIAG"] = "1"  # load libchunker_amd_diag.so (make -C chunker_amd/csrc diag)
+os.environ.setdefault("CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR", "1")
 import ctypes
 import json
 import sys

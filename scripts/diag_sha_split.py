@@ -4,8 +4,11 @@ Prints one JSON line: the DPP bank-mask lane probe the split rounds rely on, cyc
 per round of a lone wave for the split rounds (cg_diag_sha_rounds_split) and the
 one-lane rounds (cg_diag_sha_rounds), and for configs 2 and a quarter of config 4
 the digest-stage time at several caps on split workgroups
-(cg_diag_sha_split_max; 0 = one lane per chunk everywhere), with the digests
+(cg_test_sha_split_max; 0 = one lane per chunk everywhere), with the digests
 compared against the one-lane run."""
+import os
+os.environ["CHUNKER_AMD_DIAG"] = "1"  # load libchunker_amd_diag.so (make -C chunker_amd/csrc diag)
+os.environ.setdefault("CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR", "1")
 import ctypes
 import json
 import sys
@@ -18,11 +21,11 @@ import chunker_amd as ca  # noqa: E402
 from chunker_amd._lib import lib  # noqa: E402
 from chunker_amd.nar import synth_nars  # noqa: E402
 
-lib.cg_diag_sha_split_max.argtypes = [ctypes.c_uint32]
-lib.cg_diag_sha_split_max.restype = ctypes.c_uint32
+lib.cg_test_sha_split_max.argtypes = [ctypes.c_uint32]
+lib.cg_test_sha_split_max.restype = ctypes.c_uint32
 lib.cg_diag_dpp_probe.argtypes = [ctypes.c_void_p]
-lib.cg_diag_sha_quad_max.argtypes = [ctypes.c_uint32]
-lib.cg_diag_sha_quad_max.restype = ctypes.c_uint32
+lib.cg_test_sha_quad_max.argtypes = [ctypes.c_uint32]
+lib.cg_test_sha_quad_max.restype = ctypes.c_uint32
 lib.cg_diag_sha_rounds_split.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                          ctypes.c_void_p]
 lib.cg_diag_sha_rounds.argtypes = [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
@@ -59,8 +62,8 @@ for name, (n, size, params) in CFG.items():
     ref = None
     row = {}
     for qmax, smax in ((0, 0), (0, 256), (256, 0), (256, 256), (64, 256)):
-        prevq = lib.cg_diag_sha_quad_max(qmax)
-        prev = lib.cg_diag_sha_split_max(smax)
+        prevq = lib.cg_test_sha_quad_max(qmax)
+        prev = lib.cg_test_sha_split_max(smax)
         lib.cg_set_profiling(1)
         times = []
         for _ in range(3):
@@ -68,8 +71,8 @@ for name, (n, size, params) in CFG.items():
             lib.cg_last_stage_times(buf, 5)
             times.append(buf[4])
         lib.cg_set_profiling(0)
-        lib.cg_diag_sha_split_max(prev)
-        lib.cg_diag_sha_quad_max(prevq)
+        lib.cg_test_sha_split_max(prev)
+        lib.cg_test_sha_quad_max(prevq)
         nch = int(first[-1])
         dig = out[: nch * 48].view(-1, 48)[:, 16:].cpu().numpy()
         if ref is None:

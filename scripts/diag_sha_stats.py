@@ -1,4 +1,7 @@
 """Diagnostic: producer/consumer spin shares of the SHA kernel on config-2/4 batches."""
+import os
+os.environ["CHUNKER_AMD_DIAG"] = "1"  # load libchunker_amd_diag.so (make -C chunker_amd/csrc diag)
+os.environ.setdefault("CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR", "1")
 import ctypes
 import json
 import sys

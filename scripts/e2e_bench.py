@@ -1,6 +1,8 @@
 """End-to-end rate from host memory: NAR bytes start in host RAM
 (pageable numpy, or pinned), cross PCIe, are chunked + digested on the GPU, and the
 descriptors come back to host RAM.  Host API cg_chunk_batch (one call per batch)."""
+import os
+os.environ.setdefault("CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR", "1")  # placeholder GEAR: see tables/README.md
 import argparse
 import json
 import sys

@@ -3,6 +3,8 @@ memory through ChunkStream (reader slices) and PushChunker (caller slices, the N
 pattern), SHA-256, default params.  Reported per slice size; the GPU ChunkStream default
 is the 256 MiB slice (chunking.stream_read_size).  CPU: the oracle's PushChunker
 restatement (serial scan + serial SHA-NI, one thread) on a 256 MiB sample, 8 MiB pushes."""
+import os
+os.environ.setdefault("CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR", "1")  # placeholder GEAR: see tables/README.md
 import io
 import json
 import os

@@ -32,7 +32,20 @@ def test_library_exports_every_declared_symbol(ca):
     for s in syms:
         assert hasattr(ca.lib, s), f"missing export {s}"
     assert set(syms) == set(_lib.EXPORTS)
-    assert ca.lib.cg_abi_version() == 1
+    for s in _lib.TEST_HOOKS:
+        assert hasattr(ca.lib, s), f"missing test hook {s}"
+    assert ca.lib.cg_abi_version() == _lib.ABI_VERSION == 2
+
+
+def test_product_library_has_no_diagnostic_kernels(ca):
+    """Diagnostic kernels and modes live in libchunker_amd_diag.so only (make diag)."""
+    import subprocess
+
+    from chunker_amd import _lib
+
+    out = subprocess.run(["nm", "-D", "--defined-only", str(_lib.LIB_PATH)], capture_output=True, text=True,
+                         check=True).stdout
+    assert "cg_diag_" not in out and "k_diag" not in out
 
 
 def test_desc_layout(ca):
@@ -109,16 +122,51 @@ def test_no_cpu_fallback_without_gpu(ca):
 def test_gear_table_plumbing(ca):
     from oracle import oracle as O
 
-    g = np.zeros(256, np.uint64)
-    ca.lib.cg_get_gear_table(g.ctypes.data)
-    assert np.array_equal(g, O.GEAR)
+    g, m = ca.get_cdc_tables()
+    assert np.array_equal(g, O.GEAR) and np.array_equal(m, O.MASKS)
     assert bool(ca.lib.cg_gear_is_placeholder()) == O.GEAR_IS_PLACEHOLDER
     alt = (O.GEAR ^ np.uint64(1)).astype(np.uint64)
-    ca.lib.cg_set_gear_table(alt.ctypes.data)
-    ca.lib.cg_get_gear_table(g.ctypes.data)
-    assert np.array_equal(g, alt) and ca.lib.cg_gear_is_placeholder() == 0
-    ca.lib.cg_set_gear_table(O.GEAR.ctypes.data)
+    alt_m = O.MASKS.copy()
+    alt_m[14] ^= np.uint64(1 << 3)
+    try:
+        ca.set_cdc_tables(alt, alt_m)
+        g, m = ca.get_cdc_tables()
+        assert np.array_equal(g, alt) and np.array_equal(m, alt_m) and ca.lib.cg_gear_is_placeholder() == 0
+        assert not ca.tables_verified()  # a new set is unverified until the selftest passes
+        ca.set_cdc_tables(O.GEAR)  # masks=None keeps the current MASKS
+        g, m = ca.get_cdc_tables()
+        assert np.array_equal(g, O.GEAR) and np.array_equal(m, alt_m)
+        # the windowed GPU scan needs every tested bit within 48 bytes of history
+        bad = O.MASKS.copy()
+        bad[20] |= np.uint64(1 << 48)
+        with pytest.raises(ca.InvalidOptionsError, match="bits above 47"):
+            ca.set_cdc_tables(O.GEAR, bad)
+    finally:
+        ca.set_cdc_tables(O.GEAR, O.MASKS)
     assert bool(ca.lib.cg_gear_is_placeholder()) == O.GEAR_IS_PLACEHOLDER
+
+
+def test_error_fields_cross_the_abi(ca):
+    """ChunkingError::Bounds {data_len, offset, length} is rebuilt from
+    cg_last_error_detail (src/chunking.rs:35-42) -- no device needed for this one:
+    a device batch whose offsets do not start at 0 is rejected up front."""
+    import ctypes as C
+
+    offs = np.array([5, 10, 40], np.uint64)
+    first = np.zeros(3, np.uint64)
+    st = ca.lib.cg_chunk_batch_device(None, offs.ctypes.data, 2, 0, 0, 0, 1, None, 0, first.ctypes.data, None)
+    assert st == 1
+    assert ca._lib.last_error_detail() == (1, 40, 5, 0)
+    with pytest.raises(ca.BoundsError) as ei:
+        ca.chunk_batch_device(0, offs, 0, 0)
+    e = ei.value
+    assert (e.data_len, e.offset, e.length) == (40, 5, 0)
+    assert str(e) == "bounds_check_failed: offset 5 + length 0 exceeds data length 40"
+    # a successful call clears the detail
+    assert ca.lib.cg_validate(0, 0, 0, None, 0) == 0
+    assert ca._lib.last_error_detail() == (0, 0, 0, 0)
+    msg = C.create_string_buffer(8)
+    assert ca.lib.cg_validate(32, 64, 128, msg, 8) == 4 and ca._lib.last_error_detail()[0] == 4
 
 
 def test_synthetic_nar_layout(ca):

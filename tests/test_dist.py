@@ -58,3 +58,58 @@ def test_gather_descriptors_gloo(counts):
         rng = np.random.default_rng(r)
         want = rng.integers(0, 256, max(counts[r], 1) * DESC_BYTES + 96, dtype=np.uint8)[: counts[r] * DESC_BYTES]
         assert got[r] == want.tobytes()
+
+
+def _shard_worker(rank, world, port, n_total, params, q):
+    """One rank of the sharded pipeline on CPU: the oracle stands in for the GPU engine
+    (same descriptor layout), the gather is the code bench.py runs over RCCL."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from chunker_amd.dist import gather_batch
+    from chunker_amd.nar import synth_nars
+    from oracle import oracle as O
+
+    mine = shard_nars(n_total, world, rank)
+    sizes = [200_000 + 8 * (i % 5) for i in mine]
+    descs, first = [], [0]
+    if len(sizes):
+        data, offs = synth_nars(sizes, first_index=mine.start)
+        for i in range(len(sizes)):
+            d = O.chunk_descriptors(data[offs[i]:offs[i + 1]], *params, algo=1, nthreads=1)
+            descs.append(d)
+            first.append(first[-1] + len(d))
+    flat = np.concatenate(descs) if descs else np.zeros(0, O.DESC_DTYPE)
+    buf = torch.from_numpy(np.concatenate([flat.view(np.uint8), np.zeros(96, np.uint8)]))
+    out = gather_batch(buf, np.array(first, np.uint64))
+    if rank == 0:
+        q.put((out[0].numpy().tobytes(), out[1].tolist()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_total", [7, 1])
+def test_sharded_batch_reassembles_single_process_result(n_total):
+    """shard_nars + per-rank chunking + gather_batch == one process over all NARs
+    (world size 2, gloo); n_total = 1 leaves rank 1 with no NAR."""
+    from chunker_amd.nar import synth_nars
+    from oracle import oracle as O
+
+    world, params = 2, (4096, 16384, 65536)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, n_total, params, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got_bytes, got_first = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sizes = [200_000 + 8 * (i % 5) for i in range(n_total)]
+    data, offs = synth_nars(sizes, first_index=0)
+    want, first = [], [0]
+    for i in range(n_total):
+        d = O.chunk_descriptors(data[offs[i]:offs[i + 1]], *params, algo=1, nthreads=1)
+        want.append(d)
+        first.append(first[-1] + len(d))
+    assert got_first == first
+    assert got_bytes == np.concatenate(want).tobytes()

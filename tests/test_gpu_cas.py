@@ -59,15 +59,11 @@ def test_shake_kat_and_reference_cas_cases(cas, O):
 
 
 def _pair_max(v):
-    """Cap the CAS pair tier (cg_diag_cas_pair_max): -1 = wave budget only, 0 = one lane
-    per span everywhere, k = the k longest spans on lane pairs; returns the old cap."""
-    import ctypes
-
+    """Cap the CAS pair tier (test hook cg_test_cas_pair_max): -1 = wave budget only, 0 =
+    one lane per span everywhere, k = the k longest spans on lane pairs; returns the old cap."""
     from chunker_amd import lib
 
-    f = lib.cg_diag_cas_pair_max
-    f.argtypes, f.restype = [ctypes.c_int64], ctypes.c_int64
-    return f(v)
+    return lib.cg_test_cas_pair_max(v)
 
 
 TIERS = pytest.mark.parametrize("pair_max", [-1, 0, 37], ids=["pairs", "single", "mixed"])

@@ -298,20 +298,21 @@ def test_digest_spans_all_lengths(ca, O):
 
 def _sha_kinds(ca, quad_max, pair_max):
     """Cap the quad and pair workgroups of the SHA-256 launch; returns the old caps."""
-    fq, fp = ca.lib.cg_diag_sha_quad_max, ca.lib.cg_diag_sha_split_max
-    for f in (fq, fp):
-        f.argtypes = [ctypes.c_uint32]
-        f.restype = ctypes.c_uint32
-    return fq(quad_max), fp(pair_max)
+    return ca.lib.cg_test_sha_quad_max(quad_max), ca.lib.cg_test_sha_split_max(pair_max)
 
 
 def test_dpp_bank_mask_lane_probe(ca):
     """The split-lane SHA-256 rounds pair lanes 4 apart in a DPP row: a row_shl:4 add
     with bank_mask 0x5 writes lanes 0-3 and 8-11 of each row from lanes 4-7 / 12-15
-    and leaves the others untouched."""
-    ca.lib.cg_diag_dpp_probe.argtypes = [ctypes.c_void_p]
+    and leaves the others untouched (probe kernel in the diagnostics build)."""
+    from chunker_amd._lib import DIAG_LIB_PATH, diag_lib
+
+    if not DIAG_LIB_PATH.exists():
+        pytest.skip("diagnostics build not present (make -C chunker_amd/csrc diag)")
+    D = diag_lib()
+    D.cg_diag_dpp_probe.argtypes = [ctypes.c_void_p]
     out = np.zeros(64, np.uint32)
-    assert ca.lib.cg_diag_dpp_probe(out.ctypes.data) == 0
+    assert D.cg_diag_dpp_probe(out.ctypes.data) == 0
     want = [(1000 + 2 * L + 4) if ((L >> 2) & 1) == 0 else L for L in range(64)]
     assert out.tolist() == want
 

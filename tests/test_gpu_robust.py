@@ -1,0 +1,167 @@
+"""GPU robustness of the engine behind the C ABI: concurrent callers, failure
+reporting, and the reference's error variants with their fields.
+
+* Re-entrancy (include/chunker_gpu.h "Threading"): the reference's callers are
+  concurrent -- thread-per-connection HTTP (crates/proto/nix/src/lib.rs:153-162),
+  BEAM dirty schedulers, rayon -- so 8 host threads chunk distinct inputs at once,
+  through the host entry and through the device entry on 8 distinct streams; every
+  result equals the oracle's.
+* The SHA-256 producer/consumer spin guard (sha256.hip) reports an expired wait as
+  CG_E_IO instead of returning digests computed from a stale ring slot.
+* BufferLimitExceeded{attempted, limit} (src/chunking.rs:49-50) carries its fields.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+P = (16_384, 65_536, 262_144)
+
+
+@pytest.fixture(scope="module")
+def ca(gpu):
+    import chunker_amd
+
+    return chunker_amd
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import oracle
+
+    return oracle
+
+
+def _same(got, ref):
+    return (len(got) == len(ref) and np.array_equal(got["offset"], ref["offset"])
+            and np.array_equal(got["length"], ref["length"]) and np.array_equal(got["hash"], ref["hash"]))
+
+
+@pytest.mark.parametrize("algo", [1, 0], ids=["sha256", "blake3"])
+def test_concurrent_host_callers(ca, O, algo):
+    from chunker_amd.nar import synth_nars
+
+    n_threads, per = 8, 6
+    batches = []
+    for t in range(n_threads):
+        sizes = [(3 << 20) + 8 * ((t * 7 + k) % 13) for k in range(per)]
+        data, offs = synth_nars(sizes, first_index=100 + t * per)
+        batches.append((data, offs))
+    results, errors = [None] * n_threads, []
+    start = threading.Barrier(n_threads)
+
+    def work(t):
+        try:
+            data, offs = batches[t]
+            start.wait()
+            for _ in range(2):  # twice: workspaces are recycled between callers
+                results[t] = ca.chunk_batch([data[offs[i]:offs[i + 1]] for i in range(per)], *P, hash=algo)
+        except Exception as e:  # noqa: BLE001
+            errors.append((t, repr(e)))
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(n_threads)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=100)
+    assert not errors, errors
+    for t, (data, offs) in enumerate(batches):
+        for i in range(per):
+            ref = O.chunk_descriptors(data[offs[i]:offs[i + 1]], *P, algo=algo, nthreads=8)
+            assert _same(results[t][i], ref), (t, i)
+
+
+def test_concurrent_device_callers_on_distinct_streams(ca, O):
+    import torch
+
+    from chunker_amd.nar import synth_nars
+
+    n_threads, per = 8, 4
+    jobs = []
+    for t in range(n_threads):
+        sizes = [(4 << 20) + 8 * k for k in range(per)]
+        data, offs = synth_nars(sizes, first_index=300 + t * per)
+        d = torch.from_numpy(data).cuda()
+        cap = ca.chunking.batch_capacity(offs, P[0])
+        out = torch.zeros(cap * 48, dtype=torch.uint8, device="cuda")
+        jobs.append((data, offs, d, out, cap, torch.cuda.Stream()))
+    torch.cuda.synchronize()
+    firsts, errors = [None] * n_threads, []
+    start = threading.Barrier(n_threads)
+
+    def work(t):
+        try:
+            data, offs, d, out, cap, s = jobs[t]
+            start.wait()
+            firsts[t] = ca.chunk_batch_device(d.data_ptr(), offs, out.data_ptr(), cap, *P, stream=s.cuda_stream)
+        except Exception as e:  # noqa: BLE001
+            errors.append((t, repr(e)))
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(n_threads)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=100)
+    assert not errors, errors
+    torch.cuda.synchronize()
+    for t, (data, offs, d, out, cap, s) in enumerate(jobs):
+        descs = out.cpu().numpy().view(ca.DESC_DTYPE)
+        first = firsts[t]
+        for i in range(per):
+            ref = O.chunk_descriptors(data[offs[i]:offs[i + 1]], *P, algo=1, nthreads=8)
+            assert _same(descs[int(first[i]):int(first[i + 1])], ref), (t, i)
+
+
+def test_sha_spin_guard_timeout_is_an_error(ca, O):
+    """With the spin limit forced to 0 every hand-off wait expires at once: the kernel
+    finishes (no hang) but flags the launch, and the call fails with CG_E_IO instead of
+    returning digests read from stale LDS ring slots.  Restored, the same call is exact."""
+    data = np.random.default_rng(11).integers(0, 256, 6 << 20, dtype=np.uint8)
+    old = ca.lib.cg_test_sha_spin_limit(0)
+    try:
+        with pytest.raises(ca.IoError, match="spin guard"):
+            ca.chunk_descriptors_array(data, *P)
+        assert ca._lib.last_error_detail()[0] == 2
+    finally:
+        ca.lib.cg_test_sha_spin_limit(old)
+    assert _same(ca.chunk_descriptors_array(data, *P), O.chunk_descriptors(data, *P, algo=1, nthreads=8))
+
+
+def test_buffer_limit_fields(ca):
+    """A device batch too large for HBM: BufferLimitExceeded{attempted, limit} with the
+    failed allocation's size and the device's free bytes (no kernel is launched)."""
+    import torch
+
+    free, _ = torch.cuda.mem_get_info()
+    d = torch.zeros(1024, dtype=torch.uint8, device="cuda")
+    offs = np.array([0, 1 << 50], np.uint64)  # claims a 1 PiB batch
+    with pytest.raises(ca.BufferLimitExceededError) as ei:
+        ca.chunk_batch_device(d.data_ptr(), offs, d.data_ptr(), 1)
+    e = ei.value
+    assert e.attempted > free and 0 < e.limit <= free + (64 << 20)
+    assert str(e) == f"buffer_limit_exceeded: attempted {e.attempted} bytes, limit {e.limit} bytes"
+    # the engine is still usable afterwards
+    assert len(ca.chunk_descriptors(b"hello world")) == 1
+
+
+def test_push_handle_survives_a_failed_push(ca):
+    """A push that fails inside the engine leaves the handle as it was: the
+    same slice pushed again continues the stream exactly."""
+    data = np.random.default_rng(5).integers(0, 256, 2_000_000, dtype=np.uint8).tobytes()
+    params = (8_192, 32_768, 131_072)
+    want = ca.chunk_data(data, *params)
+    pc = ca.PushChunker(*params)
+    got = list(pc.push(data[:700_000]))
+    old = ca.lib.cg_test_sha_spin_limit(0)
+    try:
+        with pytest.raises(ca.IoError):
+            pc.push(data[700_000:1_400_000])
+    finally:
+        ca.lib.cg_test_sha_spin_limit(old)
+    got += pc.push(data[700_000:1_400_000])
+    got += pc.push(data[1_400_000:])
+    got += pc.finish()
+    assert got == want
+    assert b"".join(c.payload for c in got) == data
