@@ -41,7 +41,8 @@ EXPORTS = (
     "cg_push_finish", "cg_push_bytes_consumed", "cg_push_out_capacity", "cg_push_free", "cg_hash_spans_device",
     "cg_set_cdc_tables", "cg_get_cdc_tables", "cg_set_gear_table", "cg_get_gear_table", "cg_gear_is_placeholder",
     "cg_selftest", "cg_tables_verified", "cg_set_profiling", "cg_last_stage_times", "cg_synth_nars", "cg_hash",
-    "cg_cas_ids_device", "cg_cas_id", "cg_node_put_batch_device", "cg_node_put",
+    "cg_cas_ids_device", "cg_cas_id", "cg_node_put_batch_device", "cg_node_put", "cg_stream_new", "cg_stream_push",
+    "cg_stream_finish", "cg_stream_take", "cg_stream_pending", "cg_stream_bytes_consumed", "cg_stream_free",
 )
 # test hooks the product library exports beyond the header (tier caps, spin-guard limit)
 TEST_HOOKS = ("cg_test_sha_quad_max", "cg_test_sha_split_max", "cg_test_sha_spin_limit", "cg_test_cas_pair_max")
@@ -88,6 +89,20 @@ def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
     L.cg_push_out_capacity.restype = sz
     L.cg_push_free.argtypes = [p]
     L.cg_push_free.restype = None
+    L.cg_stream_new.argtypes = [u64, u64, u64, i, u64, u64, ctypes.POINTER(i)]
+    L.cg_stream_new.restype = p
+    L.cg_stream_push.argtypes = [p, p, u64]
+    L.cg_stream_push.restype = i
+    L.cg_stream_finish.argtypes = [p]
+    L.cg_stream_finish.restype = i
+    L.cg_stream_take.argtypes = [p, p, sz, psz, i]
+    L.cg_stream_take.restype = i
+    L.cg_stream_pending.argtypes = [p]
+    L.cg_stream_pending.restype = u64
+    L.cg_stream_bytes_consumed.argtypes = [p]
+    L.cg_stream_bytes_consumed.restype = u64
+    L.cg_stream_free.argtypes = [p]
+    L.cg_stream_free.restype = None
     L.cg_hash_spans_device.argtypes = [p, p, p, sz, i, p, p]
     L.cg_hash_spans_device.restype = i
     L.cg_hash.argtypes = [p, u64, i, p]

@@ -13,7 +13,8 @@ ChunkMetadata / ChunkDescriptor        :76-155 (equality ignores payload, :120-1
 ChunkingOptions.resolve                :157-231
 chunk_data / chunk_data_with_hash      :241-297
 chunk_descriptors[_with_hash]          :299-374
-ChunkStream                            :382-740 (read-slice sizing :713-716, env cap :427-433)
+ChunkStream                            :382-740 (read-slice sizing :713-716, env cap :427-433),
+                                       pipelined on the GPU (cg_stream_*)
 PushChunker                            :742-829
 chunk_stream / chunk_stream_with_hash  :1132-1166
 =====================================  ======================================================
@@ -26,6 +27,7 @@ from __future__ import annotations
 import ctypes
 import enum
 import os
+from collections import deque
 from dataclasses import dataclass, field
 from typing import BinaryIO, Iterator, Sequence
 
@@ -172,11 +174,13 @@ class ChunkDescriptor:
 
 @dataclass(eq=False)
 class ChunkMetadata:
-    """ChunkMetadata (src/chunking.rs:76-98); equality/hash ignore payload (:120-134)."""
+    """ChunkMetadata (src/chunking.rs:76-98); equality/hash ignore payload (:120-134).
+    payload is bytes-like: `bytes`, or from ChunkStream a read-only memoryview into the
+    slice it was read in (zero-copy, like the reference's `Bytes`)."""
     hash: bytes
     offset: int
     length: int
-    payload: bytes = field(default=b"", repr=False)
+    payload: bytes | memoryview = field(default=b"", repr=False)
 
     def hash_hex(self) -> str:
         return self.hash.hex()
@@ -420,56 +424,99 @@ def effective_read_slice_cap() -> int:
     return DEFAULT_READ_SLICE_CAP
 
 
-# A GPU push costs about one digest chain of its longest chunk whatever the slice size
-# (streaming), so without an explicit CHUNKER_READ_SLICE_CAP_BYTES the
-# stream reads MAX_READ_SLICE_CAP-sized slices instead of the reference's 8 MiB default.
-# Chunks do not depend on the slice size (test_push_matches_in_memory_across_slice_sizes).
 def stream_read_size(max_size: int) -> int:
-    """Read size per refill: src/chunking.rs:713-716 when the cap is pinned by the
-    environment, else the GPU slice (MAX_READ_SLICE_CAP)."""
+    """Read size per refill, src/chunking.rs:713-716:
+    max(min(max(max_size * 8, 4 MiB), cap), 4096), cap = CHUNKER_READ_SLICE_CAP_BYTES
+    (default 8 MiB)."""
     target = max(max_size * 8, 4 * 1024 * 1024)
-    if os.environ.get("CHUNKER_READ_SLICE_CAP_BYTES") is None:
-        target = max(target, MAX_READ_SLICE_CAP)
-        return target
     return max(min(target, effective_read_slice_cap()), MIN_READ_SLICE_CAP)
 
 
+DEFAULT_STREAM_INFLIGHT = 512 * 1024 * 1024
+
+
+def stream_inflight_bytes() -> int:
+    """HBM the engine may hold for one ChunkStream's slices in flight (cg_stream_new):
+    CHUNKER_AMD_STREAM_INFLIGHT_BYTES, default 512 MiB.  The host keeps the same
+    slices alive until their chunks are emitted (payloads are slices of them)."""
+    try:
+        v = int(os.environ.get("CHUNKER_AMD_STREAM_INFLIGHT_BYTES", ""))
+        if v > 0:
+            return v
+    except ValueError:
+        pass
+    return DEFAULT_STREAM_INFLIGHT
+
+
 class ChunkStream:
-    """ChunkStream (src/chunking.rs:382-740): pull chunks from a binary reader."""
+    """ChunkStream (src/chunking.rs:382-740): pull chunks from a binary reader.
+
+    Reads slices of the reference's size (stream_read_size) and pushes them into the
+    engine's pipelined stream handle (cg_stream_*): cut points are found per slice, the
+    digests of many slices run concurrently on the GPU, and chunks come back strictly in
+    stream order with the reference's (offset, length, hash).  One slice is read ahead
+    on a helper thread while the engine works (the ctypes calls release the GIL)."""
 
     def __init__(self, reader: BinaryIO, min_size=None, avg_size=None, max_size=None,
                  hash: HashAlgorithm = HashAlgorithm.Sha256):
         self._reader = reader
-        self._push = PushChunker(min_size, avg_size, max_size, hash)
-        self._max = self._push.options.max_size
-        self._pending: list[ChunkMetadata] = []
+        self.options = ChunkingOptions.resolve(min_size, avg_size, max_size)
+        self.hash = HashAlgorithm(hash)
+        self._slice = stream_read_size(self.options.max_size)
+        st = ctypes.c_int(0)
+        o = self.options
+        self._h = lib.cg_stream_new(o.min_size, o.avg_size, o.max_size, int(self.hash), self._slice,
+                                    stream_inflight_bytes(), ctypes.byref(st))
+        if not self._h:
+            _raise(st.value)
+        self._segs: deque = deque()  # (stream offset, bytes) not yet fully emitted
+        self._pushed = 0
+        self._pending: deque = deque()
         self._eof = False
-        # read-ahead: the next slice is read on a helper thread while the engine chunks
-        # and digests the current one (the ctypes call releases the GIL); the bytes and
-        # their order are exactly what sequential reads return
+        self._done = False
+        self._out = np.zeros(4096, DESC_DTYPE)
         self._pool = None
         self._next = None
+
+    @classmethod
+    def new_with_hash(cls, reader, min_size, avg_size, max_size, hash):
+        return cls(reader, min_size, avg_size, max_size, hash)
 
     def _read_async(self):
         from concurrent.futures import ThreadPoolExecutor
 
         if self._pool is None:
             self._pool = ThreadPoolExecutor(1, thread_name_prefix="chunk-stream-read")
-        self._next = self._pool.submit(self._reader.read, stream_read_size(self._max))
+        self._next = self._pool.submit(self._reader.read, self._slice)
 
     def _close_pool(self):
         if self._pool is not None:
             self._pool.shutdown(wait=True)
             self._pool = None
 
-    def __del__(self):
-        pool = getattr(self, "_pool", None)
-        if pool is not None:
-            pool.shutdown(wait=False)
+    def _take(self, wait: bool) -> int:
+        n = ctypes.c_size_t(0)
+        _check(lib.cg_stream_take(self._h, self._out.ctypes.data, len(self._out), ctypes.byref(n), int(wait)))
+        for d in self._out[: n.value]:
+            off, ln = int(d["offset"]), int(d["length"])
+            self._pending.append(ChunkMetadata(bytes(d["hash"]), off, ln, self._payload(off, ln)))
+        if n.value:  # drop slices wholly before the last emitted byte
+            end = self._pending[-1].offset + self._pending[-1].length
+            while self._segs and self._segs[0][0] + len(self._segs[0][1]) <= end:
+                self._segs.popleft()
+        return n.value
 
-    @classmethod
-    def new_with_hash(cls, reader, min_size, avg_size, max_size, hash):
-        return cls(reader, min_size, avg_size, max_size, hash)
+    def _payload(self, off: int, ln: int) -> bytes:
+        parts = []
+        for start, mv in self._segs:
+            if start >= off + ln:
+                break
+            lo, hi = max(off, start), min(off + ln, start + len(mv))
+            if lo < hi:
+                parts.append(mv[lo - start:hi - start])
+        # one slice: a zero-copy view of the bytes read (the reference's Bytes::split_to,
+        # src/chunking.rs:592); a chunk spanning slices is joined once
+        return parts[0] if len(parts) == 1 else b"".join(parts)
 
     def __iter__(self) -> Iterator[ChunkMetadata]:
         return self
@@ -477,9 +524,15 @@ class ChunkStream:
     def __next__(self) -> ChunkMetadata:
         while True:
             if self._pending:
-                return self._pending.pop(0)
-            if self._eof:
+                return self._pending.popleft()
+            if self._done:
                 raise StopIteration
+            if self._eof:
+                if self._take(True) == 0 and lib.cg_stream_pending(self._h) == 0:
+                    self._done = True
+                continue
+            if self._take(False):
+                continue
             if self._next is None:
                 self._read_async()
             try:
@@ -492,11 +545,27 @@ class ChunkStream:
             if not buf:
                 self._next = None
                 self._close_pool()
+                _check(lib.cg_stream_finish(self._h))
                 self._eof = True
-                self._pending.extend(self._push.finish())
-            else:
-                self._read_async()
-                self._pending.extend(self._push.push(buf))
+                continue
+            self._read_async()
+            a = _as_u8(buf)
+            _check(lib.cg_stream_push(self._h, _ptr(a), len(a)))
+            keep = buf if isinstance(buf, bytes) else a.tobytes()
+            self._segs.append((self._pushed, memoryview(keep)))
+            self._pushed += len(keep)
+
+    def bytes_consumed(self) -> int:
+        return int(lib.cg_stream_bytes_consumed(self._h))
+
+    def __del__(self):
+        pool = getattr(self, "_pool", None)
+        if pool is not None:
+            pool.shutdown(wait=False)
+        h = getattr(self, "_h", None)
+        if h:
+            lib.cg_stream_free(h)
+            self._h = None
 
 
 def chunk_stream_with_hash(reader, min_size=None, avg_size=None, max_size=None,

@@ -1,0 +1,158 @@
+// runtime.h -- internals shared by the host runtime's translation units (runtime.hip:
+// batch pipeline, push handle, tables; stream.hip: the pipelined stream handle).
+// Nothing here is part of the C ABI (include/chunker_gpu.h).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/chunker_gpu.h"
+#include "common.h"
+
+namespace cgrt {
+
+// reference defaults, src/chunking.rs:179-181
+constexpr uint64_t DEF_MIN = 256 * 1024, DEF_AVG = 1024 * 1024, DEF_MAX = 4 * 1024 * 1024;
+// fastcdc::v2020 ranges [ext], pinned by src/chunking.rs:1401-1415
+constexpr uint64_t MINIMUM_MIN = 64, MINIMUM_MAX = 1048576, AVERAGE_MIN = 256, AVERAGE_MAX = 4194304,
+                   MAXIMUM_MIN = 1024, MAXIMUM_MAX = 16777216;
+
+// Failure reporting: status code + thread-local message (cg_last_error_message) and
+// the ChunkingError fields (cg_last_error_detail).
+int fail(int code, const std::string &msg);
+void clear_error();
+int fail_bounds(uint64_t data_len, uint64_t offset, uint64_t length, const std::string &what);
+int fail_limit(uint64_t attempted, const std::string &what);
+int hip_fail(hipError_t e, const char *what, uint64_t attempted = 0);
+
+#define HIP_TRY(expr)                                   \
+    do {                                                \
+        hipError_t _e = (expr);                         \
+        if (_e != hipSuccess) return hip_fail(_e, #expr); \
+    } while (0)
+
+// FastCDC v2020 tables (runtime.hip): one immutable snapshot per installed set.
+struct Tables {
+    uint64_t gear[256];
+    uint64_t masks[26];
+    uint64_t epoch;
+    bool placeholder;
+};
+
+std::shared_ptr<const Tables> tables();
+// Fail-closed gate in front of every chunking entry point.
+int check_tables();
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes, const char *name) {
+        if (bytes <= cap) return CG_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = bytes + bytes / 4 + 256;
+        hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return hip_fail(e, name, want);
+        }
+        cap = want;
+        return CG_OK;
+    }
+    template <class T>
+    T *as() const { return static_cast<T *>(p); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+struct PinBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return CG_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = bytes + bytes / 4 + 256;
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return hip_fail(e, "hipHostMalloc", want);
+        }
+        cap = want;
+        return CG_OK;
+    }
+    template <class T>
+    T *as() const { return static_cast<T *>(p); }
+};
+
+enum { EV_START, EV_SCAN, EV_COMPACT, EV_WALK, EV_ASSEMBLE, EV_DIGEST, EV_N };
+
+struct Workspace {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    uint64_t gear_epoch = 0;
+    DevBuf gear, seg_count, seg_cand, eoff, scan_tmp, entries, nar_off, cap_base, wchunk, nar_nchunks, nar_first,
+        chunk_abs, b3_gcount, b3_gbase, b3_gcv, b3_gmap, in, out, span_off, span_len, order, cas_order, ids,
+        man_abs, man_desc, sha_err;
+    PinBuf stage, err_stage;
+    hipEvent_t ev[EV_N] = {};
+    // CAS ids run on side_stream, concurrently with the digest: both stages are bound by
+    // their longest chunk's serial chain, not by the chip, so they overlap for free.
+    hipStream_t side_stream = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_cas = nullptr;
+    // Streams map onto the process's few hardware queues (GPU_MAX_HW_QUEUES, 4 by default)
+    // and two streams on one queue serialise: the side stream exists only where used.
+    int ensure_side_stream() {
+        if (!side_stream) HIP_TRY(hipStreamCreateWithFlags(&side_stream, hipStreamNonBlocking));
+        return CG_OK;
+    }
+    int init(int dev) {
+        device = dev;
+        HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        for (auto &e : ev) HIP_TRY(hipEventCreate(&e));
+        HIP_TRY(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+        HIP_TRY(hipEventCreate(&ev_cas));
+        return CG_OK;
+    }
+};
+
+int current_device(int *dev);
+int acquire(Workspace **out);
+void release(Workspace *ws);
+struct WsGuard {
+    Workspace *ws;
+    ~WsGuard() {
+        if (ws) release(ws);
+    }
+};
+
+struct Opts {
+    uint64_t min, avg, max;
+};
+
+int resolve(uint64_t mn, uint64_t avg, uint64_t mx, Opts *o, char *msg, size_t cap);
+uint64_t capacity_of(uint64_t len, uint64_t mn);
+uint32_t logarithm2(uint32_t v);
+
+// SHA-256 spin-guard word of a workspace: arm before a digest launch, fetch with the
+// call's results, check after the stream sync.
+int sha_err_arm(Workspace *ws, hipStream_t st);
+int sha_err_fetch(Workspace *ws, hipStream_t st);
+int sha_err_check(Workspace *ws);
+
+// The device pipeline for one batch (scan -> compact -> walk -> assemble -> digest).
+int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, size_t n_nars, const Opts &o,
+              int algo, cg_desc *d_out, size_t out_cap, uint64_t *h_nar_first, hipStream_t st,
+              uint8_t *d_chunk_ids = nullptr, uint8_t *h_manifest_ids = nullptr, bool digest = true);
+
+}  // namespace cgrt

@@ -17,19 +17,12 @@
 #include <thread>
 #include <vector>
 
-#include "../../include/chunker_gpu.h"
-#include "common.h"
 #include "gear_table.h"
+#include "runtime.h"
 
-namespace {
+namespace cgrt {
 
 static_assert(sizeof(cg_desc) == 48, "cg_desc must be 48 bytes");
-
-// reference defaults, src/chunking.rs:179-181
-constexpr uint64_t DEF_MIN = 256 * 1024, DEF_AVG = 1024 * 1024, DEF_MAX = 4 * 1024 * 1024;
-// fastcdc::v2020 ranges [ext], pinned by src/chunking.rs:1401-1415
-constexpr uint64_t MINIMUM_MIN = 64, MINIMUM_MAX = 1048576, AVERAGE_MIN = 256, AVERAGE_MAX = 4194304,
-                   MAXIMUM_MIN = 1024, MAXIMUM_MAX = 16777216;
 
 thread_local std::string t_err;
 thread_local uint64_t t_detail[3];  // ChunkingError fields of the last failure (cg_last_error_detail)
@@ -70,7 +63,7 @@ int fail_limit(uint64_t attempted, const std::string &what) {
     return CG_E_BUFFER_LIMIT;
 }
 
-int hip_fail(hipError_t e, const char *what, uint64_t attempted = 0) {
+int hip_fail(hipError_t e, const char *what, uint64_t attempted) {
     if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) {
         (void)hipGetLastError();  // clear the sticky allocation error
         return fail_limit(attempted, std::string("device allocation failed: ") + what);
@@ -88,13 +81,6 @@ int hip_fail(hipError_t e, const char *what, uint64_t attempted = 0) {
 // (src/chunking.rs:1266-1297) on the GPU (cg_selftest, run lazily on first use), unless
 // CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR=1 -- the test / bench opt-in -- is set.
 // ---------------------------------------------------------------------------
-struct Tables {
-    uint64_t gear[256];
-    uint64_t masks[26];
-    uint64_t epoch;
-    bool placeholder;
-};
-
 std::mutex g_tab_mu;
 std::shared_ptr<const Tables> g_tab;
 std::atomic<uint64_t> g_tab_epoch{1};
@@ -118,87 +104,7 @@ bool allow_unverified_tables() {
     return v && v[0] == '1' && v[1] == 0;
 }
 
-#define HIP_TRY(expr)                                   \
-    do {                                                \
-        hipError_t _e = (expr);                         \
-        if (_e != hipSuccess) return hip_fail(_e, #expr); \
-    } while (0)
-
 uint32_t logarithm2(uint32_t v) { return (uint32_t)std::round(std::log2((double)v)); }
-
-struct DevBuf {
-    void *p = nullptr;
-    size_t cap = 0;
-    int ensure(size_t bytes, const char *name) {
-        if (bytes <= cap) return CG_OK;
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-        size_t want = bytes + bytes / 4 + 256;
-        hipError_t e = hipMalloc(&p, want);
-        if (e != hipSuccess) {
-            p = nullptr;
-            return hip_fail(e, name, want);
-        }
-        cap = want;
-        return CG_OK;
-    }
-    template <class T>
-    T *as() const { return static_cast<T *>(p); }
-    void release() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-    }
-};
-
-struct PinBuf {
-    void *p = nullptr;
-    size_t cap = 0;
-    int ensure(size_t bytes) {
-        if (bytes <= cap) return CG_OK;
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        cap = 0;
-        size_t want = bytes + bytes / 4 + 256;
-        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
-        if (e != hipSuccess) {
-            p = nullptr;
-            return hip_fail(e, "hipHostMalloc", want);
-        }
-        cap = want;
-        return CG_OK;
-    }
-    template <class T>
-    T *as() const { return static_cast<T *>(p); }
-};
-
-enum { EV_START, EV_SCAN, EV_COMPACT, EV_WALK, EV_ASSEMBLE, EV_DIGEST, EV_N };
-
-struct Workspace {
-    int device = -1;
-    hipStream_t stream = nullptr;
-    uint64_t gear_epoch = 0;
-    DevBuf gear, seg_count, seg_cand, eoff, scan_tmp, entries, nar_off, cap_base, wchunk, nar_nchunks, nar_first,
-        chunk_abs, b3_gcount, b3_gbase, b3_gcv, b3_gmap, in, out, span_off, span_len, order, cas_order, ids,
-        man_abs, man_desc, sha_err;
-    PinBuf stage, err_stage;
-    hipEvent_t ev[EV_N] = {};
-    // CAS ids run on side_stream, concurrently with the digest: both stages are bound by
-    // their longest chunk's serial chain, not by the chip, so they overlap for free.
-    hipStream_t side_stream = nullptr;
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_cas = nullptr;
-    int init(int dev) {
-        device = dev;
-        HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-        HIP_TRY(hipStreamCreateWithFlags(&side_stream, hipStreamNonBlocking));
-        for (auto &e : ev) HIP_TRY(hipEventCreate(&e));
-        HIP_TRY(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
-        HIP_TRY(hipEventCreate(&ev_cas));
-        return CG_OK;
-    }
-};
 
 struct DevicePool {
     std::mutex mu;
@@ -245,13 +151,6 @@ void release(Workspace *ws) {
     pool.free_list.push_back(ws);
 }
 
-struct WsGuard {
-    Workspace *ws;
-    ~WsGuard() {
-        if (ws) release(ws);
-    }
-};
-
 // Upload the snapshot's GEAR table to this workspace (once per table epoch).
 int ensure_gear(Workspace *ws, const Tables &t) {
     if (ws->gear_epoch == t.epoch && ws->gear.p) return CG_OK;
@@ -261,10 +160,6 @@ int ensure_gear(Workspace *ws, const Tables &t) {
     ws->gear_epoch = t.epoch;
     return CG_OK;
 }
-
-struct Opts {
-    uint64_t min, avg, max;
-};
 
 // The SHA-256 kernel's spin-guard word (launch_sha256 d_err): zeroed before a digest
 // launch, copied back with the call's other results, checked after the stream sync.
@@ -346,7 +241,7 @@ uint32_t seg_slots(const CdcParams &p) {
 // stage forks onto ws->side_stream after descriptor assembly and joins before return.
 int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, size_t n_nars, const Opts &o,
               int algo, cg_desc *d_out, size_t out_cap, uint64_t *h_nar_first, hipStream_t st,
-              uint8_t *d_chunk_ids = nullptr, uint8_t *h_manifest_ids = nullptr, bool digest = true) {
+              uint8_t *d_chunk_ids, uint8_t *h_manifest_ids, bool digest) {
     if (algo != CG_BLAKE3 && algo != CG_SHA256) return fail(CG_E_INVALID_OPTIONS, "unknown hash algorithm");
     if (((uintptr_t)d_data & 15u) != 0) return fail(CG_E_IO, "device input must be 16-byte aligned");
     int rc;
@@ -433,6 +328,7 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
         if ((rc = ws->man_abs.ensure((n_nars + 1) * 8, "manifest spans"))) return rc;
         if ((rc = ws->man_desc.ensure((n_nars + 2) * sizeof(cg_desc), "manifest spans"))) return rc;
         d_man = ws->ids.as<uint8_t>();
+        if ((rc = ws->ensure_side_stream())) return rc;
         hipStream_t side = ws->side_stream;
         HIP_TRY(hipEventRecord(ws->ev_fork, st));
         HIP_TRY(hipStreamWaitEvent(side, ws->ev_fork, 0));
@@ -663,7 +559,9 @@ int check_kind(uint32_t kind) {
     return CG_OK;
 }
 
-}  // namespace
+}  // namespace cgrt
+
+using namespace cgrt;
 
 // ---------------------------------------------------------------------------
 // PushChunker (src/chunking.rs:753-829) over drain_finalized_chunks (:541-673)
@@ -692,7 +590,7 @@ struct cg_push {
     }
 };
 
-namespace {
+namespace cgrt {
 
 // drain_finalized_chunks (src/chunking.rs:541-673) on the GPU.  The retained buffer
 // is staged once; boundaries for all of it come from the device pipeline (the
@@ -815,7 +713,7 @@ int push_append(cg_push *h, const uint8_t *data, uint64_t len) {
     return CG_OK;
 }
 
-}  // namespace
+}  // namespace cgrt
 
 extern "C" {
 

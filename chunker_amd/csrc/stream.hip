@@ -1,0 +1,359 @@
+// stream.hip -- pipelined stream handle (cg_stream_*): ChunkStream (src/chunking.rs:675-740)
+// over drain_finalized_chunks (:541-673) with many read slices in flight.
+//
+// A SHA-256 / BLAKE3 digest costs one serial chain per chunk (~60 ms for a 4 MiB
+// chunk on the GPU), so a stream that waits for each slice's digests
+// (cg_push_*) runs at slice / 60 ms.  This handle instead keeps the stream's bytes in
+// an HBM arena of slots and separates two pipelines:
+//   * boundaries, synchronous per pushed slice, on the handle's workspace stream: the
+//     slice is copied H2D behind the retained tail (in the slot that holds it), the
+//     scan / walk find every cut of [tail, slice), the host applies the reference's
+//     retain rule (:579-584), and the retained tail moves D2D to the next slot;
+//   * digests, asynchronous: final chunks accumulate in an open group; a group of
+//     >= group_bytes is launched on one of a few digest streams and completes later.
+// Chunks come out of cg_stream_take strictly in stream order, with the exact
+// (offset, length, hash) the reference's ChunkStream / PushChunker yields.  Memory is
+// bounded by the arena (slots are reused only after every group reading them has
+// completed); when no slot is free a push waits for the oldest group.
+#include <algorithm>
+#include <cstring>
+#include <deque>
+
+#include "runtime.h"
+
+namespace cgrt {
+
+// One digest launch in flight: device scratch, pinned staging and its own stream.
+struct Lane {
+    hipStream_t st = nullptr;
+    hipEvent_t done = nullptr;
+    DevBuf desc, abs, total, order, err, b3_gcount, b3_gbase, b3_gcv, b3_gmap, scan_tmp;
+    PinBuf stage;  // [descs | abs | total | err]
+    bool busy = false;
+    int init() {
+        HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreateWithFlags(&done, hipEventDisableTiming));
+        return CG_OK;
+    }
+    void destroy() {
+        if (st) (void)hipStreamSynchronize(st);
+        for (DevBuf *b : {&desc, &abs, &total, &order, &err, &b3_gcount, &b3_gbase, &b3_gcv, &b3_gmap, &scan_tmp})
+            b->release();
+        if (stage.p) (void)hipHostFree(stage.p);
+        if (done) (void)hipEventDestroy(done);
+        if (st) (void)hipStreamDestroy(st);
+    }
+};
+
+// The final chunks of a run of consecutive slots [slot_lo, slot_hi], one digest launch.
+struct Group {
+    std::vector<cg_desc> desc;  // offsets are stream offsets (ChunkMetadata::offset)
+    std::vector<uint64_t> abs;  // arena offsets of the same chunks
+    uint64_t slot_lo = 0, slot_hi = 0, bytes = 0;
+    int lane = -1;
+};
+
+}  // namespace cgrt
+
+using namespace cgrt;
+
+struct cg_stream {
+    Opts o;
+    int algo = CG_SHA256;
+    int device = -1;
+    Workspace *ws = nullptr;  // boundary pipeline, held for the handle's lifetime
+    DevBuf arena;
+    uint64_t slot_bytes = 0, nslots = 0, group_bytes = 0;
+    uint64_t cur = 0;       // sequence number of the slot holding the retained tail
+    uint64_t tail = 0;      // retained bytes at the start of slot `cur`
+    uint64_t position = 0;  // stream offset of slot `cur`'s first byte
+    uint64_t pushed = 0;
+    bool finished = false;
+    Group open;
+    std::deque<Group> inflight;
+    std::deque<cg_desc> ready;
+    std::vector<Lane> lanes;
+    std::vector<cg_desc> scratch;  // boundary descriptors of the current slot
+    hipEvent_t ev_bytes = nullptr;  // boundary stream position a digest launch must wait for
+    ~cg_stream() {
+        if (device < 0) return;
+        int prev = 0;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(device);
+        for (Lane &l : lanes) l.destroy();
+        if (ws) {
+            (void)hipStreamSynchronize(ws->stream);
+            release(ws);
+        }
+        if (ev_bytes) (void)hipEventDestroy(ev_bytes);
+        arena.release();
+        (void)hipSetDevice(prev);
+    }
+};
+
+namespace cgrt {
+
+uint8_t *slot_ptr(cg_stream *h, uint64_t seq) { return h->arena.as<uint8_t>() + (seq % h->nslots) * h->slot_bytes; }
+uint64_t slot_off(const cg_stream *h, uint64_t seq) { return (seq % h->nslots) * h->slot_bytes; }
+
+// Wait for the oldest launched group, check it, and move its chunks (now with digests)
+// to the ready queue.
+int complete_oldest(cg_stream *h) {
+    Group &g = h->inflight.front();
+    Lane &l = h->lanes[g.lane];
+    HIP_TRY(hipEventSynchronize(l.done));
+    const size_t n = g.desc.size();
+    const uint8_t *st = l.stage.as<uint8_t>();
+    const uint32_t err = *reinterpret_cast<const uint32_t *>(st + n * sizeof(cg_desc) + n * 8 + 8);
+    l.busy = false;
+    if (err)
+        return fail(CG_E_IO, "stream digest: a producer/consumer hand-off hit the SHA-256 kernel's spin guard");
+    const cg_desc *res = reinterpret_cast<const cg_desc *>(st);
+    for (size_t k = 0; k < n; ++k) {
+        cg_desc d = g.desc[k];
+        memcpy(d.hash, res[k].hash, 32);
+        h->ready.push_back(d);
+    }
+    h->inflight.pop_front();
+    return CG_OK;
+}
+
+// Launch the open group's digests on a free lane (waiting for the oldest group if none).
+int launch_open(cg_stream *h) {
+    if (h->open.desc.empty()) return CG_OK;
+    int rc;
+    int li = -1;
+    for (;;) {
+        for (size_t i = 0; i < h->lanes.size(); ++i)
+            if (!h->lanes[i].busy) li = (int)i;
+        if (li >= 0) break;
+        if ((rc = complete_oldest(h))) return rc;
+    }
+    Lane &l = h->lanes[li];
+    Group g = std::move(h->open);
+    h->open = Group();
+    const size_t n = g.desc.size();
+    const size_t nd = n * sizeof(cg_desc);
+    if ((rc = l.stage.ensure(nd + n * 8 + 16))) return rc;
+    uint8_t *stg = l.stage.as<uint8_t>();
+    memcpy(stg, g.desc.data(), nd);  // the kernels read lengths here and chunk bytes at arena + abs
+    memcpy(stg + nd, g.abs.data(), n * 8);
+    *reinterpret_cast<uint64_t *>(stg + nd + n * 8) = n;
+    *reinterpret_cast<uint32_t *>(stg + nd + n * 8 + 8) = 0;
+    if ((rc = l.desc.ensure(nd + 64, "stream descriptors"))) return rc;
+    if ((rc = l.abs.ensure(n * 8 + 64, "stream offsets"))) return rc;
+    if ((rc = l.total.ensure(64, "stream total"))) return rc;
+    if ((rc = l.err.ensure(64, "stream err"))) return rc;
+    // the chunk bytes were written (H2D, tail moves) on the boundary stream
+    HIP_TRY(hipEventRecord(h->ev_bytes, h->ws->stream));
+    HIP_TRY(hipStreamWaitEvent(l.st, h->ev_bytes, 0));
+    HIP_TRY(hipMemcpyAsync(l.desc.p, stg, nd, hipMemcpyHostToDevice, l.st));
+    HIP_TRY(hipMemcpyAsync(l.abs.p, stg + nd, n * 8, hipMemcpyHostToDevice, l.st));
+    HIP_TRY(hipMemcpyAsync(l.total.p, stg + nd + n * 8, 8, hipMemcpyHostToDevice, l.st));
+    HIP_TRY(hipMemsetAsync(l.err.p, 0, 4, l.st));
+    uint8_t *hb = l.desc.as<uint8_t>() + offsetof(cg_desc, hash);
+    const uint8_t *base = h->arena.as<uint8_t>();
+    const uint64_t *d_total = l.total.as<uint64_t>();
+    if (h->algo == CG_SHA256) {
+        if ((rc = l.order.ensure(cg::sha256_order_tmp_elems(n) * 4, "order"))) return rc;
+        cg::launch_sha256(base, l.abs.as<uint64_t>(), l.desc.p, d_total, n, n, h->o.max, l.order.as<uint32_t>(), hb,
+                          sizeof(cg_desc), l.err.as<uint32_t>(), l.st);
+    } else {
+        const uint64_t gb = cg::blake3_group_bound(g.bytes, n);
+        if ((rc = l.b3_gcount.ensure((n + 1) * 4, "b3_gcount"))) return rc;
+        if ((rc = l.b3_gbase.ensure((n + 1) * 8, "b3_gbase"))) return rc;
+        if ((rc = l.b3_gcv.ensure((gb + 1) * 32, "b3_gcv"))) return rc;
+        if ((rc = l.b3_gmap.ensure((gb + 1) * 4, "b3_gmap"))) return rc;
+        if ((rc = l.scan_tmp.ensure(cg::exclusive_scan_tmp_elems(n) * 8 + 64, "scan_tmp"))) return rc;
+        cg::launch_blake3(base, l.abs.as<uint64_t>(), l.desc.p, d_total, n, g.bytes, hb, sizeof(cg_desc),
+                          l.b3_gmap.as<uint32_t>(), l.b3_gbase.as<uint64_t>(), l.b3_gcount.as<uint32_t>(),
+                          l.scan_tmp.as<uint64_t>(), l.b3_gcv.as<uint32_t>(), l.st);
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(stg, l.desc.p, nd, hipMemcpyDeviceToHost, l.st));
+    HIP_TRY(hipMemcpyAsync(stg + nd + n * 8 + 8, l.err.p, 4, hipMemcpyDeviceToHost, l.st));
+    HIP_TRY(hipEventRecord(l.done, l.st));
+    l.busy = true;
+    g.lane = li;
+    h->inflight.push_back(std::move(g));
+    return CG_OK;
+}
+
+// Make slot `seq` writable: every group reading its previous tenant (seq - nslots) done.
+int free_slot(cg_stream *h, uint64_t seq) {
+    int rc;
+    for (;;) {
+        const uint64_t oldest = !h->inflight.empty() ? h->inflight.front().slot_lo
+                                : !h->open.desc.empty() ? h->open.slot_lo
+                                                        : h->cur;
+        if (seq < oldest + h->nslots) return CG_OK;
+        if (h->inflight.empty()) {
+            if ((rc = launch_open(h))) return rc;
+        } else if ((rc = complete_oldest(h))) {
+            return rc;
+        }
+    }
+}
+
+// drain_finalized_chunks over slot `cur` = [tail | `len` new bytes already copied in].
+int stream_drain(cg_stream *h, uint64_t len, bool eof) {
+    int rc;
+    const uint64_t buf = h->tail + len;
+    if (buf == 0 || (buf < h->o.min && !eof)) {
+        h->tail = buf;
+        return CG_OK;
+    }
+    Workspace *ws = h->ws;
+    const uint64_t cap = capacity_of(buf, h->o.min);
+    if ((rc = ws->out.ensure((cap + 1) * sizeof(cg_desc), "descriptors"))) return rc;
+    uint64_t offs[2] = {0, buf}, first[2] = {0, 0};
+    if ((rc = run_batch(ws, slot_ptr(h, h->cur), offs, 1, h->o, h->algo, ws->out.as<cg_desc>(), cap, first,
+                        ws->stream, nullptr, nullptr, /*digest=*/false)))
+        return rc;
+    const uint64_t total = first[1];
+    h->scratch.resize(total);
+    if (total) {
+        HIP_TRY(hipMemcpyAsync(h->scratch.data(), ws->out.p, total * sizeof(cg_desc), hipMemcpyDeviceToHost,
+                               ws->stream));
+        HIP_TRY(hipStreamSynchronize(ws->stream));
+    }
+    uint64_t consumed = 0;
+    const uint64_t base = slot_off(h, h->cur);
+    for (uint64_t k = 0; k < total; ++k) {
+        const cg_desc &d = h->scratch[k];
+        if (d.length == 0) return fail(CG_E_ZERO_LENGTH_CHUNK, "FastCDC returned a chunk with length 0");
+        if (d.offset + d.length == buf && !eof && d.length < h->o.max) break;  // retained tail (:579-584)
+        if (h->open.desc.empty()) h->open.slot_lo = h->cur;
+        h->open.slot_hi = h->cur;
+        cg_desc c{};
+        c.offset = h->position + d.offset;
+        c.length = d.length;
+        h->open.desc.push_back(c);
+        h->open.abs.push_back(base + d.offset);
+        h->open.bytes += d.length;
+        consumed += d.length;
+    }
+    if (eof && consumed < buf) return fail(CG_E_IO, "stream: chunks do not cover the buffer at finish");
+    const uint64_t rest = buf - consumed;
+    if (consumed) {  // the chunks emitted from this slot stay put; the next slice goes to the next slot
+        if ((rc = free_slot(h, h->cur + 1))) return rc;
+        if (rest)  // the retained tail moves to the front of that slot
+            HIP_TRY(hipMemcpyAsync(slot_ptr(h, h->cur + 1), slot_ptr(h, h->cur) + consumed, rest,
+                                   hipMemcpyDeviceToDevice, ws->stream));
+        h->cur += 1;
+    }
+    h->position += consumed;
+    h->tail = rest;
+    if (h->open.bytes >= h->group_bytes) return launch_open(h);
+    return CG_OK;
+}
+
+}  // namespace cgrt
+
+extern "C" {
+
+cg_stream *cg_stream_new(uint64_t min_size, uint64_t avg_size, uint64_t max_size, int algo, uint64_t slice_bytes,
+                         uint64_t inflight_bytes, int *status) {
+    clear_error();
+    Opts o;
+    int rc = resolve(min_size, avg_size, max_size, &o, nullptr, 0);
+    if (!rc && algo != CG_BLAKE3 && algo != CG_SHA256) rc = fail(CG_E_INVALID_OPTIONS, "unknown hash algorithm");
+    if (!rc) rc = check_tables();
+    int dev = 0;
+    if (!rc) rc = current_device(&dev);
+    if (rc) {
+        if (status) *status = rc;
+        return nullptr;
+    }
+    cg_stream *h = new cg_stream();
+    h->o = o;
+    h->algo = algo;
+    h->device = dev;
+    // slot = the largest retained tail (< max) + one slice; groups of ~1/4 of the arena
+    const uint64_t slice = std::max<uint64_t>(slice_bytes ? slice_bytes : 8ull << 20, 4096);
+    h->slot_bytes = (o.max + slice + 256 + 255) & ~255ull;
+    const uint64_t budget = inflight_bytes ? inflight_bytes : 512ull << 20;
+    h->nslots = std::max<uint64_t>(budget / h->slot_bytes, 4);
+    h->group_bytes = std::max<uint64_t>(h->nslots * h->slot_bytes / 4, slice);
+    const int nlanes = 3;
+    if (!(rc = acquire(&h->ws)) && !(rc = h->arena.ensure(h->nslots * h->slot_bytes, "stream arena"))) {
+        const hipError_t e = hipEventCreateWithFlags(&h->ev_bytes, hipEventDisableTiming);
+        if (e != hipSuccess) rc = hip_fail(e, "hipEventCreate");
+    }
+    h->lanes.resize(nlanes);
+    for (int i = 0; !rc && i < nlanes; ++i) rc = h->lanes[i].init();
+    if (rc) {
+        delete h;
+        if (status) *status = rc;
+        return nullptr;
+    }
+    if (status) *status = CG_OK;
+    return h;
+}
+
+int cg_stream_push(cg_stream *h, const uint8_t *data, uint64_t len) {
+    clear_error();
+    if (!h) return fail(CG_E_IO, "null stream handle");
+    if (h->finished) return fail(CG_E_INVALID_OPTIONS, "push called after finish");
+    int rc = check_tables();
+    if (rc) return rc;
+    while (len) {  // a slice larger than a slot goes in slot-sized pieces (chunks do not depend on slicing)
+        const uint64_t room = h->slot_bytes - 256 - h->tail;
+        const uint64_t take = std::min(len, room);
+        HIP_TRY(hipMemcpyAsync(slot_ptr(h, h->cur) + h->tail, data, take, hipMemcpyHostToDevice, h->ws->stream));
+        if ((rc = stream_drain(h, take, false))) return rc;
+        h->pushed += take;
+        data += take;
+        len -= take;
+    }
+    return CG_OK;
+}
+
+int cg_stream_finish(cg_stream *h) {
+    clear_error();
+    if (!h) return fail(CG_E_IO, "null stream handle");
+    if (h->finished) return CG_OK;
+    int rc = check_tables();
+    if (rc) return rc;
+    h->finished = true;
+    if ((rc = stream_drain(h, 0, true))) return rc;
+    return launch_open(h);
+}
+
+int cg_stream_take(cg_stream *h, cg_desc *out, size_t out_cap, size_t *n_out, int wait) {
+    clear_error();
+    if (n_out) *n_out = 0;
+    if (!h) return fail(CG_E_IO, "null stream handle");
+    int rc;
+    while (h->ready.empty()) {
+        if (!h->inflight.empty()) {
+            const Lane &l = h->lanes[h->inflight.front().lane];
+            if (!wait && hipEventQuery(l.done) == hipErrorNotReady) break;
+            if ((rc = complete_oldest(h))) return rc;
+        } else if (wait && !h->open.desc.empty()) {
+            if ((rc = launch_open(h))) return rc;
+        } else {
+            break;
+        }
+    }
+    size_t n = 0;
+    while (n < out_cap && !h->ready.empty()) {
+        out[n++] = h->ready.front();
+        h->ready.pop_front();
+    }
+    if (n_out) *n_out = n;
+    return CG_OK;
+}
+
+uint64_t cg_stream_pending(const cg_stream *h) {
+    if (!h) return 0;
+    uint64_t n = h->ready.size() + h->open.desc.size();
+    for (const Group &g : h->inflight) n += g.desc.size();
+    return n;
+}
+
+uint64_t cg_stream_bytes_consumed(const cg_stream *h) { return h ? h->pushed : 0; }
+
+void cg_stream_free(cg_stream *h) { delete h; }
+
+}  // extern "C"

@@ -108,6 +108,28 @@ uint64_t cg_push_bytes_consumed(const cg_push *h); /* PushChunker::bytes_consume
 size_t cg_push_out_capacity(const cg_push *h, uint64_t next_len);
 void cg_push_free(cg_push *h);
 
+/* Pipelined stream: ChunkStream::next (src/chunking.rs:675-740) over
+ * drain_finalized_chunks (:541-673) with many read slices in flight.  Each push finds
+ * the slice's cut points at once (the reference's retain rule, :579-584), but the
+ * chunks' digests run asynchronously, grouped over several slices; cg_stream_take
+ * returns finished chunks strictly in stream order (offsets are stream offsets), with
+ * exactly the (offset, length, hash) ChunkStream / PushChunker yields.  Device memory
+ * is bounded by `inflight_bytes` (0 = 512 MiB): an arena of slots of max_size +
+ * slice_bytes (0 = 8 MiB, the reference's read size, :713-716) bytes, each reused only
+ * after the digests reading it completed -- a push waits for them when none is free.
+ * take with wait = 0 returns what has completed; wait != 0 blocks until at least one
+ * chunk is ready or nothing is pending.  push after finish -> CG_E_INVALID_OPTIONS.
+ * Single owner, like cg_push. */
+typedef struct cg_stream cg_stream;
+cg_stream *cg_stream_new(uint64_t min_size, uint64_t avg_size, uint64_t max_size, int algo, uint64_t slice_bytes,
+                         uint64_t inflight_bytes, int *status);
+int cg_stream_push(cg_stream *h, const uint8_t *data, uint64_t len);
+int cg_stream_finish(cg_stream *h);
+int cg_stream_take(cg_stream *h, cg_desc *out, size_t out_cap, size_t *n_out, int wait);
+uint64_t cg_stream_pending(const cg_stream *h);       /* chunks found but not yet taken */
+uint64_t cg_stream_bytes_consumed(const cg_stream *h); /* bytes pushed so far */
+void cg_stream_free(cg_stream *h);
+
 /* Digest-only entry (sha256_hash_raw src/hashing.rs:36-44 / blake3::hash) over n
  * device-resident spans; d_digests receives n*32 bytes. */
 int cg_hash_spans_device(const uint8_t *d_data, const uint64_t *d_offsets, const uint64_t *d_lengths, size_t n,

@@ -528,6 +528,7 @@ typedef struct {
     uint64_t mn, avg, mx;
     int algo;
     int finished;
+    int nthreads; /* digest pool when a drain emits > 4 chunks (rayon par_iter, src/chunking.rs:637-641) */
 } or_push;
 
 or_push *or_push_new(uint64_t mn, uint64_t avg, uint64_t mx, int algo, int *status) {
@@ -539,8 +540,11 @@ or_push *or_push_new(uint64_t mn, uint64_t avg, uint64_t mx, int algo, int *stat
     h->avg = avg;
     h->mx = mx;
     h->algo = algo;
+    h->nthreads = 1;
     return h;
 }
+
+void or_push_set_threads(or_push *h, int nthreads) { h->nthreads = nthreads > 0 ? nthreads : 1; }
 
 void or_push_free(or_push *h) {
     if (!h) return;
@@ -570,8 +574,11 @@ static int drain(or_push *h, int eof, or_desc *out, size_t cap, size_t *n_out) {
         }
         total = processed;
     }
-    for (size_t i = 0; i < n; i++)
-        compute_hash(h->buf + (out[i].offset - h->position), out[i].length, h->algo, out[i].hash);
+    if (n > 4 && h->nthreads > 1) /* offsets are stream offsets: rebase the buffer pointer */
+        or_hash_descs(h->buf - h->position, out, n, h->algo, h->nthreads);
+    else
+        for (size_t i = 0; i < n; i++)
+            compute_hash(h->buf + (out[i].offset - h->position), out[i].length, h->algo, out[i].hash);
     memmove(h->buf, h->buf + total, h->len - total);
     h->len -= total;
     h->position += total;

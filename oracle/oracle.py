@@ -82,6 +82,7 @@ def lib() -> ctypes.CDLL:
         L.or_push_push.restype = ctypes.c_int
         L.or_push_finish.argtypes = [p, p, sz, ctypes.POINTER(sz)]
         L.or_push_finish.restype = ctypes.c_int
+        L.or_push_set_threads.argtypes = [p, ctypes.c_int]
         L.or_push_bytes_consumed.argtypes = [p]
         L.or_push_bytes_consumed.restype = u64
         L.or_set_tables(GEAR.ctypes.data, MASKS.ctypes.data)
@@ -218,7 +219,7 @@ def node_put(data, mn=None, avg=None, mx=None, nthreads: int = 1):
 class Push:
     """PushChunker (src/chunking.rs:753-829) over drain_finalized_chunks (:541-673)."""
 
-    def __init__(self, mn=None, avg=None, mx=None, algo=SHA256):
+    def __init__(self, mn=None, avg=None, mx=None, algo=SHA256, nthreads=1):
         self.mn = 256 * 1024 if mn is None else mn
         self.avg = 1024 * 1024 if avg is None else avg
         self.mx = 4 * 1024 * 1024 if mx is None else mx
@@ -226,6 +227,7 @@ class Push:
         self.h = lib().or_push_new(self.mn, self.avg, self.mx, algo, ctypes.byref(st))
         if not self.h:
             raise ValueError(validate(self.mn, self.avg, self.mx)[1])
+        lib().or_push_set_threads(self.h, nthreads)
         self._cap_bytes = 0
 
     def _out(self, extra: int):

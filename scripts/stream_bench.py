@@ -1,88 +1,104 @@
-"""Streaming rates: one 1 GiB xorshift stream from host
-memory through ChunkStream (reader slices) and PushChunker (caller slices, the NIF's
-pattern), SHA-256, default params.  Reported per slice size; the GPU ChunkStream default
-is the 256 MiB slice (chunking.stream_read_size).  CPU: the oracle's PushChunker
-restatement (serial scan + serial SHA-NI, one thread) on a 256 MiB sample, 8 MiB pushes."""
+"""Streaming rates: one 1 GiB synthetic NAR stream from
+host memory, SHA-256, default params (256K/1M/4M), at the reference's read size
+(8 MiB, src/chunking.rs:713-716 with the default cap :417).
+
+* ChunkStream: the pipelined engine stream (cg_stream_*) behind the Python mirror
+  (payload objects included), for several in-flight HBM budgets;
+* engine_stream: cg_stream_push / cg_stream_take alone (descriptors only: what a Rust
+  caller pays before its zero-copy split_to);
+* engine_push: the synchronous PushChunker handle (cg_push_*), one round trip per slice;
+* cpu_push: the oracle's PushChunker restatement (serial FastCDC, SHA-NI, digests on a
+  16-thread pool when a drain emits > 4 chunks, as the reference's par_iter does,
+  src/chunking.rs:637-641), 8 MiB pushes, over the same 1 GiB.
+Every GPU variant is checked chunk for chunk against the eager result."""
 import os
 os.environ.setdefault("CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR", "1")  # placeholder GEAR: see tables/README.md
-import io
-import json
-import os
-import sys
-import time
+os.environ.pop("CHUNKER_READ_SLICE_CAP_BYTES", None)  # the reference's default sizing
+import ctypes  # noqa: E402
+import io  # noqa: E402
+import json  # noqa: E402
+import sys  # noqa: E402
+import time  # noqa: E402
 
-import numpy as np
+import numpy as np  # noqa: E402
 
 sys.path.insert(0, ".")
 import chunker_amd as ca  # noqa: E402
+from chunker_amd._lib import DESC_DTYPE, lib  # noqa: E402
 from chunker_amd.nar import synth_nars  # noqa: E402
 
 N = 1 << 30
+SL = 8 << 20
 data, _ = synth_nars([N])
 raw = data.tobytes()
-res = {"workload": "1 GiB synthetic NAR stream, SHA-256, 256K/1M/4M"}
-ref = None
-# ChunkStream: the reference's sizing with its 8 MiB default cap (env pinned), then the
-# GPU default (env unset: 256 MiB slices, chunking.stream_read_size)
-for cap in (8 << 20, None):
-    if cap:
-        os.environ["CHUNKER_READ_SLICE_CAP_BYTES"] = str(cap)
-    else:
-        os.environ.pop("CHUNKER_READ_SLICE_CAP_BYTES", None)
-    rs = ca.chunking.stream_read_size(4 << 20)
-    t0 = time.perf_counter()
-    chunks = ca.chunk_stream(io.BytesIO(raw))
-    dt = time.perf_counter() - t0
-    key = [(c.offset, c.length, c.hash) for c in chunks]
-    ref = ref or key
-    assert key == ref
-    res[f"stream_read_{rs >> 20}MiB"] = {"GiB_per_s": round(N / dt / 2**30, 3), "s": round(dt, 3),
-                                          "chunks": len(chunks)}
-for sl in (8 << 20, 64 << 20, 256 << 20):
-    p = ca.PushChunker()
-    t0 = time.perf_counter()
-    out = []
-    for i in range(0, N, sl):
-        out += p.push(raw[i:i + sl])
-    out += p.finish()
-    dt = time.perf_counter() - t0
-    assert [(c.offset, c.length, c.hash) for c in out] == ref
-    res[f"push_{sl >> 20}MiB"] = {"GiB_per_s": round(N / dt / 2**30, 3), "s": round(dt, 3)}
-# engine alone: cg_push_push on slices of one host array (descriptors only, no payload
-# objects) -- what a Rust caller pays before its zero-copy split_to
-import ctypes  # noqa: E402
+res = {"workload": "1 GiB synthetic NAR stream, SHA-256, 256K/1M/4M, 8 MiB reads"}
+eager = ca.chunk_descriptors_array(data)
+ref = [(int(d["offset"]), int(d["length"]), bytes(d["hash"])) for d in eager]
+res["chunks"] = len(ref)
 
-from chunker_amd._lib import DESC_DTYPE, lib  # noqa: E402
 
-for sl in (8 << 20, 64 << 20, 256 << 20):
+def key(chunks):
+    return [(c.offset, c.length, c.hash) for c in chunks]
+
+
+for inflight in (256 << 20, 512 << 20, 1 << 30):
+    os.environ["CHUNKER_AMD_STREAM_INFLIGHT_BYTES"] = str(inflight)
+    list(ca.ChunkStream(io.BytesIO(raw[: 64 << 20])))  # warm (allocations)
+    t0 = time.perf_counter()
+    chunks = list(ca.ChunkStream(io.BytesIO(raw)))
+    dt = time.perf_counter() - t0
+    assert key(chunks) == ref
+    res[f"ChunkStream_inflight_{inflight >> 20}MiB"] = {"GiB_per_s": round(N / dt / 2**30, 3), "s": round(dt, 3)}
+    del chunks
+
+for inflight in (256 << 20, 512 << 20, 1 << 30):
     st = ctypes.c_int(0)
-    h = lib.cg_push_new(256 << 10, 1 << 20, 4 << 20, 1, ctypes.byref(st))
-    out = np.zeros(4096, DESC_DTYPE)
+    h = lib.cg_stream_new(256 << 10, 1 << 20, 4 << 20, 1, SL, inflight, ctypes.byref(st))
+    out = np.zeros(8192, DESC_DTYPE)
     n = ctypes.c_size_t(0)
     got = []
     t0 = time.perf_counter()
-    for i in range(0, N, sl):
-        assert lib.cg_push_push(h, data.ctypes.data + i, min(sl, N - i), out.ctypes.data, len(out), ctypes.byref(n)) == 0
-        got.append(out[:n.value].copy())
-    assert lib.cg_push_finish(h, out.ctypes.data, len(out), ctypes.byref(n)) == 0
-    got.append(out[:n.value].copy())
+    for i in range(0, N, SL):
+        assert lib.cg_stream_push(h, data.ctypes.data + i, min(SL, N - i)) == 0
+        assert lib.cg_stream_take(h, out.ctypes.data, len(out), ctypes.byref(n), 0) == 0
+        got.append(out[: n.value].copy())
+    assert lib.cg_stream_finish(h) == 0
+    while True:
+        assert lib.cg_stream_take(h, out.ctypes.data, len(out), ctypes.byref(n), 1) == 0
+        if not n.value:
+            break
+        got.append(out[: n.value].copy())
     dt = time.perf_counter() - t0
-    lib.cg_push_free(h)
+    lib.cg_stream_free(h)
     g = np.concatenate(got)
     assert [(int(x["offset"]), int(x["length"]), bytes(x["hash"])) for x in g] == ref
-    res[f"engine_push_{sl >> 20}MiB"] = {"GiB_per_s": round(N / dt / 2**30, 3), "s": round(dt, 3),
-                                          "ms_per_push": round(dt * 1e3 / (N // sl + 1), 2)}
-eager = ca.chunk_data(raw)
-assert [(c.offset, c.length, c.hash) for c in eager] == ref
+    res[f"engine_stream_inflight_{inflight >> 20}MiB"] = {"GiB_per_s": round(N / dt / 2**30, 3), "s": round(dt, 3)}
+
+st = ctypes.c_int(0)
+h = lib.cg_push_new(256 << 10, 1 << 20, 4 << 20, 1, ctypes.byref(st))
+out = np.zeros(4096, DESC_DTYPE)
+n = ctypes.c_size_t(0)
+got = []
+M = 256 << 20  # the synchronous handle is slow: a 256 MiB prefix
+t0 = time.perf_counter()
+for i in range(0, M, SL):
+    assert lib.cg_push_push(h, data.ctypes.data + i, SL, out.ctypes.data, len(out), ctypes.byref(n)) == 0
+    got.append(out[:n.value].copy())
+dt = time.perf_counter() - t0
+lib.cg_push_free(h)
+res["engine_push_sync_8MiB"] = {"GiB_per_s": round(M / dt / 2**30, 3), "sample_bytes": M,
+                                "ms_per_push": round(dt * 1e3 / (M // SL), 2)}
+
 from oracle import oracle as O  # noqa: E402
 
-S = 256 << 20
-p = O.Push()
-t0 = time.perf_counter()
-n = 0
-for i in range(0, S, 8 << 20):
-    n += len(p.push(data[i:i + (8 << 20)]))
-n += len(p.finish())
-dt = time.perf_counter() - t0
-res["cpu_push_8MiB"] = {"GiB_per_s": round(S / dt / 2**30, 3), "sample_bytes": S, "threads": 1, "kind": "port"}
+for nt in (1, 16):
+    p = O.Push(nthreads=nt)
+    t0 = time.perf_counter()
+    cnt = 0
+    for i in range(0, N, SL):
+        cnt += len(p.push(data[i:i + SL]))
+    cnt += len(p.finish())
+    dt = time.perf_counter() - t0
+    assert cnt == len(ref)
+    res[f"cpu_push_8MiB_{nt}t"] = {"GiB_per_s": round(N / dt / 2**30, 3), "threads": nt, "kind": "port"}
 print(json.dumps(res))

@@ -117,6 +117,9 @@ def test_no_cpu_fallback_without_gpu(ca):
         ca.chunk_descriptors(b"hello world")
     with pytest.raises(ca.DeviceUnavailableError):
         ca.PushChunker().push(bytes(300_000))
+    import io
+    with pytest.raises(ca.DeviceUnavailableError):
+        ca.chunk_stream(io.BytesIO(bytes(300_000)))
 
 
 def test_gear_table_plumbing(ca):
@@ -207,16 +210,17 @@ def test_cas_entry_validation_without_gpu(ca):
 
 
 def test_stream_read_size(ca, monkeypatch):
-    """ChunkStream refill size: the reference's formula (src/chunking.rs:713-716) when
-    CHUNKER_READ_SLICE_CAP_BYTES pins the cap, else the GPU slice (256 MiB)."""
-    from chunker_amd.chunking import MAX_READ_SLICE_CAP, stream_read_size
+    """ChunkStream refill size is the reference's formula (src/chunking.rs:713-716):
+    max(min(max(max_size * 8, 4 MiB), cap), 4096), cap from CHUNKER_READ_SLICE_CAP_BYTES
+    in 4 KiB..256 MiB, default 8 MiB (:417-433)."""
+    from chunker_amd.chunking import stream_read_size
 
     monkeypatch.delenv("CHUNKER_READ_SLICE_CAP_BYTES", raising=False)
-    assert stream_read_size(4 << 20) == MAX_READ_SLICE_CAP
-    assert stream_read_size(64 << 20) == 512 << 20
-    monkeypatch.setenv("CHUNKER_READ_SLICE_CAP_BYTES", str(8 << 20))
     assert stream_read_size(4 << 20) == 8 << 20
-    assert stream_read_size(1024) == 4 << 20 if (4 << 20) <= (8 << 20) else True
+    assert stream_read_size(256 << 10) == 4 << 20
+    assert stream_read_size(1024) == 4 << 20
+    monkeypatch.setenv("CHUNKER_READ_SLICE_CAP_BYTES", str(64 << 20))
+    assert stream_read_size(4 << 20) == 32 << 20
     monkeypatch.setenv("CHUNKER_READ_SLICE_CAP_BYTES", "4096")
     assert stream_read_size(1 << 20) == 4096
     monkeypatch.setenv("CHUNKER_READ_SLICE_CAP_BYTES", "12")  # out of range -> 8 MiB default

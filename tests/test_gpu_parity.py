@@ -232,6 +232,63 @@ def test_stream_matches_in_memory(ca, params, seed, n):
     assert total == len(data)
 
 
+@pytest.mark.parametrize("algo", [SHA, B3], ids=["sha256", "blake3"])
+@pytest.mark.parametrize("cap,inflight", [(65_536, 1), (300_000, 2 << 20), (4 << 20, 64 << 20)],
+                         ids=["4slots", "wrap", "wide"])
+def test_pipelined_stream_many_slices(ca, O, monkeypatch, algo, cap, inflight):
+    """The pipelined ChunkStream (cg_stream_*) over many read slices: slots wrap around
+    the arena (inflight=1 -> the 4-slot minimum, so pushes wait for digests), groups
+    span slices, and every chunk equals the oracle's eager result, in order."""
+    monkeypatch.setenv("CHUNKER_READ_SLICE_CAP_BYTES", str(cap))
+    monkeypatch.setenv("CHUNKER_AMD_STREAM_INFLIGHT_BYTES", str(inflight))
+    data = rand_bytes(9_000_017, 77).tobytes()
+    params = (16_384, 65_536, 262_144)
+    got = list(ca.ChunkStream(io.BytesIO(data), *params, hash=algo))
+    ref = O.chunk_descriptors(data, *params, algo=algo, nthreads=8)
+    assert [(c.offset, c.length, c.hash) for c in got] == \
+        [(int(r["offset"]), int(r["length"]), bytes(r["hash"])) for r in ref]
+    assert b"".join(c.payload for c in got) == data
+
+
+def test_stream_abi_push_take_interleaved(ca, O):
+    """cg_stream_* directly: uneven pushes (empty, tiny, larger than a slot), takes with
+    wait = 0 between them, then finish + blocking takes; same chunks as the oracle."""
+    import ctypes
+
+    data = rand_bytes(5_000_000, 91).tobytes()
+    params = (8_192, 32_768, 131_072)
+    st = ctypes.c_int(0)
+    h = ca.lib.cg_stream_new(*params, SHA, 100_000, 1 << 20, ctypes.byref(st))
+    assert h and st.value == 0
+    out = np.zeros(64, ca.DESC_DTYPE)
+    n = ctypes.c_size_t(0)
+    got = []
+    steps = [0, 1, 7, 100_000, 999_999, 3, 250_000, 1_500_000]
+    pos, i = 0, 0
+    try:
+        while pos < len(data):
+            k = min(steps[i % len(steps)], len(data) - pos)
+            i += 1
+            buf = np.frombuffer(data[pos:pos + k], np.uint8) if k else np.zeros(1, np.uint8)
+            assert ca.lib.cg_stream_push(h, buf.ctypes.data, k) == 0
+            pos += k
+            assert ca.lib.cg_stream_take(h, out.ctypes.data, len(out), ctypes.byref(n), 0) == 0
+            got += [(int(d["offset"]), int(d["length"]), bytes(d["hash"])) for d in out[: n.value]]
+        assert ca.lib.cg_stream_bytes_consumed(h) == len(data)
+        assert ca.lib.cg_stream_finish(h) == 0
+        assert ca.lib.cg_stream_push(h, out.ctypes.data, 1) == 4  # push after finish
+        while True:
+            assert ca.lib.cg_stream_take(h, out.ctypes.data, len(out), ctypes.byref(n), 1) == 0
+            if n.value == 0:
+                break
+            got += [(int(d["offset"]), int(d["length"]), bytes(d["hash"])) for d in out[: n.value]]
+        assert ca.lib.cg_stream_pending(h) == 0
+    finally:
+        ca.lib.cg_stream_free(h)
+    ref = O.chunk_descriptors(data, *params, algo=SHA, nthreads=8)
+    assert got == [(int(r["offset"]), int(r["length"]), bytes(r["hash"])) for r in ref]
+
+
 def test_stream_small_read_cap(ca, monkeypatch):
     monkeypatch.setenv("CHUNKER_READ_SLICE_CAP_BYTES", "4096")
     data = (b"streaming chunker parity test" * 2048)

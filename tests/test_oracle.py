@@ -172,7 +172,7 @@ def test_push_restatement_matches_eager(slice_size):
     data = rng.integers(0, 256, 1_500_000, dtype=np.uint8).tobytes()
     params = (8_192, 32_768, 131_072)
     ref = O.chunk_descriptors(data, *params, algo=B3, nthreads=4)
-    p = O.Push(*params, algo=B3)
+    p = O.Push(*params, algo=B3, nthreads=1 if slice_size < 100_000 else 4)
     got = []
     for k in range(0, len(data), slice_size):
         got += list(p.push(data[k:k + slice_size]))

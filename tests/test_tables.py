@@ -125,3 +125,28 @@ def test_gpu_unverified_table_runs_selftest_on_first_use(ca, gpu, monkeypatch):
         assert np.array_equal(got["offset"], ref["offset"]) and np.array_equal(got["length"], ref["length"])
     finally:
         ca.set_cdc_tables(O.GEAR, O.MASKS)
+
+
+def test_installer_parses_crate_source_and_refuses_a_wrong_table(tmp_path):
+    """scripts/install_fastcdc_tables.py reads the crate's `GEAR` / `MASKS` array
+    literals and writes nothing unless the oracle then reproduces the reference fixture;
+    the placeholder written as such a source is refused with the boundaries it gives."""
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parent.parent
+    src = "pub(super) const MASKS: [u64; 26] = [\n" + ",\n".join(f"    0x{int(v):016x}" for v in O.MASKS) + "\n];\n"
+    src += "#[rustfmt::skip]\nconst GEAR: [u64; 256] = [\n"
+    src += ",\n".join(f"    0x{int(v):016x}, // entry {i}"[:-len(f", // entry {i}")] + f" // {i}"
+                      for i, v in enumerate(O.GEAR)) + "\n];\n"
+    f = tmp_path / "mod.rs"
+    f.write_text(src)
+    before = (root / "tables" / "fastcdc_v2020_gear.txt").read_text()
+    r = subprocess.run([sys.executable, str(root / "scripts" / "install_fastcdc_tables.py"), str(f)],
+                       capture_output=True, text=True)
+    if O.GEAR_IS_PLACEHOLDER:
+        assert r.returncode != 0 and "REFUSED" in r.stderr + r.stdout
+        ref = O.fastcdc(fixture_bytes(), 1024, 6000, 16 * 1024)
+        assert f"give {len(ref)} chunks" in r.stderr + r.stdout
+    assert (root / "tables" / "fastcdc_v2020_gear.txt").read_text() == before
