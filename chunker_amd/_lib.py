@@ -141,8 +141,11 @@ def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
     return L
 
 
-# CHUNKER_AMD_DIAG=1 (scripts/diag_*.py only) loads the diagnostics build in its place
-lib = _load(DIAG_LIB_PATH if __import__("os").environ.get("CHUNKER_AMD_DIAG") == "1" else LIB_PATH)
+# CHUNKER_AMD_DIAG=1 (scripts/diag_*.py only) loads the diagnostics build in its place;
+# CHUNKER_AMD_LIB=<path> loads another build of the same ABI (kernel A/B experiments)
+_env = __import__("os").environ
+lib = _load(Path(_env["CHUNKER_AMD_LIB"]) if _env.get("CHUNKER_AMD_LIB")
+            else DIAG_LIB_PATH if _env.get("CHUNKER_AMD_DIAG") == "1" else LIB_PATH)
 assert lib.cg_abi_version() == ABI_VERSION
 
 _diag = None

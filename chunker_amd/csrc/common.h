@@ -7,7 +7,9 @@
 // buffer, after a HALO-byte warm-up.  Every FastCDC v2020 mask lives in bits <= 47,
 // so 48 bytes of history make the rolling Gear hash's tested bits exact
 // (SURVEY.md Appendix A.3).
+#ifndef CG_SEG
 #define CG_SEG 4096u
+#endif
 #define CG_HALO 48u
 #define CG_SCAN_BLOCK 256u
 

@@ -141,6 +141,11 @@ extern uint32_t g_scan_diag;
 }
 extern "C" void cg_diag_scan_mode(uint32_t mode) { cg::g_scan_diag = mode; }
 namespace cg {
+extern uint32_t g_scan_variant;
+}
+// 0 = product k_scan; 1 = round-1 quad-transpose kernel; 2 = LDS-staged; 3 = page per wave
+extern "C" void cg_diag_scan_variant(uint32_t v) { cg::g_scan_variant = v; }
+namespace cg {
 extern uint32_t g_b3_diag;
 }
 // 1 = BLAKE3 leaves compress register words without loading them (digests garbage)

@@ -9,6 +9,9 @@
 // the tested bits equal those of the crate's per-chunk hash for every position at
 // least 47 bytes past the chunk's hash start.  The 47
 // positions before that are recomputed exactly by the walker.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.h"
 
 namespace cg {
@@ -26,16 +29,244 @@ __device__ __forceinline__ uint32_t gear_flags(uint64_t h, uint64_t mask_s, uint
 #define GEAR_COPIES 32u
 #define SCAN2_T 512u
 #define PIECE 128u
+#define QPIECE 64u  // bytes per hashed piece (one 64-bit `hits` bit each)
 
+__device__ __forceinline__ uint64_t lds_gear(const char *base, uint32_t addr) {
+    return *reinterpret_cast<const uint64_t *>(base + addr);
+}
+
+// ---------------------------------------------------------------------------
+// K1 (the product kernel).  One lane per CG_SEG segment of the flat batch buffer, after
+// a CG_HALO warm-up, as the round-1 quad-transpose kernel (k_scan_quad, diagnostics build), but:
+//  * every lane loads its OWN segment (4 x dwordx4 per 64-B piece, both pieces of a
+//    128-B line in one burst, two to three pieces ahead), so no quad transpose
+//    (the DPP movs + selects cost ~1 VALU per byte in k_scan);
+//  * the hash is kept as H' = H << 16 (mod 2^64) with the LDS table pre-shifted
+//    (GEAR[v] << 16): exact for H's bits 0..47, where every FastCDC mask lives, and
+//    H's bits 16..47 are H''s high dword -- the prefilter test is one v_and_b32 on it
+//    (mask bits 12..15 are left to the exact re-walk), folded two bytes at a time
+//    into a running v_min3_u32;
+//  * a lookup address (byte << 8 | copy offset) is one SDWA v_mov_b32 writing the
+//    byte into bits 8..15 of a register that keeps the lane's copy offset in bits
+//    0..7 (v_perm_b32 in k_scan is a half-rate instruction on gfx950).
+// Per byte: 1 SDWA mov + 1 ds_read_b64 + 1 v_lshl_add_u64 + 1 v_and_b32 + 1/2 v_min3_u32.
+// ---------------------------------------------------------------------------
+#define SCAN_SHIFT 16u
+
+template <int B>
+__device__ __forceinline__ void sdwa_byte_addr(uint32_t &a, uint32_t w) {
+    if constexpr (B == 0)
+        asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_0" : "+v"(a) : "v"(w));
+    else if constexpr (B == 1)
+        asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_1" : "+v"(a) : "v"(w));
+    else if constexpr (B == 2)
+        asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2" : "+v"(a) : "v"(w));
+    else
+        asm("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_3" : "+v"(a) : "v"(w));
+}
+
+// the 4 lookups of dword w: addresses in a[0..3] (bits 0..7 = this lane's copy offset)
+__device__ __forceinline__ void lookup4(const char *gbase, uint32_t (&a)[4], uint32_t w, uint64_t (&g)[4]) {
+    sdwa_byte_addr<0>(a[0], w);
+    sdwa_byte_addr<1>(a[1], w);
+    sdwa_byte_addr<2>(a[2], w);
+    sdwa_byte_addr<3>(a[3], w);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) g[b] = lds_gear(gbase, a[b]);
+}
+
+__device__ __forceinline__ uint32_t gear_flags64(uint64_t h, uint64_t ms, uint64_t ml) {
+    return ((h & ms) == 0 ? CG_FLAG_S : 0u) | ((h & ml) == 0 ? CG_FLAG_L : 0u);
+}
+
+template <bool PRE, int RING = 4>
+__global__ __launch_bounds__(SCAN2_T) void k_scan(const uint8_t *__restrict__ data, uint64_t n,
+                                                      const uint64_t *__restrict__ gear_g, uint64_t mask_s,
+                                                      uint64_t mask_l, uint32_t cap, uint32_t *__restrict__ seg_count,
+                                                      uint32_t *__restrict__ seg_cand, uint64_t nseg) {
+    __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * GEAR_COPIES];
+    for (uint32_t i = threadIdx.x; i < 256 * GEAR_COPIES; i += SCAN2_T)
+        s_gear[i] = gear_g[i / GEAR_COPIES] << SCAN_SHIFT;
+    __syncthreads();
+    const char *gbase = reinterpret_cast<const char *>(s_gear);
+
+    const uint64_t seg = (uint64_t)blockIdx.x * SCAN2_T + threadIdx.x;
+    if (seg - (threadIdx.x & 63u) >= nseg) return;  // whole wave past the end
+    const bool active = seg < nseg;
+    const uint32_t lo8 = (threadIdx.x & 31u) * 8u;
+    const uint64_t start = seg * CG_SEG;
+    const uint64_t end = active ? (start + CG_SEG < n ? start + CG_SEG : n) : start;
+    const uint32_t npieces = active ? (uint32_t)((end - start) / QPIECE) : 0u;
+    const uint64_t ms = mask_s << SCAN_SHIFT, ml = mask_l << SCAN_SHIFT;
+    const uint32_t mh = (uint32_t)((mask_s & mask_l) >> (32 - SCAN_SHIFT));  // H bits 16..47 = H' high dword
+
+    uint32_t ad[2][4];  // lookup address registers: bits 0..7 stay this lane's copy offset
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) ad[i][b] = lo8;
+
+    uint64_t h = 0;
+    if (active && start >= CG_HALO) {  // warm-up over the 48 bytes before the segment
+        const uint4 *hp = reinterpret_cast<const uint4 *>(data + start - CG_HALO);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const uint4 v = hp[k];
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint64_t g[4];
+                lookup4(gbase, ad[0], w[j], g);
+#pragma unroll
+                for (int b = 0; b < 4; ++b) h = (h << 1) + g[b];
+            }
+        }
+    }
+
+    uint32_t count = 0;
+    uint64_t hits = 0;  // PRE: bit r = piece r may hold a candidate
+    uint32_t *cand = seg_cand + seg * cap;
+    const uint32_t rounds = CG_SEG / QPIECE;  // wave-uniform trip count
+    static_assert(CG_SEG / QPIECE <= 64, "hits mask holds one bit per piece");
+    // RING pieces in registers; loads go out BURST = RING / 2 pieces (RING / 2 x 64 B of
+    // one segment) at a time, RING / 2 .. RING - 1 pieces ahead of the one being hashed
+    constexpr int BURST = RING / 2;
+    static_assert(CG_SEG % (RING * QPIECE) == 0, "the ring loop hashes RING pieces per trip");
+    // Loads are unconditional (a piece past the last full one re-reads the last one, or
+    // the buffer's first bytes for a segment without a full piece): the compiler then
+    // counts vmcnt exactly and waits only for the piece about to be hashed.
+    const uint8_t *base = npieces ? data + start : data;
+    const uint32_t last = npieces ? npieces - 1u : 0u;
+    uint4 buf[RING][4];
+    auto issue = [&](uint4(&v)[4], uint32_t r) {
+        const uint4 *a = reinterpret_cast<const uint4 *>(base + (uint64_t)min(r, last) * QPIECE);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = a[j];
+    };
+#pragma unroll
+    for (int i = 0; i < BURST; ++i) issue(buf[i], i);
+#pragma unroll 1
+    for (uint32_t r = 0; r < rounds; r += RING) {
+#pragma unroll
+        for (int u = 0; u < RING; ++u) {
+            const uint32_t rr = r + u;
+            if ((u % BURST) == 0) {  // whole 128-B lines of the segment in one burst
+#pragma unroll
+                for (int i = 0; i < BURST; ++i) issue(buf[(u + BURST + i) % RING], rr + BURST + i);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            const uint32_t wd[16] = {buf[u][0].x, buf[u][0].y, buf[u][0].z, buf[u][0].w,
+                                     buf[u][1].x, buf[u][1].y, buf[u][1].z, buf[u][1].w,
+                                     buf[u][2].x, buf[u][2].y, buf[u][2].z, buf[u][2].w,
+                                     buf[u][3].x, buf[u][3].y, buf[u][3].z, buf[u][3].w};
+            if (PRE) {
+                uint64_t hn = h;
+                uint32_t acc = 0xffffffffu;
+                uint64_t g[2][4];
+                lookup4(gbase, ad[0], wd[0], g[0]);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    if (k + 1 < 16) lookup4(gbase, ad[(k + 1) & 1], wd[k + 1], g[(k + 1) & 1]);
+                    __builtin_amdgcn_sched_barrier(0);  // keep the lookups one dword ahead of the chain
+                    hn = (hn << 1) + g[k & 1][0];
+                    const uint32_t t0 = (uint32_t)(hn >> 32) & mh;
+                    hn = (hn << 1) + g[k & 1][1];
+                    const uint32_t t1 = (uint32_t)(hn >> 32) & mh;
+                    acc = min(min(acc, t0), t1);  // v_min3_u32
+                    hn = (hn << 1) + g[k & 1][2];
+                    const uint32_t t2 = (uint32_t)(hn >> 32) & mh;
+                    hn = (hn << 1) + g[k & 1][3];
+                    const uint32_t t3 = (uint32_t)(hn >> 32) & mh;
+                    acc = min(min(acc, t2), t3);
+                }
+                const bool live = rr < npieces;
+                h = live ? hn : h;
+                hits |= (live && acc == 0) ? (1ull << rr) : 0ull;
+            } else if (rr < npieces) {
+                const uint64_t p = start + (uint64_t)rr * QPIECE;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    uint64_t g[4];
+                    lookup4(gbase, ad[k & 1], wd[k], g);
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        h = (h << 1) + g[b];
+                        const uint32_t f = gear_flags64(h, ms, ml);
+                        if (f) {
+                            if (count < cap) cand[count] = ((uint32_t)(p - start + 4 * k + b) << 2) | f;
+                            ++count;
+                        }
+                    }
+                }
+            }
+        }
+    }
+    if (!active) return;
+    if (PRE) {
+        // Exact re-walk of the flagged pieces, in order, from L2/MALL-resident bytes.
+        // The hash restarts 48 bytes before the piece (or at 0 for the batch's first
+        // bytes, where the scan itself started): the tested bits (<= 47) equal the
+        // scan's, which restarted at the segment's own halo.
+        while (hits) {
+            const uint32_t r = (uint32_t)__builtin_ctzll(hits);
+            hits &= hits - 1;
+            const uint64_t p = start + (uint64_t)r * QPIECE;
+            const uint64_t q0 = p >= CG_HALO ? p - CG_HALO : 0;
+            uint64_t hh = 0;
+            for (uint64_t q = q0; q < p; q += 16) {
+                const uint4 x = *reinterpret_cast<const uint4 *>(data + q);
+                const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    uint64_t g[4];
+                    lookup4(gbase, ad[0], w[j], g);
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) hh = (hh << 1) + g[b];
+                }
+            }
+            for (uint32_t k = 0; k < QPIECE; k += 16) {
+                const uint4 x = *reinterpret_cast<const uint4 *>(data + p + k);
+                const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    uint64_t g[4];
+                    lookup4(gbase, ad[0], w[j], g);
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        hh = (hh << 1) + g[b];
+                        const uint32_t f = gear_flags64(hh, ms, ml);
+                        if (f) {
+                            if (count < cap) cand[count] = ((uint32_t)(p - start + k + 4 * j + b) << 2) | f;
+                            ++count;
+                        }
+                    }
+                }
+            }
+        }
+    }
+    for (uint64_t p = start + (uint64_t)npieces * QPIECE; p < end; ++p) {  // ragged tail (< 64 bytes)
+        h = (h << 1) + lds_gear(gbase, ((uint32_t)data[p] << 8) | lo8);
+        const uint32_t f = gear_flags64(h, ms, ml);
+        if (f) {
+            if (count < cap) cand[count] = ((uint32_t)(p - start) << 2) | f;
+            ++count;
+        }
+    }
+    seg_count[seg] = count;
+}
+
+#ifdef CG_DIAG
+// ===========================================================================
+// Alternative scan kernels, kept in the diagnostics build for the A/B measurements
+// recorded in DESIGN.md §4 (scripts/diag_scan.py --variants).
+// ===========================================================================
 // v_perm_b32 selector producing (byte b of `w`) << 8 | (byte 0 of `lo8`): the LDS
 // address of entry w.byte[b] in this lane's copy, in one instruction.
 __device__ __forceinline__ uint32_t gear_addr(uint32_t w, uint32_t lo8, int b) {
     return __builtin_amdgcn_perm(w, lo8, 0x0C0C0000u | ((4u + (uint32_t)b) << 8));
 }
 
-__device__ __forceinline__ uint64_t lds_gear(const char *base, uint32_t addr) {
-    return *reinterpret_cast<const uint64_t *>(base + addr);
-}
 
 // 4x4 transpose of 16-byte elements inside each quad of lanes: on entry lane i
 // holds v[j] = quarter i of lane j's 64-byte piece; on exit lane i holds v[j] =
@@ -71,7 +302,6 @@ __device__ __forceinline__ void quad_transpose(uint4 v[4], uint32_t lane) {
     quad_swap<0x4E, 2>(v, lane);  // quad_perm [2,3,0,1]
 }
 
-#define QPIECE 64u
 
 // K1.  Each lane owns CG_SEG bytes of the flat batch buffer.  Bytes arrive in 64-B
 // pieces loaded cooperatively by the 4 lanes of a quad (each dwordx4 instruction
@@ -85,7 +315,7 @@ __device__ __forceinline__ void quad_transpose(uint4 v[4], uint32_t lane) {
 // 3 = hashing on register-resident bytes without loads, 4 = as 3 without LDS reads;
 // + 8 = non-temporal loads.
 template <bool PRE, int DIAG = 0>
-__global__ __launch_bounds__(SCAN2_T) void k_scan(const uint8_t *__restrict__ data, uint64_t n,
+__global__ __launch_bounds__(SCAN2_T) void k_scan_quad(const uint8_t *__restrict__ data, uint64_t n,
                                                   const uint64_t *__restrict__ gear_g, uint64_t mask_s,
                                                   uint64_t mask_l, uint32_t cap, uint32_t *__restrict__ seg_count,
                                                   uint32_t *__restrict__ seg_cand, uint64_t nseg) {
@@ -131,10 +361,10 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan(const uint8_t *__restrict__ da
     }
 
     uint32_t count = 0;
-    uint64_t hits = 0;  // PRE: bit r = piece r may hold a candidate (CG_SEG / QPIECE == 64 pieces)
+    uint64_t hits = 0;  // PRE: bit r = piece r may hold a candidate (CG_SEG / QPIECE <= 64 pieces)
     uint32_t *cand = seg_cand + seg * cap;
     const uint32_t rounds = CG_SEG / QPIECE;  // wave-uniform trip count
-    static_assert(CG_SEG / QPIECE == 64, "hits mask holds one bit per piece");
+    static_assert(CG_SEG / QPIECE <= 64 && CG_SEG % (4 * QPIECE) == 0, "hits mask / ring loop geometry");
     uint4 buf[4][4];
     // Loads are unconditional (a piece index past the owner's last piece is clamped to
     // a valid address and its bytes are never hashed): with no exec-masked loads the
@@ -306,33 +536,475 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan(const uint8_t *__restrict__ da
     seg_count[seg] = count;
 }
 
+// ---------------------------------------------------------------------------
+// K1, LDS-staged form (diagnostics build: measured slower).  HBM efficiency depends on the read pattern far more than on
+// the hashing: a wave reading its 64 lanes' segments in 64-128 B runs per lane reaches
+// ~4.4-4.8 TB/s, in 256 B runs ~5.1-5.5 TB/s (scripts/diag_scan.py read patterns,
+// profiles/r02_diag_scan.json).  So each wave stages its segments through LDS:
+//  * a phase moves 256 B of each of the wave's 64 segments (16 KiB) with 16 LDS-DMA
+//    instructions (global_load_lds_dwordx4), each reading four whole 256-B runs (16
+//    lanes per run, so every 128-B line is requested whole by one instruction);
+//  * the per-lane SOURCE addresses are permuted so that the lane-linear LDS image puts
+//    segment o's 16-B chunk m at 1024 (o % 16) + 256 (o / 16) + 16 ((m + o) % 16):
+//    every ds_read_b128 lane group then reads 16 distinct bank quads (no conflicts);
+//  * the wave copies its phase into registers, issues the next phase's DMA at once,
+//    and hashes the 256 B from registers while it lands (one 16-KiB buffer per wave);
+//  * 8 waves per CU (one 512-thread workgroup, persistent over 64-segment tasks) share
+//    one 16-copy GEAR table (32 KiB; lanes c and c+16 share a copy: ~1.5-way bank
+//    conflicts on lookups), 8 x 16 KiB staging + 32 KiB = the CU's 160 KiB of LDS.
+// Hash representation and prefilter as k_scan (H' = H << 16).
+// ---------------------------------------------------------------------------
+#define LW 8u                        // waves per workgroup (one workgroup per CU)
+#define LCOPIES 16u                  // GEAR table copies
+#define LPHASE 256u                  // bytes per segment per phase
+#define LSTAGE (64u * LPHASE)        // staging bytes per wave
+static_assert(LCOPIES * 256u * 8u + LW * LSTAGE <= 163840u, "LDS budget of one CU");
+static_assert(CG_SEG % LPHASE == 0 && LPHASE % QPIECE == 0, "phase geometry");
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void gbl_void;
+
+// lookup address of byte B of w: (byte << 7) | copy offset (entry stride 128 B = 16 copies)
+template <int B>
+__device__ __forceinline__ uint32_t addr16(uint32_t w, uint32_t sh7, uint32_t cbase) {
+    uint32_t a;
+    if constexpr (B == 0)
+        asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+            : "=v"(a) : "v"(sh7), "v"(w));
+    else if constexpr (B == 1)
+        asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
+            : "=v"(a) : "v"(sh7), "v"(w));
+    else if constexpr (B == 2)
+        asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
+            : "=v"(a) : "v"(sh7), "v"(w));
+    else
+        asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3"
+            : "=v"(a) : "v"(sh7), "v"(w));
+    return a | cbase;
+}
+
+__device__ __forceinline__ void lookup4x16(const char *gbase, uint32_t w, uint32_t sh7, uint32_t cbase,
+                                           uint64_t (&g)[4]) {
+    const uint32_t a0 = addr16<0>(w, sh7, cbase), a1 = addr16<1>(w, sh7, cbase);
+    const uint32_t a2 = addr16<2>(w, sh7, cbase), a3 = addr16<3>(w, sh7, cbase);
+    g[0] = lds_gear(gbase, a0);
+    g[1] = lds_gear(gbase, a1);
+    g[2] = lds_gear(gbase, a2);
+    g[3] = lds_gear(gbase, a3);
+}
+
+template <bool PRE>
+__global__ __launch_bounds__(64 * LW) void k_scan_lds(const uint8_t *__restrict__ data, uint64_t n,
+                                                      const uint64_t *__restrict__ gear_g, uint64_t mask_s,
+                                                      uint64_t mask_l, uint32_t cap, uint32_t *__restrict__ seg_count,
+                                                      uint32_t *__restrict__ seg_cand, uint64_t nseg) {
+    __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * LCOPIES];
+    __shared__ __attribute__((aligned(16))) uint8_t s_stage[LW][LSTAGE];
+    for (uint32_t i = threadIdx.x; i < 256 * LCOPIES; i += 64 * LW) s_gear[i] = gear_g[i / LCOPIES] << SCAN_SHIFT;
+    __syncthreads();
+    const char *gbase = reinterpret_cast<const char *>(s_gear);
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    uint32_t sh7 = 7, cbase = (lane & 15u) * 8u;
+    asm volatile("" : "+v"(sh7), "+v"(cbase));  // VGPR operands of the SDWA shifts
+    uint8_t *stage = s_stage[wave];
+    // this lane's chunk m of the staged phase sits at rd + 16 ((m + lane) % 16)
+    const uint8_t *rd = stage + 1024u * (lane & 15u) + 256u * (lane >> 4);
+    const uint64_t ms = mask_s << SCAN_SHIFT, ml = mask_l << SCAN_SHIFT;
+    const uint32_t mh = (uint32_t)((mask_s & mask_l) >> (32 - SCAN_SHIFT));
+    const uint64_t ntask = (nseg + 63) / 64;
+    const uint32_t phases = CG_SEG / LPHASE;
+    static_assert(CG_SEG / QPIECE <= 64, "hits mask holds one bit per piece");
+
+    for (uint64_t task = (uint64_t)blockIdx.x * LW + wave; task < ntask; task += (uint64_t)gridDim.x * LW) {
+        const uint64_t seg = task * 64 + lane;
+        const bool active = seg < nseg;
+        const uint64_t start = seg * CG_SEG;
+        const uint64_t end = active ? (start + CG_SEG < n ? start + CG_SEG : n) : start;
+        const uint32_t npieces = active ? (uint32_t)((end - start) / QPIECE) : 0u;
+        // DMA role: instruction i reads chunk ((lane % 16) - i) % 16 of segment 16 (lane / 16) + i
+        const uint64_t grp = (task * 64 + 16u * (lane >> 4)) * CG_SEG;
+        auto dma_phase = [&](uint32_t ph) {
+#pragma unroll
+            for (uint32_t i = 0; i < 16; ++i) {
+                uint64_t src = grp + (uint64_t)i * CG_SEG + ph * LPHASE + 16u * ((lane - i) & 15u);
+                src = src + 16 <= n ? src : 0;  // past the batch: any readable bytes (never hashed)
+                __builtin_amdgcn_global_load_lds((gbl_void *)(data + src), (lds_void *)(stage + 1024u * i), 16, 0,
+                                                 0);
+            }
+        };
+
+        uint64_t h = 0;
+        if (active && start >= CG_HALO) {  // warm-up over the 48 bytes before the segment
+            const uint4 *hp = reinterpret_cast<const uint4 *>(data + start - CG_HALO);
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const uint4 v = hp[k];
+                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    uint64_t g[4];
+                    lookup4x16(gbase, w[j], sh7, cbase, g);
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) h = (h << 1) + g[b];
+                }
+            }
+        }
+        uint32_t count = 0;
+        uint64_t hits = 0;
+        uint32_t *cand = seg_cand + seg * cap;
+        dma_phase(0);
+#pragma unroll 1
+        for (uint32_t ph = 0; ph < phases; ++ph) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA of phase ph has landed
+            uint4 d[16];
+#pragma unroll
+            for (uint32_t m = 0; m < 16; ++m) d[m] = *reinterpret_cast<const uint4 *>(rd + 16u * ((m + lane) & 15u));
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // staging read out: the next phase may land
+            if (ph + 1 < phases) dma_phase(ph + 1);
+#pragma unroll
+            for (uint32_t q = 0; q < LPHASE / QPIECE; ++q) {
+                const uint32_t rr = ph * (LPHASE / QPIECE) + q;  // piece index in the segment
+                const uint32_t wd[16] = {d[4 * q].x,     d[4 * q].y,     d[4 * q].z,     d[4 * q].w,
+                                         d[4 * q + 1].x, d[4 * q + 1].y, d[4 * q + 1].z, d[4 * q + 1].w,
+                                         d[4 * q + 2].x, d[4 * q + 2].y, d[4 * q + 2].z, d[4 * q + 2].w,
+                                         d[4 * q + 3].x, d[4 * q + 3].y, d[4 * q + 3].z, d[4 * q + 3].w};
+                if (PRE) {
+                    uint64_t hn = h;
+                    uint32_t acc = 0xffffffffu;
+                    uint64_t g[2][4];
+                    lookup4x16(gbase, wd[0], sh7, cbase, g[0]);
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) {
+                        if (k + 1 < 16) lookup4x16(gbase, wd[k + 1], sh7, cbase, g[(k + 1) & 1]);
+                        hn = (hn << 1) + g[k & 1][0];
+                        const uint32_t t0 = (uint32_t)(hn >> 32) & mh;
+                        hn = (hn << 1) + g[k & 1][1];
+                        const uint32_t t1 = (uint32_t)(hn >> 32) & mh;
+                        acc = min(min(acc, t0), t1);  // v_min3_u32
+                        hn = (hn << 1) + g[k & 1][2];
+                        const uint32_t t2 = (uint32_t)(hn >> 32) & mh;
+                        hn = (hn << 1) + g[k & 1][3];
+                        const uint32_t t3 = (uint32_t)(hn >> 32) & mh;
+                        acc = min(min(acc, t2), t3);
+                    }
+                    const bool live = rr < npieces;
+                    h = live ? hn : h;
+                    hits |= (live && acc == 0) ? (1ull << rr) : 0ull;
+                } else if (rr < npieces) {
+                    const uint64_t p = start + (uint64_t)rr * QPIECE;
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) {
+                        uint64_t g[4];
+                        lookup4x16(gbase, wd[k], sh7, cbase, g);
+#pragma unroll
+                        for (int b = 0; b < 4; ++b) {
+                            h = (h << 1) + g[b];
+                            const uint32_t f = gear_flags64(h, ms, ml);
+                            if (f) {
+                                if (count < cap) cand[count] = ((uint32_t)(p - start + 4 * k + b) << 2) | f;
+                                ++count;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        if (!active) continue;
+        if (PRE) {  // exact re-walk of the flagged pieces (as k_scan)
+            while (hits) {
+                const uint32_t r = (uint32_t)__builtin_ctzll(hits);
+                hits &= hits - 1;
+                const uint64_t p = start + (uint64_t)r * QPIECE;
+                const uint64_t q0 = p >= CG_HALO ? p - CG_HALO : 0;
+                uint64_t hh = 0;
+                for (uint64_t q = q0; q < p; q += 16) {
+                    const uint4 x = *reinterpret_cast<const uint4 *>(data + q);
+                    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        uint64_t g[4];
+                        lookup4x16(gbase, w[j], sh7, cbase, g);
+#pragma unroll
+                        for (int b = 0; b < 4; ++b) hh = (hh << 1) + g[b];
+                    }
+                }
+                for (uint32_t k = 0; k < QPIECE; k += 16) {
+                    const uint4 x = *reinterpret_cast<const uint4 *>(data + p + k);
+                    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        uint64_t g[4];
+                        lookup4x16(gbase, w[j], sh7, cbase, g);
+#pragma unroll
+                        for (int b = 0; b < 4; ++b) {
+                            hh = (hh << 1) + g[b];
+                            const uint32_t f = gear_flags64(hh, ms, ml);
+                            if (f) {
+                                if (count < cap) cand[count] = ((uint32_t)(p - start + k + 4 * j + b) << 2) | f;
+                                ++count;
+                            }
+                        }
+                    }
+                }
+            }
+        }
+        for (uint64_t p = start + (uint64_t)npieces * QPIECE; p < end; ++p) {  // ragged tail (< 64 bytes)
+            h = (h << 1) + lds_gear(gbase, ((uint32_t)data[p] << 7) | cbase);
+            const uint32_t f = gear_flags64(h, ms, ml);
+            if (f) {
+                if (count < cap) cand[count] = ((uint32_t)(p - start) << 2) | f;
+                ++count;
+            }
+        }
+        seg_count[seg] = count;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K1, page-per-wave form (diagnostics build: measured slower).  What limits the other forms is the
+// HBM read pattern, not the hashing: one stream per lane (64 streams per wave, each
+// advancing 64-128 B at a time) reads at ~4.4 TB/s, whole 4 KiB pages per wave at
+// ~6.0 TB/s (scripts/diag_scan.py read patterns, profiles/r02_diag_scan.json).  So
+// here a wave walks its own run of PPW consecutive 4 KiB pages (= CG_SEG segments) in
+// order, and in each page lane L takes bytes [64 L, 64 L + 64):
+//  * the page arrives as 4 dwordx4 loads per lane (stride 64 B: the 4 instructions
+//    cover the page), two pages ahead of the one being hashed;
+//  * the 48 bytes before lane L's piece -- the window the masked bits depend on
+//     -- are lane L-1's last 48 bytes, moved over by 12 DPP
+//    wave_ror:1 movs; lane 0 takes the previous page's lane 63 (the rotation's value
+//    kept from one page to the next) and, on a run's first page, loads them;
+//  * a piece is hashed from the restart: 48 warm-up steps (lookup + shift-add) and 64
+//    tested steps, so the hash state never crosses lanes;
+//  * prefilter as k_scan (H' = H << 16, one v_and_b32 + 1/2 v_min3_u32 per byte);
+//    a lane whose piece may hold a candidate re-walks it exactly from registers, and the
+//    page's candidates are compacted in lane (= position) order by a wave prefix sum.
+// Per byte: 1.75 lookups (SDWA mov + ds_read_b64 + v_lshl_add_u64), 1 v_and_b32,
+// 1/2 v_min3_u32.
+// ---------------------------------------------------------------------------
+#define PPW 66u  // pages per wave: a multiple of the 3-page load ring (one loop path: exact vmcnt waits)
+static_assert(CG_SEG == 64u * QPIECE, "a page is one 64-B piece per lane");
+#define DPP_WAVE_ROR1 0x13C
+
+__device__ __forceinline__ uint32_t wave_ror1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, DPP_WAVE_ROR1, 0xf, 0xf, false);
+}
+
+// Exact test of every position of this lane's piece (nbytes at src, re-read from
+// L2: the rare path) from the warm-up state h0; counts the candidates and, with `out`,
+// writes them ((page offset << 2) | flags) up to `room`.  Out of line: it runs only for
+// the few pieces the prefilter flags, and inlined it would cost the hot loop registers.
+__device__ __noinline__ uint32_t exact_piece(const char *gbase, uint32_t lo8, const uint8_t *src, uint64_t h0,
+                                             uint32_t nbytes, uint64_t ms, uint64_t ml, uint32_t pos0,
+                                             uint32_t *out, uint32_t room) {
+    uint32_t w[16];
+    if (nbytes == 64) {  // whole piece: four 16-B loads in flight together (one L2 round trip)
+        const uint4 *q = reinterpret_cast<const uint4 *>(src);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint4 v = q[k];
+            w[4 * k] = v.x;
+            w[4 * k + 1] = v.y;
+            w[4 * k + 2] = v.z;
+            w[4 * k + 3] = v.w;
+        }
+    } else {  // the batch's ragged last piece: never read past its end
+#pragma unroll
+        for (int k = 0; k < 16; ++k) w[k] = 0;
+        for (uint32_t j = 0; j < nbytes; ++j) w[j >> 2] |= (uint32_t)src[j] << (8 * (j & 3));
+    }
+    uint64_t h = h0;
+    uint32_t c = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 64; ++j) {
+        h = (h << 1) + lds_gear(gbase, (((w[j >> 2] >> (8 * (j & 3))) & 0xffu) << 8) | lo8);
+        const uint32_t f = j < nbytes ? gear_flags64(h, ms, ml) : 0u;
+        if (f) {
+            if (out && c < room) out[c] = ((pos0 + j) << 2) | f;
+            ++c;
+        }
+    }
+    return c;
+}
+
+template <bool PRE>
+__global__ __launch_bounds__(SCAN2_T, 4) void k_scan_wave(const uint8_t *__restrict__ data, uint64_t n,
+                                                       const uint64_t *__restrict__ gear_g, uint64_t mask_s,
+                                                       uint64_t mask_l, uint32_t cap, uint32_t *__restrict__ seg_count,
+                                                       uint32_t *__restrict__ seg_cand, uint64_t nseg) {
+    __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * GEAR_COPIES];
+    for (uint32_t i = threadIdx.x; i < 256 * GEAR_COPIES; i += SCAN2_T)
+        s_gear[i] = gear_g[i / GEAR_COPIES] << SCAN_SHIFT;
+    __syncthreads();
+    const char *gbase = reinterpret_cast<const char *>(s_gear);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t page0 = ((uint64_t)blockIdx.x * (SCAN2_T / 64) + (threadIdx.x >> 6)) * PPW;
+    if (page0 >= nseg) return;  // whole wave (uniform)
+    // pages of the run past the batch are walked as empty pages (no output), so every run
+    // has PPW pages and the ring loop one path
+    const uint64_t page_end = page0 + PPW < nseg ? page0 + PPW : nseg;
+    const uint32_t lo8 = (threadIdx.x & 31u) * 8u;
+    uint32_t ad[2][4];  // lookup address registers: bits 0..7 stay this lane's copy offset
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) ad[i][b] = lo8;
+    const uint64_t ms = mask_s << SCAN_SHIFT, ml = mask_l << SCAN_SHIFT;
+    const uint32_t mh = (uint32_t)((mask_s & mask_l) >> (32 - SCAN_SHIFT));
+
+    // Loads are unconditional: a page past the run re-reads the run's last page, a piece
+    // past the batch end reads the batch's first bytes (never hashed as data).
+    auto issue = [&](uint4(&v)[4], uint64_t p) {
+        const uint64_t q = p < page_end ? p : page_end - 1;
+        const uint64_t a = q * CG_SEG + 64u * lane;
+        const uint4 *src = reinterpret_cast<const uint4 *>(data + (a + 64 <= n ? a : 0));
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = src[j];
+    };
+    uint4 buf[3][4];
+    issue(buf[0], page0);
+    issue(buf[1], page0 + 1);
+    // lane 0's window before the run's first page (wave-uniform: scalar registers)
+    uint32_t carry[12];
+    {
+        const uint64_t a = page0 * CG_SEG;
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(data + (a >= CG_HALO ? a - CG_HALO : 0));
+#pragma unroll
+        for (int j = 0; j < 12; ++j) carry[j] = __builtin_amdgcn_readfirstlane(src[j]);
+    }
+
+    static_assert(PPW % 3 == 0, "the ring loop hashes three pages per trip");
+#pragma unroll 1
+    for (uint64_t p = page0; p < page0 + PPW; p += 3) {
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            const uint64_t pg = p + u;
+            const bool live = pg < page_end;  // uniform
+            issue(buf[(u + 2) % 3], pg + 2);
+            __builtin_amdgcn_sched_barrier(0);
+            const uint32_t wd[16] = {buf[u][0].x, buf[u][0].y, buf[u][0].z, buf[u][0].w,
+                                     buf[u][1].x, buf[u][1].y, buf[u][1].z, buf[u][1].w,
+                                     buf[u][2].x, buf[u][2].y, buf[u][2].z, buf[u][2].w,
+                                     buf[u][3].x, buf[u][3].y, buf[u][3].z, buf[u][3].w};
+            const uint64_t pstart = pg * CG_SEG;
+            const uint64_t mine = pstart + 64u * lane;
+            const uint32_t nbytes = (!live || mine >= n) ? 0u : (n - mine >= 64 ? 64u : (uint32_t)(n - mine));
+            // the 48 bytes before this lane's piece: lane L-1's last 12 dwords
+            uint32_t prev[12];
+#pragma unroll
+            for (int k = 0; k < 12; ++k) {
+                // lane L <- lane L-1 (DPP), lane 0 <- the previous page's lane 63 (SGPR)
+                uint32_t v = wave_ror1(wd[4 + k]);
+                asm("v_writelane_b32 %0, %1, 0" : "+v"(v) : "s"(carry[k]));
+                prev[k] = v;
+                carry[k] = (uint32_t)__builtin_amdgcn_readlane((int)wd[4 + k], 63);
+            }
+            uint64_t h0 = 0;
+#pragma unroll
+            for (int k = 0; k < 12; ++k) {
+                uint64_t g[4];
+                lookup4(gbase, ad[k & 1], prev[k], g);
+#pragma unroll
+                for (int b = 0; b < 4; ++b) h0 = (h0 << 1) + g[b];
+            }
+            if (mine == 0) h0 = 0;  // the batch's first byte: no history (as the crate's restart)
+            bool hit;
+            if (PRE) {
+                uint64_t hn = h0;
+                uint32_t acc = 0xffffffffu;
+                uint64_t g[2][4];
+                lookup4(gbase, ad[0], wd[0], g[0]);
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    if (k + 1 < 16) lookup4(gbase, ad[(k + 1) & 1], wd[k + 1], g[(k + 1) & 1]);
+                    hn = (hn << 1) + g[k & 1][0];
+                    const uint32_t t0 = (uint32_t)(hn >> 32) & mh;
+                    hn = (hn << 1) + g[k & 1][1];
+                    const uint32_t t1 = (uint32_t)(hn >> 32) & mh;
+                    acc = min(min(acc, t0), t1);  // v_min3_u32
+                    hn = (hn << 1) + g[k & 1][2];
+                    const uint32_t t2 = (uint32_t)(hn >> 32) & mh;
+                    hn = (hn << 1) + g[k & 1][3];
+                    const uint32_t t3 = (uint32_t)(hn >> 32) & mh;
+                    acc = min(min(acc, t2), t3);
+                }
+                hit = (acc == 0 && nbytes) || (nbytes && nbytes < 64);  // a ragged piece is always exact
+            } else {
+                hit = nbytes != 0;
+            }
+            const uint64_t any = __ballot(hit);
+            uint32_t total = 0;
+            if (any) {  // exact pass for the flagged pieces, then compaction in lane order
+                const uint8_t *src = data + (hit ? mine : 0);
+                const uint32_t c =
+                    hit ? exact_piece(gbase, lo8, src, h0, nbytes, ms, ml, 64u * lane, nullptr, 0) : 0u;
+                uint32_t incl = c;  // inclusive prefix over lanes (position order)
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t y = (uint32_t)__shfl_up((int)incl, d, 64);
+                    if ((int)lane >= d) incl += y;
+                }
+                total = (uint32_t)__shfl((int)incl, 63, 64);
+                const uint32_t before = incl - c;
+                if (c && before < cap)
+                    exact_piece(gbase, lo8, src, h0, nbytes, ms, ml, 64u * lane, seg_cand + pg * cap + before,
+                                cap - before);
+            }
+            if (lane == 0 && live) seg_count[pg] = total;
+        }
+    }
+}
+
+#endif  // CG_DIAG
+
 #ifdef CG_DIAG
-uint32_t g_scan_diag = 0;  // set by cg_diag_scan_mode (diagnostics build only)
+uint32_t g_scan_diag = 0;     // set by cg_diag_scan_mode (quad-kernel diag modes)
+uint32_t g_scan_variant = 0;  // set by cg_diag_scan_variant: 1 quad, 2 LDS-staged, 3 page per wave
 #endif
 
 void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint64_t mask_s, uint64_t mask_l,
                  uint32_t cap, uint32_t *d_seg_count, uint32_t *d_seg_cand, uint64_t nseg, hipStream_t st) {
     if (nseg == 0) return;
     const uint64_t blocks = (nseg + SCAN2_T - 1) / SCAN2_T;
+    // prefilter when the bits of mask_s & mask_l it tests leave hits rarer than ~1 per 16 KiB
+    const bool pre = __builtin_popcountll((mask_s & mask_l) >> SCAN_SHIFT) >= 14;
 #ifdef CG_DIAG
-    if (g_scan_diag && __builtin_popcountll(mask_s & mask_l) >= 15) {
-        auto k = g_scan_diag == 1   ? k_scan<true, 1>
-                 : g_scan_diag == 2 ? k_scan<true, 2>
-                 : g_scan_diag == 3 ? k_scan<true, 3>
-                 : g_scan_diag == 4 ? k_scan<true, 4>
-                 : g_scan_diag == 8 ? k_scan<true, 8>
-                                    : k_scan<true, 9>;
+    const bool pre_quad = __builtin_popcountll(mask_s & mask_l) >= 15;
+    if (g_scan_diag && pre_quad) {
+        auto k = g_scan_diag == 1   ? k_scan_quad<true, 1>
+                 : g_scan_diag == 2 ? k_scan_quad<true, 2>
+                 : g_scan_diag == 3 ? k_scan_quad<true, 3>
+                 : g_scan_diag == 4 ? k_scan_quad<true, 4>
+                 : g_scan_diag == 8 ? k_scan_quad<true, 8>
+                                    : k_scan_quad<true, 9>;
         hipLaunchKernelGGL(k, dim3((uint32_t)blocks), dim3(SCAN2_T), 0, st, d_data, n, d_gear, mask_s, mask_l, cap,
                            d_seg_count, d_seg_cand, nseg);
         return;
     }
+    if (g_scan_variant == 1) {
+        hipLaunchKernelGGL(pre_quad ? k_scan_quad<true> : k_scan_quad<false>, dim3((uint32_t)blocks), dim3(SCAN2_T),
+                           0, st, d_data, n, d_gear, mask_s, mask_l, cap, d_seg_count, d_seg_cand, nseg);
+        return;
+    }
+    if (g_scan_variant == 2) {
+        int dev = 0, cus = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const uint64_t ntask = (nseg + 63) / 64;
+        const uint32_t grid = (uint32_t)std::min<uint64_t>(cus > 0 ? cus : 256, (ntask + LW - 1) / LW);
+        hipLaunchKernelGGL(pre ? k_scan_lds<true> : k_scan_lds<false>, dim3(grid), dim3(64 * LW), 0, st, d_data, n,
+                           d_gear, mask_s, mask_l, cap, d_seg_count, d_seg_cand, nseg);
+        return;
+    }
+    if (g_scan_variant == 3) {
+        const uint64_t waves = (nseg + PPW - 1) / PPW;
+        const uint64_t wgs = (waves + SCAN2_T / 64 - 1) / (SCAN2_T / 64);
+        hipLaunchKernelGGL(pre ? k_scan_wave<true> : k_scan_wave<false>, dim3((uint32_t)wgs), dim3(SCAN2_T), 0, st,
+                           d_data, n, d_gear, mask_s, mask_l, cap, d_seg_count, d_seg_cand, nseg);
+        return;
+    }
 #endif
-    if (__builtin_popcountll(mask_s & mask_l) >= 15)
-        hipLaunchKernelGGL(k_scan<true>, dim3((uint32_t)blocks), dim3(SCAN2_T), 0, st, d_data, n, d_gear, mask_s,
-                           mask_l, cap, d_seg_count, d_seg_cand, nseg);
-    else
-        hipLaunchKernelGGL(k_scan<false>, dim3((uint32_t)blocks), dim3(SCAN2_T), 0, st, d_data, n, d_gear, mask_s,
-                           mask_l, cap, d_seg_count, d_seg_cand, nseg);
+    hipLaunchKernelGGL(pre ? k_scan<true> : k_scan<false>, dim3((uint32_t)blocks), dim3(SCAN2_T), 0, st, d_data, n,
+                       d_gear, mask_s, mask_l, cap, d_seg_count, d_seg_cand, nseg);
 }
 
 // ---------------------------------------------------------------------------

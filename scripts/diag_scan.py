@@ -1,5 +1,9 @@
-"""Diagnostic: k_scan stage time by diag mode (0 product, 1 loads only, 2 loads +
-transpose, 3 hashing without loads) on config-2 and config-4 shaped batches."""
+"""Diagnostic: candidate-scan stage time on config-2 and config-4 shaped batches.
+
+--variants: 0 product k_scan (own segment in registers), 1 round-1 quad-transpose
+kernel, 2 LDS-staged, 3 page per wave.  --modes (quad kernel only): 0 off, 1 loads only,
+2 loads + transpose, 3 hashing without loads, 4/8/9 partial pipelines.  Then raw HBM
+read patterns (runs of L contiguous bytes per 4 KiB segment)."""
 import os
 os.environ["CHUNKER_AMD_DIAG"] = "1"  # load libchunker_amd_diag.so (make -C chunker_amd/csrc diag)
 os.environ.setdefault("CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR", "1")
@@ -17,12 +21,14 @@ from chunker_amd.nar import synth_nars  # noqa: E402
 import argparse  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--modes", default="0,8,1,9,2,3,4,0")
+ap.add_argument("--variants", default="0,1,2,3")
+ap.add_argument("--modes", default="1,2,3")
 ap.add_argument("--configs", default="c2,c4")
 ap.add_argument("--no-pattern", action="store_true")
 args = ap.parse_args()
 lib = ca.lib
 lib.cg_diag_scan_mode.argtypes = [ctypes.c_uint32]
+lib.cg_diag_scan_variant.argtypes = [ctypes.c_uint32]
 res = {}
 for name, n, size, params in [("c2", 256, 4 << 20, (256 << 10, 1 << 20, 4 << 20)),
                               ("c4", 4, 1 << 30, (64 << 10, 256 << 10, 1 << 20))]:
@@ -36,7 +42,9 @@ for name, n, size, params in [("c2", 256, 4 << 20, (256 << 10, 1 << 20, 4 << 20)
     out = torch.empty(cap * 48, dtype=torch.uint8, device="cuda")
     sp = torch.cuda.current_stream().cuda_stream
     buf = (ctypes.c_double * 5)()
-    for mode in [int(m) for m in args.modes.split(",")]:
+    runs = [(int(v), 0) for v in args.variants.split(",") if v] + [(1, int(m)) for m in args.modes.split(",") if m]
+    for variant, mode in runs:
+        lib.cg_diag_scan_variant(variant)
         lib.cg_diag_scan_mode(mode)
         ms = []
         for it in range(6):
@@ -46,9 +54,10 @@ for name, n, size, params in [("c2", 256, 4 << 20, (256 << 10, 1 << 20, 4 << 20)
             if it >= 2:
                 ms.append(buf[0])
         gib = int(offs[-1]) / 2**30
-        res[f"{name}_mode{mode}"] = {"scan_ms": round(float(np.median(ms)), 4),
+        res[f"{name}_v{variant}_mode{mode}"] = {"scan_ms": round(float(np.median(ms)), 4),
                                      "GBps": round(int(offs[-1]) / (np.median(ms) * 1e-3) / 1e9, 1)}
     lib.cg_diag_scan_mode(0)
+    lib.cg_diag_scan_variant(0)
     del d, out
     torch.cuda.empty_cache()
 print(json.dumps(res))
