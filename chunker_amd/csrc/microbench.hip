@@ -143,8 +143,13 @@ extern "C" void cg_diag_scan_mode(uint32_t mode) { cg::g_scan_diag = mode; }
 namespace cg {
 extern uint32_t g_scan_variant;
 }
-// 0 = product k_scan; 1 = round-1 quad-transpose kernel; 2 = LDS-staged; 3 = page per wave
+// 0 = product; 1 = round-1 quad-transpose kernel; 2 = LDS-staged; 3 = page per wave; 4 = k_scan; 5 = k_scan_flat by mode
 extern "C" void cg_diag_scan_variant(uint32_t v) { cg::g_scan_variant = v; }
+namespace cg {
+extern uint32_t g_scan_spw_max;
+}
+// k_scan_flat's segments-per-wave cap (a multiple of 4; 0 = the product default)
+extern "C" void cg_diag_scan_spw_max(uint32_t v) { cg::g_scan_spw_max = v; }
 namespace cg {
 extern uint32_t g_b3_diag;
 }

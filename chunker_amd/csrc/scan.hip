@@ -256,6 +256,237 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan(const uint8_t *__restrict__ da
     seg_count[seg] = count;
 }
 
+
+// ---------------------------------------------------------------------------
+// K1, flat form: the product kernel for prefilterable masks (k_scan<false> for the
+// rest).  k_scan gives every lane
+// its own 4 KiB stream, and 64 per-lane streams read HBM at ~4.4-4.9 TB/s whatever the
+// run length (scripts/diag_scan.py read patterns); whole 1 KiB rows per wave-instruction
+// read at ~5.8-6.4.  So here a wave walks a run of `spw` consecutive segments as 1 KiB
+// rows, lane L holding bytes [16 L, 16 L + 16) of each row (one dwordx4, the row
+// contiguous), and the hash crosses lanes by linearity instead of by a warm-up:
+//  * in the shifted representation H' = H << 16 (k_scan), a byte k positions back
+//    contributes GEAR'[b] << k, which vanishes mod 2^64 for k >= 48: H' at any position
+//    is exactly the sum over the 48 bytes before it (SURVEY.md App. A.3's window);
+//  * lane L forms P_L = sum_j GEAR'[b_j] << (15 - j) over its 16 bytes (16 lookups, a
+//    shift-add chain), and the state entering its block is
+//    C_L = P_{L-1} + (P_{L-2} << 16) + (P_{L-3} << 32): three DPP wave_ror:1 rotations,
+//    lanes 0..2 taking the previous row's lanes 61..63 from the rotation kept over from
+//    the previous row (one v_bitop3 select each);
+//  * from C_L the lane re-runs its 16 steps with the prefilter (one v_and_b32 + 1/2
+//    v_min3_u32 per byte, as k_scan);
+//  * a row where any lane's prefilter fires (wave-uniform branch, rare) re-runs the 16
+//    steps exactly from the registers into per-lane S / L position masks, places the
+//    candidates with a wave prefix sum into a per-wave LDS slot list (no global stores inside the row loop: vmcnt keeps counting
+//    the load ring exactly), and every 4th row flushes the finished segment's slots and
+//    count.
+// Per byte: 1 SDWA mov + 1 ds_read_b64 + 2 v_lshl_add_u64 + 1 v_and_b32 + 1/2 v_min3_u32,
+// plus 5 DPP movs + 5 selects + ~4 VALU per 16 bytes.
+// ---------------------------------------------------------------------------
+#define FLAT_ROW 1024u  // bytes per wave row (64 lanes x 16 B)
+#define FLAT_RPS (CG_SEG / FLAT_ROW)  // rows per segment
+static_assert(CG_SEG % FLAT_ROW == 0, "whole rows per segment");
+#define DPP_WAVE_ROR1 0x13C
+
+__device__ __forceinline__ uint32_t wave_ror1(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, DPP_WAVE_ROR1, 0xf, 0xf, false);
+}
+
+
+// the 16 table entries of one lane's 16-byte block
+__device__ __forceinline__ void block_lookups(const char *gbase, uint32_t (&ad)[2][4], const uint4 v,
+                                              uint64_t (&g)[4][4]) {
+    lookup4(gbase, ad[0], v.x, g[0]);
+    lookup4(gbase, ad[1], v.y, g[1]);
+    lookup4(gbase, ad[0], v.z, g[2]);
+    lookup4(gbase, ad[1], v.w, g[3]);
+}
+
+// (a << 1) + b as one v_lshl_add_u64 (left to itself the compiler re-associates the
+// chain into shift-by-2 pairs: 3 instructions per 2 bytes)
+__device__ __forceinline__ uint64_t shl1_add(uint64_t a, uint64_t b) {
+    uint64_t r;
+    asm("v_lshl_add_u64 %0, %1, 1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+
+__device__ __forceinline__ uint64_t block_partial(const uint64_t (&g)[4][4]) {
+    uint64_t P = g[0][0];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) P = shl1_add(P, g[i >> 2][i & 3]);
+    return P;
+}
+
+template <uint32_t FLAT_D, bool NT>
+__global__ __launch_bounds__(SCAN2_T) void k_scan_flat(const uint8_t *__restrict__ data, uint64_t n,
+                                                      const uint64_t *__restrict__ gear_g, uint64_t mask_s,
+                                                      uint64_t mask_l, uint32_t cap, uint32_t *__restrict__ seg_count,
+                                                      uint32_t *__restrict__ seg_cand, uint64_t nseg, uint32_t spw) {
+    __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * GEAR_COPIES];
+    __shared__ uint32_t s_slots[SCAN2_T / 64][64];  // the open segment's candidate slots, per wave
+    for (uint32_t i = threadIdx.x; i < 256 * GEAR_COPIES; i += SCAN2_T)
+        s_gear[i] = gear_g[i / GEAR_COPIES] << SCAN_SHIFT;
+    __syncthreads();
+    const char *gbase = reinterpret_cast<const char *>(s_gear);
+
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t *slots = s_slots[threadIdx.x >> 6];
+    const uint64_t seg0 = ((uint64_t)blockIdx.x * (SCAN2_T / 64) + (threadIdx.x >> 6)) * spw;
+    if (seg0 >= nseg) return;  // whole wave (uniform)
+    const uint32_t lo8 = (threadIdx.x & 31u) * 8u;
+    uint32_t ad[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) ad[i][b] = lo8;
+    const uint64_t ms = mask_s << SCAN_SHIFT, ml = mask_l << SCAN_SHIFT;
+    const uint32_t mh = (uint32_t)((mask_s & mask_l) >> (32 - SCAN_SHIFT));
+    const uint32_t m0 = lane == 0 ? 0xffffffffu : 0u;  // lane-0 select mask (bitop3 0xCA: m ? a : b)
+    const uint32_t ms_lo = (uint32_t)ms, ms_hi = (uint32_t)(ms >> 32), ml_lo = (uint32_t)ml, ml_hi = (uint32_t)(ml >> 32);
+
+    const uint64_t r0 = seg0 * CG_SEG;
+    const uint64_t nrow64 = (uint64_t)spw * FLAT_RPS;  // a multiple of FLAT_D (spw even)
+    // Loads are unconditional and never leave the batch: a block past its end reads the last
+    // block holding a batch byte (a cache hit), so the compiler counts vmcnt exactly through
+    // the ring.
+    const uint64_t last_abs = (n - 1) & ~(uint64_t)15;
+    auto blk = [&](uint64_t row) {
+        const uint64_t a = r0 + row * FLAT_ROW + 16u * lane;
+        typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+        const u32x4_t *q = reinterpret_cast<const u32x4_t *>(data + (a < last_abs ? a : last_abs));
+        const u32x4_t x = NT ? __builtin_nontemporal_load(q) : *q;
+        return uint4{x.x, x.y, x.z, x.w};
+    };
+    static_assert(FLAT_D % FLAT_RPS == 0, "a ring trip ends on a segment boundary");
+    const uint64_t end_rel = n - r0;  // rows reaching past it hold the batch end (a partial block)
+    uint4 ring[FLAT_D];
+#pragma unroll
+    for (uint32_t i = 0; i < FLAT_D; ++i) ring[i] = blk(i);
+
+    // the row before the run (lanes 61..63 feed this run's first row); zero state at the
+    // batch start, as the crate's hash restart
+    uint64_t R1 = 0, R2 = 0;
+    uint32_t R3 = 0;
+    if (r0 >= FLAT_ROW) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(data + r0 - FLAT_ROW + 16u * lane);
+        uint64_t g[4][4];
+        block_lookups(gbase, ad, v, g);
+        const uint64_t P = block_partial(g);
+        R1 = ((uint64_t)wave_ror1((uint32_t)(P >> 32)) << 32) | wave_ror1((uint32_t)P);
+        R2 = ((uint64_t)wave_ror1((uint32_t)(R1 >> 32)) << 32) | wave_ror1((uint32_t)R1);
+        R3 = wave_ror1((uint32_t)R2);
+    }
+
+    uint32_t segc = 0;  // wave-uniform: candidates of the open segment so far
+#pragma unroll 1
+    for (uint64_t r = 0; r < nrow64; r += FLAT_D) {
+#pragma unroll
+        for (uint32_t u = 0; u < FLAT_D; ++u) {
+            const uint64_t row = r + u;
+            uint64_t g[4][4];
+            block_lookups(gbase, ad, ring[u], g);
+            const uint64_t P = block_partial(g);
+            // P_{L-1}, P_{L-2}, low dword of P_{L-3}; lanes 0.. take the previous row's
+            const uint32_t a_lo = wave_ror1((uint32_t)P), a_hi = wave_ror1((uint32_t)(P >> 32));
+            const uint32_t p1_lo = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)R1, a_lo, 0xCA);
+            const uint32_t p1_hi = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)(R1 >> 32), a_hi, 0xCA);
+            R1 = ((uint64_t)a_hi << 32) | a_lo;
+            const uint32_t b_lo = wave_ror1(p1_lo), b_hi = wave_ror1(p1_hi);
+            const uint32_t p2_lo = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)R2, b_lo, 0xCA);
+            const uint32_t p2_hi = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)(R2 >> 32), b_hi, 0xCA);
+            R2 = ((uint64_t)b_hi << 32) | b_lo;
+            const uint32_t c_lo = wave_ror1(p2_lo);
+            const uint32_t p3_lo = __builtin_amdgcn_bitop3_b32(m0, R3, c_lo, 0xCA);
+            R3 = c_lo;
+            // C = P_{L-1} + (P_{L-2} << 16) + (P_{L-3} << 32), the shifted P_{L-2} by dwords
+            const uint32_t s_hi = __builtin_amdgcn_alignbit(p2_hi, p2_lo, 16) + p3_lo;
+            const uint64_t C = (((uint64_t)p1_hi << 32) | p1_lo) + (((uint64_t)s_hi << 32) | (p2_lo << 16));
+            uint64_t h = C;
+            uint32_t acc = 0xffffffffu;
+#pragma unroll
+            for (int i = 0; i < 16; i += 2) {
+                h = shl1_add(h, g[i >> 2][i & 3]);
+                const uint32_t t0 = (uint32_t)(h >> 32) & mh;
+                h = shl1_add(h, g[(i + 1) >> 2][(i + 1) & 3]);
+                const uint32_t t1 = (uint32_t)(h >> 32) & mh;
+                acc = min(min(acc, t0), t1);  // v_min3_u32
+            }
+            const bool tail = (row + 1) * FLAT_ROW > end_rel;  // uniform
+            if (__builtin_amdgcn_ballot_w64(acc == 0) != 0 || tail) {
+            bool exact = tail;
+            if (!tail) {
+                // the prefilter fired somewhere in the row (mostly on bits below 16 it cannot
+                // see): does any byte pass the full S or L mask?  2 VALU per mask per byte
+                uint32_t ex = 0xffffffffu;
+                uint64_t hx = C;
+#pragma unroll
+                for (uint32_t j = 0; j < 16; ++j) {
+                    hx = shl1_add(hx, g[j >> 2][j & 3]);
+                    const uint32_t lo = (uint32_t)hx, hi = (uint32_t)(hx >> 32);
+                    ex = min(ex, min((lo & ms_lo) | (hi & ms_hi), (lo & ml_lo) | (hi & ml_hi)));
+                }
+                exact = __builtin_amdgcn_ballot_w64(ex == 0) != 0;
+            }
+            if (exact) {
+                // exact pass from C over the 16 entries still in registers: per-lane bit
+                // masks of the S / L positions (no branches, no LDS), a wave prefix sum
+                // (ballot + mbcnt when no lane holds two), candidates into the slot list in
+                // (row, lane, byte) = position order
+                const uint64_t prel = row * FLAT_ROW + 16u * lane;
+                const uint32_t nb = prel < end_rel ? (end_rel - prel < 16 ? (uint32_t)(end_rel - prel) : 16u) : 0u;
+                uint32_t sm = 0, lm = 0;
+                h = C;
+#pragma unroll
+                for (uint32_t j = 0; j < 16; ++j) {
+                    h = shl1_add(h, g[j >> 2][j & 3]);
+                    const uint64_t zs = h & ms, zl = h & ml;
+                    const uint32_t ts = (uint32_t)zs | (uint32_t)(zs >> 32), tl = (uint32_t)zl | (uint32_t)(zl >> 32);
+                    sm |= (1u - min(ts, 1u)) << j;
+                    lm |= (1u - min(tl, 1u)) << j;
+                }
+                const uint32_t vm = nb >= 16 ? 0xffffu : (1u << nb) - 1u;
+                sm &= vm;
+                lm &= vm;
+                const uint32_t any = sm | lm, c = (uint32_t)__builtin_popcount(any);
+                uint32_t excl, total;
+                if (__builtin_amdgcn_ballot_w64(c > 1) == 0) {
+                    const uint64_t bal = __builtin_amdgcn_ballot_w64(c != 0);
+                    excl = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+                    total = (uint32_t)__builtin_popcountll(bal);
+                } else {
+                    uint32_t incl = c;
+#pragma unroll
+                    for (uint32_t d = 1; d < 64; d <<= 1) {
+                        const uint32_t y = (uint32_t)__shfl_up((int)incl, d, 64);
+                        if (lane >= d) incl += y;
+                    }
+                    excl = incl - c;
+                    total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                }
+                const uint32_t pos0 = (uint32_t)(row % FLAT_RPS) * FLAT_ROW + 16u * lane;
+                uint32_t idx = segc + excl;
+                for (uint32_t m = any; m; m &= m - 1) {
+                    const uint32_t j = (uint32_t)__builtin_ctz(m);
+                    const uint32_t f = (((sm >> j) & 1u) * CG_FLAG_S) | (((lm >> j) & 1u) * CG_FLAG_L);
+                    if (idx < cap) slots[idx] = ((pos0 + j) << 2) | f;
+                    ++idx;
+                }
+                segc += total;
+            }
+            }
+            ring[u] = blk(row + FLAT_D < nrow64 ? row + FLAT_D : nrow64 - 1);
+            if (u % FLAT_RPS == FLAT_RPS - 1) {  // segment end: flush its slots and count
+                const uint64_t seg = seg0 + row / FLAT_RPS;
+                if (seg < nseg) {
+                    if (lane < min(segc, cap)) seg_cand[seg * cap + lane] = slots[lane];
+                    if (lane == 0) seg_count[seg] = segc;
+                }
+                segc = 0;
+            }
+        }
+    }
+}
+
 #ifdef CG_DIAG
 // ===========================================================================
 // Alternative scan kernels, kept in the diagnostics build for the A/B measurements
@@ -783,11 +1014,6 @@ __global__ __launch_bounds__(64 * LW) void k_scan_lds(const uint8_t *__restrict_
 // ---------------------------------------------------------------------------
 #define PPW 66u  // pages per wave: a multiple of the 3-page load ring (one loop path: exact vmcnt waits)
 static_assert(CG_SEG == 64u * QPIECE, "a page is one 64-B piece per lane");
-#define DPP_WAVE_ROR1 0x13C
-
-__device__ __forceinline__ uint32_t wave_ror1(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, DPP_WAVE_ROR1, 0xf, 0xf, false);
-}
 
 // Exact test of every position of this lane's piece (nbytes at src, re-read from
 // L2: the rare path) from the warm-up state h0; counts the candidates and, with `out`,
@@ -958,7 +1184,8 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_wave(const uint8_t *__restr
 
 #ifdef CG_DIAG
 uint32_t g_scan_diag = 0;     // set by cg_diag_scan_mode (quad-kernel diag modes)
-uint32_t g_scan_variant = 0;  // set by cg_diag_scan_variant: 1 quad, 2 LDS-staged, 3 page per wave
+uint32_t g_scan_variant = 0;  // set by cg_diag_scan_variant: 1 quad, 2 LDS-staged, 3 page per wave, 4 k_scan, 5 flat rows
+uint32_t g_scan_spw_max = 0;  // set by cg_diag_scan_spw_max: k_scan_flat's segments-per-wave cap (0 = default)
 #endif
 
 void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint64_t mask_s, uint64_t mask_l,
@@ -966,10 +1193,11 @@ void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint
     if (nseg == 0) return;
     const uint64_t blocks = (nseg + SCAN2_T - 1) / SCAN2_T;
     // prefilter when the bits of mask_s & mask_l it tests leave hits rarer than ~1 per 16 KiB
+    // (averages >= 64 KiB with the v2020 masks)
     const bool pre = __builtin_popcountll((mask_s & mask_l) >> SCAN_SHIFT) >= 14;
 #ifdef CG_DIAG
     const bool pre_quad = __builtin_popcountll(mask_s & mask_l) >= 15;
-    if (g_scan_diag && pre_quad) {
+    if (g_scan_diag && pre_quad && g_scan_variant != 5) {
         auto k = g_scan_diag == 1   ? k_scan_quad<true, 1>
                  : g_scan_diag == 2 ? k_scan_quad<true, 2>
                  : g_scan_diag == 3 ? k_scan_quad<true, 3>
@@ -1002,9 +1230,48 @@ void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint
                            d_data, n, d_gear, mask_s, mask_l, cap, d_seg_count, d_seg_cand, nseg);
         return;
     }
+    if (g_scan_variant == 4) {
+        hipLaunchKernelGGL(pre ? k_scan<true> : k_scan<false>, dim3((uint32_t)blocks), dim3(SCAN2_T), 0, st, d_data,
+                           n, d_gear, mask_s, mask_l, cap, d_seg_count, d_seg_cand, nseg);
+        return;
+    }
 #endif
-    hipLaunchKernelGGL(pre ? k_scan<true> : k_scan<false>, dim3((uint32_t)blocks), dim3(SCAN2_T), 0, st, d_data, n,
-                       d_gear, mask_s, mask_l, cap, d_seg_count, d_seg_cand, nseg);
+    // k_scan_flat re-walks a whole 1 KiB row whenever its prefilter fires, k_scan only the
+    // lane's 64-B piece: with 14 prefilter bits (one firing per 16 rows) the two measure
+    // the same (config 4: 3.80 vs 3.86 ms per 16 GiB), with 16 (config 2) flat is 15 %
+    // faster (0.23 vs 0.27 ms per GiB; profiles/r02_v3_diag_scan.json)
+    bool flat = __builtin_popcountll((mask_s & mask_l) >> SCAN_SHIFT) >= 15;
+#ifdef CG_DIAG
+    if (g_scan_variant == 5) flat = pre;
+#endif
+    if (!flat) {
+        hipLaunchKernelGGL(pre ? k_scan<true> : k_scan<false>, dim3((uint32_t)blocks), dim3(SCAN2_T), 0, st, d_data,
+                           n, d_gear, mask_s, mask_l, cap, d_seg_count, d_seg_cand, nseg);
+        return;
+    }
+    // segments per wave: 4..64 -- enough waves for 16 per CU on 256 CUs, but runs of at most
+    // 256 KiB, so that the waves in flight (one stream each, advancing together) stay
+    // within a window of ~1 GiB rather than spread at a power-of-two stride of several MiB
+    // (measured: 4 MiB runs at config 4 read ~20 % slower)
+    uint64_t spw = (nseg + 4095) / 4096;
+    uint64_t spw_max = 64;
+#ifdef CG_DIAG
+    if (g_scan_spw_max) spw_max = g_scan_spw_max;
+#endif
+    spw = spw < 4 ? 4 : (spw > spw_max ? spw_max : (spw + 3) & ~3ull);
+    const uint64_t waves = (nseg + spw - 1) / spw;
+    const uint64_t wgs = (waves + SCAN2_T / 64 - 1) / (SCAN2_T / 64);
+    auto k = k_scan_flat<8, true>;
+#ifdef CG_DIAG
+    // variant 5: g_scan_diag bit 0 non-temporal loads, bit 1 16 rows in flight (else 8)
+    if (g_scan_variant == 5)
+        k = g_scan_diag == 1   ? k_scan_flat<8, true>
+            : g_scan_diag == 2 ? k_scan_flat<16, false>
+            : g_scan_diag == 3 ? k_scan_flat<16, true>
+                               : k_scan_flat<8, false>;
+#endif
+    hipLaunchKernelGGL(k, dim3((uint32_t)wgs), dim3(SCAN2_T), 0, st, d_data, n, d_gear, mask_s, mask_l, cap,
+                       d_seg_count, d_seg_cand, nseg, (uint32_t)spw);
 }
 
 // ---------------------------------------------------------------------------

@@ -374,6 +374,45 @@ def test_dpp_bank_mask_lane_probe(ca):
     assert out.tolist() == want
 
 
+@pytest.mark.parametrize("params", [FIX, (16 * 1024, 64 * 1024, 256 * 1024), S, D], ids=["fix", "16k", "S", "D"])
+def test_diag_scan_variants_agree(ca, params):
+    """The alternative candidate-scan kernels kept in the diagnostics build for DESIGN.md
+    §4's A/B (quad transpose, LDS-staged, page per wave, own segment per lane, the flat
+    row kernel's ring-depth / load-policy variants) give the product's descriptors on a
+    ragged multi-NAR batch, so the timings compared there are of correct kernels."""
+    from chunker_amd._lib import DIAG_LIB_PATH, diag_lib
+    from chunker_amd.chunking import DESC_DTYPE
+
+    if not DIAG_LIB_PATH.exists():
+        pytest.skip("diagnostics build not present (make -C chunker_amd/csrc diag)")
+    Dl = diag_lib()
+    Dl.cg_diag_scan_variant.argtypes = [ctypes.c_uint32]
+    Dl.cg_diag_scan_mode.argtypes = [ctypes.c_uint32]
+    sizes = [3 * 2**20 + 17, 2**20, 5 * 2**20 + 1000, 12345, 2 * 2**20 + 4095, 700 * 1024, 33]
+    nars = [rand_bytes(s, 900 + i) for i, s in enumerate(sizes)]
+    want, want_first = ca.chunking.chunk_batch_flat(np.concatenate(nars), np.cumsum([0] + sizes), *params, hash=B3)
+    flat = np.concatenate(nars)
+    offs = np.cumsum([0] + sizes).astype(np.uint64)
+    cap = ca.chunking.batch_capacity(offs, params[0])
+    try:
+        for v, mode in [(0, 0), (1, 0), (2, 0), (3, 0), (4, 0), (5, 0), (5, 1), (5, 2), (5, 3)]:
+            Dl.cg_diag_scan_variant(v)
+            Dl.cg_diag_scan_mode(mode)
+            out = np.zeros(cap, DESC_DTYPE)
+            first = np.zeros(len(sizes) + 1, np.uint64)
+            rc = Dl.cg_chunk_batch(flat.ctypes.data_as(ctypes.c_void_p), offs.ctypes.data_as(ctypes.c_void_p),
+                                   ctypes.c_size_t(len(sizes)), ctypes.c_uint64(params[0]),
+                                   ctypes.c_uint64(params[1]), ctypes.c_uint64(params[2]), ctypes.c_int(B3),
+                                   out.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(cap),
+                                   first.ctypes.data_as(ctypes.c_void_p))
+            assert rc == 0, f"variant {v}/{mode}: status {rc}"
+            assert np.array_equal(first, want_first), f"variant {v}/{mode}"
+            assert_same(out[: int(first[-1])], want, f"variant {v}/{mode}")
+    finally:
+        Dl.cg_diag_scan_variant(0)
+        Dl.cg_diag_scan_mode(0)
+
+
 @pytest.mark.parametrize("quad_max,pair_max", [(0, 0), (0, 3), (2, 3), (1 << 20, 0), (0, 1 << 20)],
                          ids=["one_lane", "pair_mixed", "quad_pair_one", "quad", "pair"])
 def test_sha_workgroup_kinds_agree(ca, O, quad_max, pair_max):
