@@ -174,7 +174,8 @@ def main():
         "traffic": None,
         "note": "digest stage: algorithmic bytes = every NAR byte once, / mean digest-stage duration over the "
                 "timed steps; scan stage reported separately",
-        "scan_kernel": {"kernel": "k_scan", "achieved": round(total_bytes / (scan_ms * 1e-3) / 1e9, 2),
+        "scan_kernel": {"kernel": scan_kernel_name(ca, params[1]),
+                        "achieved": round(total_bytes / (scan_ms * 1e-3) / 1e9, 2),
                         "frac": round(total_bytes / (scan_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                         "traffic": None},
     }
@@ -184,7 +185,7 @@ def main():
     traffic, src = pmc_traffic(args.config, dig_kernels)
     if traffic is not None:
         roofline["traffic"] = traffic
-        roofline["scan_kernel"]["traffic"] = pmc_traffic(args.config, ["k_scan"])[0]
+        roofline["scan_kernel"]["traffic"] = pmc_traffic(args.config, [roofline["scan_kernel"]["kernel"]])[0]
         roofline["traffic_source"] = src
 
     cpu = None
@@ -292,6 +293,17 @@ def sha_chain_floor(descs, n_nars, total_bytes, params, dig_ms):
     return {"longest_chunk_bytes": longest, "blocks": blocks, "tier": "quad" if quad else "pair",
             "cycles_per_round": cyc, "clock_GHz": 2.4, "floor_ms": round(floor_ms, 3),
             "frac": round(floor_ms / dig_ms, 4) if dig_ms else None}
+
+
+def scan_kernel_name(ca, avg):
+    """The K1 kernel launch_scan (scan.hip) picks for these params: k_scan_flat when the
+    prefilter sees >= 15 bits of mask_s & mask_l above bit 15, else k_scan."""
+    import math
+
+    _, masks = ca.get_cdc_tables()
+    bits = round(math.log2(avg))
+    both = int(masks[bits + 1]) & int(masks[bits - 1])
+    return "k_scan_flat" if bin(both >> 16).count("1") >= 15 else "k_scan"
 
 
 def pmc_traffic(config, kernels):
