@@ -45,7 +45,8 @@ EXPORTS = (
     "cg_stream_finish", "cg_stream_take", "cg_stream_pending", "cg_stream_bytes_consumed", "cg_stream_free",
 )
 # test hooks the product library exports beyond the header (tier caps, spin-guard limit)
-TEST_HOOKS = ("cg_test_sha_quad_max", "cg_test_sha_split_max", "cg_test_sha_spin_limit", "cg_test_cas_pair_max")
+TEST_HOOKS = ("cg_test_sha_quad_max", "cg_test_sha_split_max", "cg_test_sha_spin_limit", "cg_test_cas_pair_max",
+              "cg_test_fail_alloc")
 
 
 def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
@@ -132,6 +133,8 @@ def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
         getattr(L, name).restype = u32
     L.cg_test_cas_pair_max.argtypes = [ctypes.c_int64]
     L.cg_test_cas_pair_max.restype = ctypes.c_int64
+    L.cg_test_fail_alloc.argtypes = [ctypes.c_uint32]
+    L.cg_test_fail_alloc.restype = ctypes.c_uint32
     L.cg_set_profiling.argtypes = [i]
     L.cg_set_profiling.restype = None
     L.cg_last_stage_times.argtypes = [p, sz]

@@ -47,6 +47,9 @@ std::shared_ptr<const Tables> tables();
 // Fail-closed gate in front of every chunking entry point.
 int check_tables();
 
+// test hook (cg_test_fail_alloc): true when this device allocation is the one to fail
+bool test_alloc_fault();
+
 struct DevBuf {
     void *p = nullptr;
     size_t cap = 0;
@@ -56,7 +59,7 @@ struct DevBuf {
         p = nullptr;
         cap = 0;
         size_t want = bytes + bytes / 4 + 256;
-        hipError_t e = hipMalloc(&p, want);
+        hipError_t e = test_alloc_fault() ? hipErrorOutOfMemory : hipMalloc(&p, want);
         if (e != hipSuccess) {
             p = nullptr;
             return hip_fail(e, name, want);

@@ -63,6 +63,15 @@ int fail_limit(uint64_t attempted, const std::string &what) {
     return CG_E_BUFFER_LIMIT;
 }
 
+static std::atomic<uint32_t> g_fail_alloc{0};  // countdown: the allocation that takes it to 0 fails
+
+bool test_alloc_fault() {
+    uint32_t v = g_fail_alloc.load(std::memory_order_relaxed);
+    while (v != 0)
+        if (g_fail_alloc.compare_exchange_weak(v, v - 1, std::memory_order_relaxed)) return v == 1;
+    return false;
+}
+
 int hip_fail(hipError_t e, const char *what, uint64_t attempted) {
     if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) {
         (void)hipGetLastError();  // clear the sticky allocation error
@@ -718,6 +727,10 @@ int push_append(cg_push *h, const uint8_t *data, uint64_t len) {
 extern "C" {
 
 uint32_t cg_abi_version(void) { return CG_ABI_VERSION; }
+
+// Test hook: make the n-th device-buffer growth from now fail as out of memory (0 = off);
+// returns the previous countdown.
+uint32_t cg_test_fail_alloc(uint32_t n) { return cgrt::g_fail_alloc.exchange(n); }
 
 const char *cg_last_error_message(void) { return t_err.c_str(); }
 

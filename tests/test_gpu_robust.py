@@ -165,3 +165,28 @@ def test_push_handle_survives_a_failed_push(ca):
     got += pc.finish()
     assert got == want
     assert b"".join(c.payload for c in got) == data
+
+
+@pytest.mark.parametrize("nth", [1, 2])
+def test_push_handle_survives_failed_buffer_growth(ca, nth):
+    """a push that has to grow the device buffers and runs out of memory on
+    the first (nth=1) or the second (nth=2) of the two allocations reports
+    BufferLimitExceeded and leaves the handle holding its retained tail: the same slice
+    pushed again continues the stream exactly."""
+    data = np.random.default_rng(11).integers(0, 256, 3_000_000, dtype=np.uint8).tobytes()
+    params = (8_192, 32_768, 131_072)
+    want = ca.chunk_data(data, *params)
+    pc = ca.PushChunker(*params)
+    got = list(pc.push(data[:50_000]))
+    big = data[50_000:2_600_000]  # far past the buffers sized for the first push
+    ca.lib.cg_test_fail_alloc(nth)
+    try:
+        with pytest.raises(ca.BufferLimitExceededError):
+            pc.push(big)
+    finally:
+        ca.lib.cg_test_fail_alloc(0)
+    got += pc.push(big)
+    got += pc.push(data[2_600_000:])
+    got += pc.finish()
+    assert got == want
+    assert b"".join(c.payload for c in got) == data
