@@ -78,6 +78,37 @@ __device__ __forceinline__ uint64_t warmup_exact(const uint8_t *__restrict__ dat
     return hits ? g.s + (uint64_t)__builtin_ctzll(hits) : NONE;
 }
 
+// The same warm-up for one chunk on ONE lane (the speculative walk's verification,
+// one lane per chunk): first cut among the n <= 47 positions from s, or NONE.  The
+// bytes come in as 13 dword loads issued together (one memory round trip; byte loads
+// in the hash loop would make it 47 dependent ones), never reading at or past `lim`.
+__device__ __forceinline__ uint64_t warmup_lane(const uint8_t *__restrict__ data, const uint64_t *gear, uint64_t s,
+                                                uint32_t n, uint64_t lim, uint64_t cs, const CdcParams &P) {
+    const uint64_t a0 = s & ~3ull;
+    const uint32_t sh = (uint32_t)(s - a0);
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(data + a0);
+    uint32_t w[13];
+#pragma unroll
+    for (int i = 0; i < 13; ++i) w[i] = a0 + 4 * i + 4 <= lim ? q[i] : 0u;
+    if (a0 + 52 > lim) {  // the NAR's last bytes: finish the partial dword byte by byte
+        const uint64_t full = (lim - a0) / 4;
+        if (full < 13) {
+            uint32_t v = 0;
+            for (uint64_t b = a0 + 4 * full; b < lim; ++b) v |= (uint32_t)data[b] << (8 * (uint32_t)(b & 3));
+            w[full] = v;  // dynamic index: rare path
+        }
+    }
+    uint64_t h = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 47; ++i) {
+        const uint32_t j = sh + i;  // byte j of the dword window
+        const uint32_t byte = (w[j >> 2] >> (8 * (j & 3))) & 0xffu;
+        h = (h << 1) + gear[byte];
+        if (i < n && (h & (s + i < cs ? P.mask_s : P.mask_l)) == 0) return s + i;
+    }
+    return NONE;
+}
+
 // Windowed (48-byte) hash verdict for positions [lo, hi) of a dense segment,
 // 64 positions per pass; first hit or NONE.  Only reached for inputs with more
 // candidates than the per-segment slots.
@@ -208,14 +239,7 @@ __global__ __launch_bounds__(64) void k_walk(const uint8_t *__restrict__ data, c
                 if (rem > P.min) {
                     const Geo g = geometry(cj, rem, P);
                     const uint64_t wend = g.s + 47 < g.ce ? g.s + 47 : g.ce;
-                    uint64_t h = 0;
-                    for (uint64_t p = g.s; p < wend; ++p) {
-                        h = (h << 1) + gear[data[p]];
-                        if ((h & (p < g.cs ? P.mask_s : P.mask_l)) == 0) {
-                            my_cut = p;
-                            break;
-                        }
-                    }
+                    my_cut = warmup_lane(data, gear, g.s, (uint32_t)(wend - g.s), end, g.cs, P);
                 }
             }
             const uint64_t bal = __ballot(my_cut != NONE);
