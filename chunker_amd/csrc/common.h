@@ -46,9 +46,23 @@ size_t exclusive_scan_tmp_elems(uint64_t n);
 void launch_compact(const uint32_t *d_seg_count, const uint32_t *d_seg_cand, const uint64_t *d_eoff, uint32_t cap,
                     uint64_t nseg, uint64_t *d_entries, hipStream_t st);
 
+// Piece lists for the walk of large NARs (walk.hip, k_walk_pieces); np = 0: none.
+struct WalkPiecesHost {
+    const uint64_t *first = nullptr;  // device [n_nars + 1]
+    const uint32_t *nar = nullptr;    // device [np]
+    const uint64_t *base = nullptr;   // device [np]
+    uint32_t *count = nullptr;        // device [np]
+    uint64_t *exit = nullptr;         // device [np]
+    uint64_t *starts = nullptr;       // device, sum of per-piece capacities
+    uint64_t pb = 0, np = 0;
+};
+// The walk verifies candidate-list walks afterwards (and can use piece lists) when
+// mask_s is sparse enough that a cut inside a chunk's 47-byte warm-up is rare.
+inline bool walk_is_speculative(const CdcParams &p) { return __builtin_popcountll(p.mask_s) >= 14; }
 void launch_walk(const uint8_t *d_data, const uint64_t *d_gear, const uint64_t *d_entries, const uint64_t *d_eoff,
                  uint64_t nseg, const uint64_t *d_nar_off, const uint64_t *d_cap_base, uint64_t n_nars,
-                 CdcParams p, uint64_t *d_wchunk, uint32_t *d_nar_nchunks, hipStream_t st);
+                 CdcParams p, uint64_t *d_wchunk, uint32_t *d_nar_nchunks, const WalkPiecesHost &pieces,
+                 hipStream_t st);
 
 void launch_assemble(const uint64_t *d_nar_off, const uint64_t *d_cap_base, const uint64_t *d_wchunk,
                      const uint64_t *d_nar_first, uint64_t n_nars, void *d_out, uint64_t out_cap,

@@ -271,11 +271,31 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
     P.mask_s = tab->masks[bits + 1];
     P.mask_l = tab->masks[bits - 1];
 
-    // host staging: nar_off (n+1), cap_base (n+1), nar_first (n+1)
-    if ((rc = ws->stage.ensure(3 * (n_nars + 1) * sizeof(uint64_t)))) return rc;
+    // Walk pieces (walk.hip k_walk_pieces): NARs of at least two piece lengths are also
+    // walked piece by piece in parallel; a piece is long enough (32 max-size chunks, at
+    // least 8 MiB) for a walk started at its first byte to meet the NAR's own cut
+    // sequence within a few chunks.
+    const uint64_t pb = std::max<uint64_t>(32 * o.max, 8ull << 20);
+    uint64_t np = 0, pcap = 0;
+    if (cg::walk_is_speculative(P))
+        for (size_t i = 0; i < n_nars; ++i) {
+            const uint64_t k = (h_nar_off[i + 1] - h_nar_off[i]) / pb;
+            if (k >= 2) {
+                np += k;
+                pcap += capacity_of(h_nar_off[i + 1] - h_nar_off[i], o.min) + 2 * k;
+            }
+        }
+
+    // host staging: nar_off (n+1), cap_base (n+1), nar_first (n+1), then the piece
+    // tables: first (n+1), base (np), nar (np, u32)
+    const size_t stage_words = 4 * (n_nars + 1) + np + (np + 1) / 2;
+    if ((rc = ws->stage.ensure(stage_words * sizeof(uint64_t)))) return rc;
     uint64_t *s_off = ws->stage.as<uint64_t>();
     uint64_t *s_cap = s_off + (n_nars + 1);
     uint64_t *s_first = s_cap + (n_nars + 1);
+    uint64_t *s_pfirst = s_first + (n_nars + 1);
+    uint64_t *s_pbase = s_pfirst + (n_nars + 1);
+    uint32_t *s_pnar = reinterpret_cast<uint32_t *>(s_pbase + np);
     memcpy(s_off, h_nar_off, (n_nars + 1) * sizeof(uint64_t));
     uint64_t total_cap = 0;
     for (size_t i = 0; i < n_nars; ++i) {
@@ -283,6 +303,39 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
         total_cap += capacity_of(h_nar_off[i + 1] - h_nar_off[i], o.min);
     }
     s_cap[n_nars] = total_cap;
+    cg::WalkPiecesHost pieces;
+    if (np) {
+        uint64_t g = 0, lb = 0;
+        for (size_t i = 0; i < n_nars; ++i) {
+            s_pfirst[i] = g;
+            const uint64_t len = h_nar_off[i + 1] - h_nar_off[i], k = len / pb;
+            if (k < 2) continue;
+            for (uint64_t j = 0; j < k; ++j, ++g) {
+                const uint64_t plen = j + 1 < k ? pb : len - j * pb;
+                s_pbase[g] = lb;
+                s_pnar[g] = (uint32_t)i;
+                lb += capacity_of(plen, o.min) + 2;
+            }
+        }
+        s_pfirst[n_nars] = g;
+        if ((rc = ws->pc_first.ensure((n_nars + 1) * 8, "walk pieces"))) return rc;
+        if ((rc = ws->pc_base.ensure(np * 8, "walk pieces"))) return rc;
+        if ((rc = ws->pc_nar.ensure(np * 4, "walk pieces"))) return rc;
+        if ((rc = ws->pc_count.ensure(np * 4, "walk pieces"))) return rc;
+        if ((rc = ws->pc_exit.ensure(np * 8, "walk pieces"))) return rc;
+        if ((rc = ws->pc_starts.ensure(std::max<uint64_t>(lb, pcap) * 8, "walk pieces"))) return rc;
+        HIP_TRY(hipMemcpyAsync(ws->pc_first.p, s_pfirst, (n_nars + 1) * 8, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(ws->pc_base.p, s_pbase, np * 8, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(ws->pc_nar.p, s_pnar, np * 4, hipMemcpyHostToDevice, st));
+        pieces.first = ws->pc_first.as<uint64_t>();
+        pieces.nar = ws->pc_nar.as<uint32_t>();
+        pieces.base = ws->pc_base.as<uint64_t>();
+        pieces.count = ws->pc_count.as<uint32_t>();
+        pieces.exit = ws->pc_exit.as<uint64_t>();
+        pieces.starts = ws->pc_starts.as<uint64_t>();
+        pieces.pb = pb;
+        pieces.np = np;
+    }
 
     const uint64_t nseg = (total_len + CG_SEG - 1) / CG_SEG;
     const uint32_t slots = seg_slots(P);
@@ -322,7 +375,7 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
     if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_COMPACT], st));
     cg::launch_walk(d_data, ws->gear.as<uint64_t>(), ws->entries.as<uint64_t>(), ws->eoff.as<uint64_t>(), nseg,
                     ws->nar_off.as<uint64_t>(), ws->cap_base.as<uint64_t>(), n_nars, P, ws->wchunk.as<uint64_t>(),
-                    ws->nar_nchunks.as<uint32_t>(), st);
+                    ws->nar_nchunks.as<uint32_t>(), pieces, st);
     if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_WALK], st));
     cg::launch_exclusive_scan_u32(ws->nar_nchunks.as<uint32_t>(), ws->nar_first.as<uint64_t>(), n_nars, 0,
                                   ws->scan_tmp.as<uint64_t>(), st);

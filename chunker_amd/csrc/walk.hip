@@ -12,18 +12,6 @@
 
 namespace cg {
 
-__device__ __forceinline__ uint64_t lower_bound_u64(const uint64_t *__restrict__ a, uint64_t n, uint64_t key) {
-    uint64_t lo = 0, hi = n;
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (a[mid] < key)
-            lo = mid + 1;
-        else
-            hi = mid;
-    }
-    return lo;
-}
-
 #define NONE (~0ull)
 
 // Re-read of a value this wave stored earlier in the launch: an agent-scope load
@@ -173,18 +161,96 @@ __device__ uint64_t list_search(EntryWin &w, const uint64_t *__restrict__ entrie
     }
 }
 
+// Position the entry window at the first entry of the segment holding c (entries are
+// sorted by position, segment seg's at [eoff[seg], eoff[seg + 1])): one load.
+__device__ __forceinline__ void win_seek(EntryWin &w, const uint64_t *__restrict__ entries, uint64_t n_entries,
+                                         const uint64_t *__restrict__ eoff, uint64_t c, uint32_t lane) {
+    w.base = eoff[c / CG_SEG];
+    win_load(w, entries, n_entries, lane);
+}
+
+// Length of the chunk starting at c (NAR end `end`): exact warm-up or candidate list
+// only (spec), then the candidate list.
+__device__ __forceinline__ uint64_t chunk_len(const uint8_t *__restrict__ data, const uint64_t *gear, EntryWin &w,
+                                              const uint64_t *__restrict__ entries, uint64_t n_entries, uint64_t c,
+                                              uint64_t end, const CdcParams &P, bool exact, uint32_t lane) {
+    const uint64_t rem = end - c;
+    if (rem <= P.min) return rem;
+    const Geo g = geometry(c, rem, P);
+    uint64_t cut = exact ? warmup_exact(data, gear, g, P, lane) : NONE;
+    if (cut == NONE) {
+        const uint64_t q0 = g.s + 47 < g.ce ? g.s + 47 : g.ce;
+        cut = list_search(w, entries, n_entries, data, gear, q0, g.cs, g.ce, P, lane);
+    }
+    return cut == NONE ? g.R : cut - c;
+}
+
+// Speculative piece walks (large NARs).  A NAR of several piece lengths (pb bytes;
+// the last piece takes the remainder) is walked piece by piece in parallel: the wave of
+// piece k starts at the piece's first byte as if a chunk started there, and records the
+// start of every chunk it finds below the piece end plus the first start at or past it
+// (`exit`).  Cut sequences are a function of the previous cut alone, so once the NAR's
+// true sequence reaches any recorded start it follows that piece's list to its exit:
+// k_walk uses the lists as a cache of "the chunks from here", and walks normally only
+// until it lands on a cached start (typically one or two chunks into each piece).
+struct WalkPieces {
+    const uint64_t *first;   // [n_nars + 1] piece range of each NAR (empty: no pieces)
+    const uint32_t *nar;     // [np] the NAR of each piece
+    const uint64_t *base;    // [np] start of each piece's list in `starts`
+    uint32_t *count;         // [np] chunks recorded per piece
+    uint64_t *exit;          // [np] first chunk start at or past the piece end
+    uint64_t *starts;        // recorded chunk starts (absolute)
+    uint64_t pb;             // piece bytes
+    uint64_t np;             // pieces in the batch (0: no cache)
+};
+
+__global__ __launch_bounds__(64) void k_walk_pieces(const uint8_t *__restrict__ data,
+                                                    const uint64_t *__restrict__ gear_g,
+                                                    const uint64_t *__restrict__ entries,
+                                                    const uint64_t *__restrict__ eoff, uint64_t nseg,
+                                                    const uint64_t *__restrict__ nar_off, CdcParams P, WalkPieces wp) {
+    __shared__ uint64_t gear[256];
+    for (uint32_t i = threadIdx.x; i < 256; i += 64) gear[i] = gear_g[i];
+    __syncthreads();
+    const uint64_t g = blockIdx.x;
+    if (g >= wp.np) return;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t nar = wp.nar[g];
+    const uint64_t c0 = nar_off[nar], end = nar_off[nar + 1];
+    const uint64_t k = g - wp.first[nar], npc = wp.first[nar + 1] - wp.first[nar];
+    const uint64_t b = c0 + k * wp.pb, e = k + 1 < npc ? b + wp.pb : end;
+    const uint64_t n_entries = eoff[nseg];
+    uint64_t *out = wp.starts + wp.base[g];
+    EntryWin w;
+    win_seek(w, entries, n_entries, eoff, b, lane);
+    uint64_t c = b;
+    uint32_t cnt = 0;
+    while (c < e) {
+        const uint64_t len = chunk_len(data, gear, w, entries, n_entries, c, end, P, false, lane);
+        if (lane == 0) out[cnt] = c;
+        ++cnt;
+        c += len;
+    }
+    if (lane == 0) {
+        wp.count[g] = cnt;
+        wp.exit[g] = c;
+    }
+}
+
 // K2: one wave per NAR.  spec = 1: walk with the candidate list only, then verify
 // every chunk's 47-position warm-up in parallel (one lane per chunk) and re-walk
 // from the first chunk whose warm-up holds a cut (rare when mask_s has >= 14
 // bits; falls back to exact mode after 4 re-walks).  spec = 0: exact warm-up per
-// chunk.  Both produce the crate's cut sequence exactly.
+// chunk.  Both produce the crate's cut sequence exactly.  With piece lists (wp.np,
+// spec only) the walk takes whole runs of chunks from them (k_walk_pieces); they come
+// from the same candidate-list walk, so the verification below covers them too.
 __global__ __launch_bounds__(64) void k_walk(const uint8_t *__restrict__ data, const uint64_t *__restrict__ gear_g,
                                              const uint64_t *__restrict__ entries,
                                              const uint64_t *__restrict__ eoff, uint64_t nseg,
                                              const uint64_t *__restrict__ nar_off,
                                              const uint64_t *__restrict__ cap_base, uint64_t n_nars, CdcParams P,
                                              uint64_t *__restrict__ wchunk, uint32_t *__restrict__ nar_nchunks,
-                                             int spec) {
+                                             int spec, WalkPieces wp) {
     __shared__ uint64_t gear[256];
     for (uint32_t i = threadIdx.x; i < 256; i += 64) gear[i] = gear_g[i];
     __syncthreads();
@@ -194,31 +260,73 @@ __global__ __launch_bounds__(64) void k_walk(const uint8_t *__restrict__ data, c
     const uint64_t n_entries = eoff[nseg];
     const uint64_t c0 = nar_off[nar], end = nar_off[nar + 1];
     uint64_t *out = wchunk + 2 * cap_base[nar];
+    const uint64_t pk0 = wp.np ? wp.first[nar] : 0, npc = wp.np ? wp.first[nar + 1] - pk0 : 0;
 
     EntryWin w;
-    w.base = lower_bound_u64(entries, n_entries, ((c0 / CG_SEG) * CG_SEG) << 2);
-    win_load(w, entries, n_entries, lane);
+    win_seek(w, entries, n_entries, eoff, c0, lane);
 
     uint64_t k = 0, c = c0;
     uint32_t rewalks = 0;
     bool exact = spec == 0;
     for (;;) {
         const uint64_t k_start = k;
-        const EntryWin w_start = w;
+        uint64_t cur = ~0ull, ci = 0;  // piece being searched, and the search cursor in its list
+        uint64_t wbase = ~0ull, wv = ~0ull;  // the 64 list entries from wbase, one per lane
+        bool seek = false;
         while (c < end) {
-            const uint64_t rem = end - c;
-            uint64_t len;
-            if (rem <= P.min) {
-                len = rem;
-            } else {
-                const Geo g = geometry(c, rem, P);
-                uint64_t cut = exact ? warmup_exact(data, gear, g, P, lane) : NONE;
-                if (cut == NONE) {
-                    const uint64_t q0 = g.s + 47 < g.ce ? g.s + 47 : g.ce;
-                    cut = list_search(w, entries, n_entries, data, gear, q0, g.cs, g.ce, P, lane);
+            if (npc && !exact) {
+                const uint64_t kp = (c - c0) / wp.pb < npc ? (c - c0) / wp.pb : npc - 1;
+                if (kp != cur) {
+                    cur = kp;
+                    ci = 0;
+                    wbase = ~0ull;
                 }
-                len = cut == NONE ? g.R : cut - c;
+                const uint64_t pg = pk0 + kp;
+                const uint64_t *lst = wp.starts + wp.base[pg];
+                const uint64_t m = wp.count[pg];
+                // c among the piece's recorded starts (sorted) from the cursor on, 64 per
+                // wave-load, the loaded window kept while the cursor stays inside it
+                uint64_t hit = NONE;
+                while (ci < m) {
+                    const uint64_t blk = ci & ~63ull;
+                    if (blk != wbase) {
+                        wbase = blk;
+                        wv = blk + lane < m ? lst[blk + lane] : ~0ull;
+                    }
+                    const bool live = blk + lane >= ci;
+                    const uint64_t eq = __ballot(live && wv == c);
+                    if (eq) {
+                        hit = blk + (uint64_t)__builtin_ctzll(eq);
+                        break;
+                    }
+                    const uint64_t gt = __ballot(live && wv > c);
+                    if (gt) {
+                        ci = blk + (uint64_t)__builtin_ctzll(gt);
+                        break;
+                    }
+                    ci = blk + 64;
+                }
+                if (hit != NONE) {  // the rest of the piece's list is the NAR's sequence
+                    const uint64_t ex = wp.exit[pg];
+                    for (uint64_t t = hit; t < m; t += 64) {
+                        const uint64_t i = t + lane;
+                        if (i < m) {
+                            const uint64_t a = lst[i], nx = i + 1 < m ? lst[i + 1] : ex;
+                            out[2 * (k + i - hit)] = a;
+                            out[2 * (k + i - hit) + 1] = nx - a;
+                        }
+                    }
+                    k += m - hit;
+                    c = ex;
+                    seek = true;  // the entry window is behind c now
+                    continue;
+                }
             }
+            if (seek) {
+                win_seek(w, entries, n_entries, eoff, c, lane);
+                seek = false;
+            }
+            const uint64_t len = chunk_len(data, gear, w, entries, n_entries, c, end, P, exact, lane);
             if (lane == 0) {
                 out[2 * k] = c;
                 out[2 * k + 1] = len;
@@ -228,7 +336,7 @@ __global__ __launch_bounds__(64) void k_walk(const uint8_t *__restrict__ data, c
         }
         if (exact) break;
         // verify warm-ups of chunks [k_start, k): lane i takes chunk k_start + i + 64t
-        __syncthreads();  // out[] written by lane 0 is read by other lanes below
+        __syncthreads();  // out[] written by other lanes is read below
         uint64_t bad = NONE, bad_cut = 0;
         for (uint64_t b = k_start; b < k && bad == NONE; b += 64) {
             const uint64_t j = b + lane;
@@ -255,10 +363,7 @@ __global__ __launch_bounds__(64) void k_walk(const uint8_t *__restrict__ data, c
         if (lane == 0) out[2 * bad + 1] = bad_cut - cb;
         k = bad + 1;
         c = bad_cut;
-        // restart the entry window at the segment holding c (entries are sorted)
-        w = w_start;
-        w.base = lower_bound_u64(entries, n_entries, ((c / CG_SEG) * CG_SEG) << 2);
-        win_load(w, entries, n_entries, lane);
+        win_seek(w, entries, n_entries, eoff, c, lane);  // entries are sorted: restart at c's segment
         if (++rewalks >= 4) exact = true;
         __syncthreads();
     }
@@ -267,11 +372,17 @@ __global__ __launch_bounds__(64) void k_walk(const uint8_t *__restrict__ data, c
 
 void launch_walk(const uint8_t *d_data, const uint64_t *d_gear, const uint64_t *d_entries, const uint64_t *d_eoff,
                  uint64_t nseg, const uint64_t *d_nar_off, const uint64_t *d_cap_base, uint64_t n_nars,
-                 CdcParams p, uint64_t *d_wchunk, uint32_t *d_nar_nchunks, hipStream_t st) {
+                 CdcParams p, uint64_t *d_wchunk, uint32_t *d_nar_nchunks, const WalkPiecesHost &pieces,
+                 hipStream_t st) {
     if (n_nars == 0) return;
-    const int spec = __builtin_popcountll(p.mask_s) >= 14 ? 1 : 0;
+    const int spec = walk_is_speculative(p) ? 1 : 0;
+    WalkPieces wp{pieces.first, pieces.nar, pieces.base, pieces.count, pieces.exit, pieces.starts, pieces.pb,
+                  spec ? pieces.np : 0};
+    if (wp.np)
+        hipLaunchKernelGGL(k_walk_pieces, dim3((uint32_t)wp.np), dim3(64), 0, st, d_data, d_gear, d_entries, d_eoff,
+                           nseg, d_nar_off, p, wp);
     hipLaunchKernelGGL(k_walk, dim3((uint32_t)n_nars), dim3(64), 0, st, d_data, d_gear, d_entries, d_eoff, nseg,
-                       d_nar_off, d_cap_base, n_nars, p, d_wchunk, d_nar_nchunks, spec);
+                       d_nar_off, d_cap_base, n_nars, p, d_wchunk, d_nar_nchunks, spec, wp);
 }
 
 // One wave per NAR: copy the walker's (abs offset, length) list into the caller's

@@ -116,6 +116,27 @@ def test_speculative_walk_rewalks(ca, O, params, seed):
         assert_same(got[i], O.chunk_descriptors(part, *params, algo=SHA), f"part{i}")
 
 
+@pytest.mark.parametrize("params", [(4096, 16384, 65536), ODD2, (1024, 6000, 16384)], ids=["16k", "odd2", "fix"])
+def test_piece_walks(ca, O, params):
+    """NARs of two or more walk pieces (8 MiB here) are also walked piece by piece in
+    parallel from each piece's first byte, and the NAR's walk takes whole runs of
+    chunks from those lists once its sequence meets them: random NARs (sequences meet
+    within a chunk or two), long zero runs (no candidates: max-size cuts that meet only
+    when the piece length is a multiple of max, never for ODD2's 70001) and pieces
+    that are zeros and random in turn, plus NARs just under / over two pieces."""
+    rng = np.random.default_rng(31)
+    mib = 1 << 20
+    zr = np.zeros(20 * mib, np.uint8)
+    zr[3 * mib:5 * mib] = rng.integers(0, 256, 2 * mib, dtype=np.uint8)
+    zr[13 * mib + 77:15 * mib] = rng.integers(0, 256, 2 * mib - 77, dtype=np.uint8)
+    nars = [rng.integers(0, 256, 40 * mib + 123, dtype=np.uint8), zr,
+            rng.integers(0, 256, 16 * mib - 1, dtype=np.uint8), rng.integers(0, 256, 16 * mib + 1, dtype=np.uint8),
+            np.zeros(17 * mib + 5, np.uint8)]
+    got = ca.chunk_batch(nars, *params, hash=B3)
+    for i, nar in enumerate(nars):
+        assert_same(got[i], O.chunk_descriptors(nar, *params, algo=B3), f"nar{i} len={len(nar)}")
+
+
 @pytest.mark.parametrize("algo", [SHA, B3], ids=["sha256", "blake3"])
 def test_batch_ragged_unaligned(ca, O, algo):
     rng = np.random.default_rng(99)
