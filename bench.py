@@ -87,6 +87,11 @@ def main():
     # The installed GEAR table is the labelled placeholder (tables/README.md) and the
     # engine refuses to chunk with it unless opted in; the JSON says which table ran.
     os.environ.setdefault("CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR", "1")
+    # HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default) and streams
+    # sharing one serialise, so concurrent callers need more: the deployment setting
+    # DESIGN.md §7 / INTEGRATION.md recommend (single-batch value unchanged; K = 8 / 32
+    # batches in flight 38 / 51 -> 92 / 95 GiB/s).  Set before anything initialises HIP.
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
     import torch
     import torch.distributed as dist
