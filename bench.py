@@ -66,6 +66,8 @@ def parse_args():
     ap.add_argument("--no-concurrent", action="store_true", help="skip the K-batches-in-flight measurement")
     ap.add_argument("--concurrent", default="8,32", help="K values of the in-flight measurement")
     ap.add_argument("--concurrent-only", action="store_true", help="only the in-flight measurement (profiling)")
+    ap.add_argument("--hw-queues", type=int, default=16, choices=range(0, 33), metavar="0..32",
+                    help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's)")
     return ap.parse_args()
 
 
@@ -90,8 +92,10 @@ def main():
     # HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default) and streams
     # sharing one serialise, so concurrent callers need more: the deployment setting
     # DESIGN.md §7 / INTEGRATION.md recommend (single-batch value unchanged; K = 8 / 32
-    # batches in flight 38 / 51 -> 92 / 95 GiB/s).  Set before anything initialises HIP.
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+    # batches in flight 38 / 51 -> 92 / 95 GiB/s).  Set before anything initialises HIP;
+    # --hw-queues 0 keeps the environment's value.
+    if args.hw_queues:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
 
     import torch
     import torch.distributed as dist

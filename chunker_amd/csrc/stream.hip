@@ -16,6 +16,7 @@
 // bounded by the arena (slots are reused only after every group reading them has
 // completed); when no slot is free a push waits for the oldest group.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 
@@ -269,13 +270,18 @@ cg_stream *cg_stream_new(uint64_t min_size, uint64_t avg_size, uint64_t max_size
     h->o = o;
     h->algo = algo;
     h->device = dev;
-    // slot = the largest retained tail (< max) + one slice; groups of ~1/4 of the arena
+    // slot = the largest retained tail (< max) + one slice.  Digest lanes: one per
+    // hardware queue left beside the workspace stream's (GPU_MAX_HW_QUEUES, HIP's
+    // default 4; streams sharing a queue serialise), 3..8; groups of ~1/(lanes + 1) of
+    // the arena, so every lane can hold one while the next fills.
     const uint64_t slice = std::max<uint64_t>(slice_bytes ? slice_bytes : 8ull << 20, 4096);
     h->slot_bytes = (o.max + slice + 256 + 255) & ~255ull;
     const uint64_t budget = inflight_bytes ? inflight_bytes : 512ull << 20;
     h->nslots = std::max<uint64_t>(budget / h->slot_bytes, 4);
-    h->group_bytes = std::max<uint64_t>(h->nslots * h->slot_bytes / 4, slice);
-    const int nlanes = 3;
+    int queues = 4;
+    if (const char *q = std::getenv("GPU_MAX_HW_QUEUES")) queues = std::atoi(q) > 0 ? std::atoi(q) : 4;
+    const int nlanes = std::min(std::max(queues - 1, 3), 8);
+    h->group_bytes = std::max<uint64_t>(h->nslots * h->slot_bytes / (uint64_t)(nlanes + 1), slice);
     if (!(rc = acquire(&h->ws)) && !(rc = h->arena.ensure(h->nslots * h->slot_bytes, "stream arena"))) {
         const hipError_t e = hipEventCreateWithFlags(&h->ev_bytes, hipEventDisableTiming);
         if (e != hipSuccess) rc = hip_fail(e, "hipEventCreate");

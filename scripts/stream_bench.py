@@ -14,6 +14,7 @@ Every GPU variant is checked chunk for chunk against the eager result."""
 import os
 os.environ.setdefault("CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR", "1")  # placeholder GEAR: see tables/README.md
 os.environ.pop("CHUNKER_READ_SLICE_CAP_BYTES", None)  # the reference's default sizing
+os.environ["GPU_MAX_HW_QUEUES"] = "16"  # as bench.py; before HIP initialises
 import ctypes  # noqa: E402
 import io  # noqa: E402
 import json  # noqa: E402
@@ -31,7 +32,8 @@ N = 1 << 30
 SL = 8 << 20
 data, _ = synth_nars([N])
 raw = data.tobytes()
-res = {"workload": "1 GiB synthetic NAR stream, SHA-256, 256K/1M/4M, 8 MiB reads"}
+res = {"workload": "1 GiB synthetic NAR stream, SHA-256, 256K/1M/4M, 8 MiB reads",
+       "hw_queues": os.environ["GPU_MAX_HW_QUEUES"]}
 eager = ca.chunk_descriptors_array(data)
 ref = [(int(d["offset"]), int(d["length"]), bytes(d["hash"])) for d in eager]
 res["chunks"] = len(ref)
