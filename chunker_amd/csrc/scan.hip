@@ -318,32 +318,15 @@ __device__ __forceinline__ uint64_t block_partial(const uint64_t (&g)[4][4]) {
 }
 
 template <uint32_t FLAT_D, bool NT>
-__global__ __launch_bounds__(SCAN2_T) void k_scan_flat(const uint8_t *__restrict__ data, uint64_t n,
+__global__ __launch_bounds__(SCAN2_T) void k_scan_flat(const uint8_t *data, uint64_t n,
                                                       const uint64_t *__restrict__ gear_g, uint64_t mask_s,
                                                       uint64_t mask_l, uint32_t cap, uint32_t *__restrict__ seg_count,
                                                       uint32_t *__restrict__ seg_cand, uint64_t nseg, uint32_t spw) {
     __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * GEAR_COPIES];
     __shared__ uint32_t s_slots[SCAN2_T / 64][64];  // the open segment's candidate slots, per wave
-    for (uint32_t i = threadIdx.x; i < 256 * GEAR_COPIES; i += SCAN2_T)
-        s_gear[i] = gear_g[i / GEAR_COPIES] << SCAN_SHIFT;
-    __syncthreads();
-    const char *gbase = reinterpret_cast<const char *>(s_gear);
-
     const uint32_t lane = threadIdx.x & 63u;
-    uint32_t *slots = s_slots[threadIdx.x >> 6];
     const uint64_t seg0 = ((uint64_t)blockIdx.x * (SCAN2_T / 64) + (threadIdx.x >> 6)) * spw;
-    if (seg0 >= nseg) return;  // whole wave (uniform)
-    const uint32_t lo8 = (threadIdx.x & 31u) * 8u;
-    uint32_t ad[2][4];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) ad[i][b] = lo8;
-    const uint64_t ms = mask_s << SCAN_SHIFT, ml = mask_l << SCAN_SHIFT;
-    const uint32_t mh = (uint32_t)((mask_s & mask_l) >> (32 - SCAN_SHIFT));
-    const uint32_t m0 = lane == 0 ? 0xffffffffu : 0u;  // lane-0 select mask (bitop3 0xCA: m ? a : b)
-    const uint32_t ms_lo = (uint32_t)ms, ms_hi = (uint32_t)(ms >> 32), ml_lo = (uint32_t)ml, ml_hi = (uint32_t)(ml >> 32);
-
+    const bool active = seg0 < nseg;  // whole wave (uniform)
     const uint64_t r0 = seg0 * CG_SEG;
     const uint64_t nrow64 = (uint64_t)spw * FLAT_RPS;  // a multiple of FLAT_D (spw even)
     // Loads are unconditional and never leave the batch: a block past its end reads the last
@@ -358,19 +341,42 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan_flat(const uint8_t *__restrict
         return uint4{x.x, x.y, x.z, x.w};
     };
     static_assert(FLAT_D % FLAT_RPS == 0, "a ring trip ends on a segment boundary");
-    const uint64_t end_rel = n - r0;  // rows reaching past it hold the batch end (a partial block)
+    // this thread's Gear entry, then the row before the run (lanes 61..63 feed this run's
+    // first row) and the first FLAT_D rows: one memory round trip before the table fill
+    static_assert(SCAN2_T == 2 * 256 && GEAR_COPIES == 32, "two threads per Gear entry, 16 copies each");
+    const uint32_t ge = threadIdx.x >> 1;
+    const uint64_t gv = gear_g[ge] << SCAN_SHIFT;
     uint4 ring[FLAT_D];
 #pragma unroll
-    for (uint32_t i = 0; i < FLAT_D; ++i) ring[i] = blk(i);
+    for (uint32_t i = 0; i < FLAT_D; ++i) ring[i] = blk(active ? i : 0);
+    const bool has_pro = active && r0 >= FLAT_ROW;
+    const uint4 pro = *reinterpret_cast<const uint4 *>(data + (has_pro ? r0 - FLAT_ROW + 16u * lane : 0));
+    __builtin_amdgcn_sched_barrier(0);  // every load above is issued before the fill waits for gv
+    // copies rotated by the entry so the 32 threads of a parity write 32 distinct banks
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) s_gear[ge * GEAR_COPIES + (((threadIdx.x & 1u) * 16u + j + ge) & 31u)] = gv;
+    __syncthreads();
+    if (!active) return;
+    const char *gbase = reinterpret_cast<const char *>(s_gear);
+    uint32_t *slots = s_slots[threadIdx.x >> 6];
+    const uint32_t lo8 = (threadIdx.x & 31u) * 8u;
+    uint32_t ad[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) ad[i][b] = lo8;
+    const uint64_t ms = mask_s << SCAN_SHIFT, ml = mask_l << SCAN_SHIFT;
+    const uint32_t mh = (uint32_t)((mask_s & mask_l) >> (32 - SCAN_SHIFT));
+    const uint32_t m0 = lane == 0 ? 0xffffffffu : 0u;  // lane-0 select mask (bitop3 0xCA: m ? a : b)
+    const uint32_t ms_lo = (uint32_t)ms, ms_hi = (uint32_t)(ms >> 32), ml_lo = (uint32_t)ml, ml_hi = (uint32_t)(ml >> 32);
+    const uint64_t end_rel = n - r0;  // rows reaching past it hold the batch end (a partial block)
 
-    // the row before the run (lanes 61..63 feed this run's first row); zero state at the
-    // batch start, as the crate's hash restart
+    // zero state at the batch start, as the crate's hash restart
     uint64_t R1 = 0, R2 = 0;
     uint32_t R3 = 0;
-    if (r0 >= FLAT_ROW) {
-        const uint4 v = *reinterpret_cast<const uint4 *>(data + r0 - FLAT_ROW + 16u * lane);
+    if (has_pro) {
         uint64_t g[4][4];
-        block_lookups(gbase, ad, v, g);
+        block_lookups(gbase, ad, pro, g);
         const uint64_t P = block_partial(g);
         R1 = ((uint64_t)wave_ror1((uint32_t)(P >> 32)) << 32) | wave_ror1((uint32_t)P);
         R2 = ((uint64_t)wave_ror1((uint32_t)(R1 >> 32)) << 32) | wave_ror1((uint32_t)R1);

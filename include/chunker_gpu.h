@@ -117,7 +117,8 @@ void cg_push_free(cg_push *h);
  * is bounded by `inflight_bytes` (0 = 512 MiB): an arena of slots of max_size +
  * slice_bytes (0 = 8 MiB, the reference's read size, :713-716) bytes, each reused only
  * after the digests reading it completed -- a push waits for them when none is free.
- * take with wait = 0 returns what has completed; wait != 0 blocks until at least one
+ * Digests run on one HIP stream per hardware queue beside the call's own
+ * (GPU_MAX_HW_QUEUES - 1, 3..8, read at cg_stream_new).  take with wait = 0 returns what has completed; wait != 0 blocks until at least one
  * chunk is ready or nothing is pending.  push after finish -> CG_E_INVALID_OPTIONS.
  * Single owner, like cg_push. */
 typedef struct cg_stream cg_stream;
