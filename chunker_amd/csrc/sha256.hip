@@ -6,6 +6,8 @@
 // only parallelism is across chunks.  One lane owns one chunk; its blocks are
 // loaded as aligned dwords and realigned + byte-swapped with one v_perm_b32 per
 // word (chunk offsets are arbitrary bytes).  Rotates are v_alignbit_b32.
+#include <algorithm>
+
 #include "common.h"
 
 namespace cg {
@@ -813,15 +815,19 @@ constexpr uint32_t g_sha_mode = 0;
 uint32_t g_sha_split_max = 256;
 // Quad workgroups per launch (8 longest chunks each).  Test hook cg_test_sha_quad_max.
 uint32_t g_sha_quad_max = 256;
+// Quad workgroups when the batch fills the GPU: a few, for the longest chunks only
+// (config 4: 32 -> digest 23.7 -> 21.7 ms; all 256 would hold back the one-lane
+// workgroups queued behind them, 26 ms).  Test hook cg_test_sha_quad_fill.
+uint32_t g_sha_quad_fill = 32;
 // Spin-guard limit (sleeps per wait) of the producer/consumer hand-off: test hook
 // cg_test_sha_spin_limit.
 uint32_t g_sha_spin_limit = 1u << 26;
 
 // Workgroup tiers for a launch of up to max_chunks chunks, `expected` of them
 // likely (total bytes / (min + avg)).  A quad workgroup holds a whole workgroup's
-// LDS for 8 chunks, so quads are used only when the one-lane tier left behind them
-// fits in one round of workgroups (<= 256 x 64 chunks): on a batch that fills the
-// GPU (config 4) they would hold back the one-lane workgroups queued behind them.
+// LDS for 8 chunks, so up to 256 quads are used only when the one-lane tier left
+// behind them fits in one round of workgroups (<= 256 x 64 chunks); on a batch that
+// fills the GPU (config 4) only g_sha_quad_fill of them, for the longest chunks.
 uint32_t sha256_grid(uint64_t max_chunks, uint64_t expected, uint32_t *nquad_out, uint32_t *npair_out) {
     auto tiers = [&](uint64_t qmax, uint64_t &nq, uint64_t &np) {
         nq = (max_chunks + 7) / 8;
@@ -832,7 +838,7 @@ uint32_t sha256_grid(uint64_t max_chunks, uint64_t expected, uint32_t *nquad_out
     };
     uint64_t nq, np;
     tiers(g_sha_quad_max, nq, np);
-    if (expected > 8 * nq + 32 * np + 256 * 64) tiers(0, nq, np);
+    if (expected > 8 * nq + 32 * np + 256 * 64) tiers(std::min<uint64_t>(g_sha_quad_max, g_sha_quad_fill), nq, np);
     const uint64_t rest = max_chunks > 8 * nq + 32 * np ? max_chunks - 8 * nq - 32 * np : 0;
     if (nquad_out) *nquad_out = (uint32_t)nq;
     if (npair_out) *npair_out = (uint32_t)np;
@@ -952,6 +958,12 @@ extern "C" uint32_t cg_test_sha_split_max(uint32_t v) {
 extern "C" uint32_t cg_test_sha_spin_limit(uint32_t v) {
     const uint32_t old = cg::g_sha_spin_limit;
     cg::g_sha_spin_limit = v;
+    return old;
+}
+
+extern "C" uint32_t cg_test_sha_quad_fill(uint32_t v) {
+    const uint32_t old = cg::g_sha_quad_fill;
+    cg::g_sha_quad_fill = v;
     return old;
 }
 
