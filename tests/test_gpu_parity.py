@@ -485,3 +485,47 @@ def test_full_size_config2_batch(ca, O):
     nt = min(16, os.cpu_count() or 1)
     for i, nar in enumerate(nars):
         assert_same(got[i], O.chunk_descriptors(nar, *D, algo=SHA, nthreads=nt), f"nar{i}")
+
+
+def _random_options(rng, large):
+    """Valid (min, avg, max) spread over the option space (src/chunking.rs:190-231),
+    log-uniform, so every scan / walk path is drawn: dense masks (k_scan<false>, exact
+    walk), 14 prefilter bits (k_scan + speculative walk), >= 15 (k_scan_flat, drawn
+    with `large`: averages of 256 KiB .. 4 MiB)."""
+    avg = int(2 ** (rng.uniform(18, 22) if large else rng.uniform(8, 18)))
+    mn = int(min(avg, 2 ** rng.uniform(6, min(20, np.log2(avg) + 0.01))))
+    mx = int(max(avg, 1024, 2 ** rng.uniform(np.log2(max(avg, 1024)), 24)))
+    return max(mn, 64), avg, min(mx, 16 * 1024 * 1024)
+
+
+def _random_nar(rng, n):
+    kind = rng.integers(0, 4)
+    if kind == 0:
+        return rng.integers(0, 256, n, dtype=np.uint8)
+    if kind == 1:  # low entropy: few symbols
+        return rng.integers(0, 3, n, dtype=np.uint8) * 85
+    if kind == 2:  # zero runs with random islands
+        a = np.zeros(n, np.uint8)
+        for _ in range(int(rng.integers(0, 6))):
+            s = int(rng.integers(0, max(n, 1)))
+            e = min(n, s + int(rng.integers(1, 200_000)))
+            a[s:e] = rng.integers(0, 256, e - s, dtype=np.uint8)
+        return a
+    return fixture_bytes(n)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_randomized_options_batches(ca, O, seed):
+    """Property sweep (in the spirit of tests/proptest_suite.rs): random valid options,
+    random ragged batches of random / low-entropy / zero-run / fixture-pattern NARs, both
+    digests; every NAR bit-exact vs the oracle."""
+    rng = np.random.default_rng(1000 + seed)
+    params = _random_options(rng, large=seed % 2 == 0)
+    sizes = [int(x) for x in rng.integers(0, 3 * 1024 * 1024, int(rng.integers(1, 9)))]
+    if seed % 3 == 0:
+        sizes.append(int(rng.integers(16, 40)) * 1024 * 1024 + int(rng.integers(0, 4096)))  # multi-piece walk
+    nars = [_random_nar(rng, n) for n in sizes]
+    algo = SHA if seed % 4 < 2 else B3
+    got = ca.chunk_batch(nars, *params, hash=algo)
+    for i, nar in enumerate(nars):
+        assert_same(got[i], O.chunk_descriptors(nar, *params, algo=algo), f"{params} nar{i} len={len(nar)}")
