@@ -451,10 +451,10 @@ __device__ __forceinline__ void sha_rounds_split(uint32_t st[4], const uint4 (&c
     uint32_t x0 = st[0], x1 = st[1], x2 = st[2], x3 = st[3];
     const uint32_t r0 = __hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     SPL32(0, cur)
-    if (prefetch) {
-        if (__builtin_expect(r0 <= knext, 0)) wait_ready(ready, knext, false);
-        load_w8(nxt, next_row);
-    }
+    if (__builtin_expect(prefetch && r0 <= knext, 0)) wait_ready(ready, knext, false);
+    // unconditional (after the last block it reads a stale ring slot nobody uses): a load
+    // inside a branch made the compiler drain lgkmcnt at the join, an LDS round trip per block
+    load_w8(nxt, next_row);
     SPL32(32, cur)
     st[0] = active ? st[0] + x0 : st[0];
     st[1] = active ? st[1] + x1 : st[1];
