@@ -106,10 +106,8 @@ __device__ __forceinline__ void sha_rounds_pf(uint32_t st[8], const uint4 (&cur)
     SHA_8RND(8, cur);
     SHA_8RND(16, cur);
     SHA_8RND(24, cur);
-    if (prefetch) {
-        if (__builtin_expect(r0 <= knext, 0)) wait_ready(ready, knext, false);
-        load_w(nxt, next_row);
-    }
+    if (__builtin_expect(prefetch && r0 <= knext, 0)) wait_ready(ready, knext, false);
+    load_w(nxt, next_row);  // unconditional, as in sha_rounds_split
     SHA_8RND(32, cur);
     SHA_8RND(40, cur);
     SHA_8RND(48, cur);
