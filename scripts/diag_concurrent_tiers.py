@@ -1,0 +1,31 @@
+"""Diagnostic: aggregate rate of K config-2 batches in flight (bench.py's `concurrent`
+measurement) by SHA-256 workgroup tiers: the product's latency tiers (quads and pairs
+for the longest chunks) vs one lane per chunk everywhere (cg_test_sha_quad_max /
+cg_test_sha_split_max = 0), which spends 5x fewer lane-instructions per round."""
+import os
+os.environ.setdefault("CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR", "1")
+os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("CHUNKER_AMD_DIAG_HW_QUEUES", "16")
+import argparse  # noqa: E402
+import json  # noqa: E402
+import sys  # noqa: E402
+
+sys.path.insert(0, ".")
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import chunker_amd as ca  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--concurrent", default="1,8,32")
+ap.add_argument("--zeros", action="store_true")
+args = ap.parse_args()
+n_per, nar_bytes, params, algo, _ = bench.CONFIGS["c2"]
+res = {"hw_queues": os.environ["GPU_MAX_HW_QUEUES"]}
+for name, q, p in [("latency_tiers", 256, 256), ("one_lane", 0, 0), ("pairs_only", 0, 256)]:
+    oq, op = ca.lib.cg_test_sha_quad_max(q), ca.lib.cg_test_sha_split_max(p)
+    try:
+        res[name] = bench.concurrent_rates(ca, torch, args, n_per, nar_bytes, params, algo)
+    finally:
+        ca.lib.cg_test_sha_quad_max(oq)
+        ca.lib.cg_test_sha_split_max(op)
+print(json.dumps(res))
