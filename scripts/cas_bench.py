@@ -2,11 +2,11 @@
 cg_node_put_batch_device (FastCDC + SHA-256 descriptors + one SHAKE-256 ContentId per
 chunk + one manifest id per NAR) next to cg_chunk_batch_device alone, and the CAS
 kernel by itself over the same chunk spans (cg_cas_ids_device).  Stage times come
-import os
-os.environ.setdefault("CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR", "1")  # placeholder GEAR: see tables/README.md
 from the library's HIP events (cg_last_stage_times; stage 6 = CAS on the side
 stream).  CPU baseline: oracle.node_put (hashlib SHAKE-256 + the C FastCDC/SHA-NI
 port) on a 16-thread pool over a bounded sample of NARs."""
+import os
+os.environ.setdefault("CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR", "1")  # placeholder GEAR: see tables/README.md
 import argparse
 import json
 import sys

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-.}"
 R=$(pwd)
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-TAG=${TAG:-r01}
+TAG=${TAG:-r02}
 timeout -k 10 300 python -u -m pytest tests/test_gpu_cas.py -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_cas.log 2>&1 \
  && echo "cas tests ok" \
  && timeout -k 10 600 python -u -m pytest tests/ -x -q -m "gpu and not slow" --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 \
