@@ -551,7 +551,9 @@ class ChunkStream:
             self._read_async()
             a = _as_u8(buf)
             _check(lib.cg_stream_push(self._h, _ptr(a), len(a)))
-            keep = buf if isinstance(buf, bytes) else a.tobytes()
+            # payloads are views of what was read: keep immutable buffers as they are
+            # (bytes, read-only views), copy anything the reader might reuse
+            keep = buf if isinstance(buf, bytes) or (isinstance(buf, memoryview) and buf.readonly) else a.tobytes()
             self._segs.append((self._pushed, memoryview(keep)))
             self._pushed += len(keep)
 
