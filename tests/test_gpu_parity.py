@@ -529,3 +529,55 @@ def test_randomized_options_batches(ca, O, seed):
     got = ca.chunk_batch(nars, *params, hash=algo)
     for i, nar in enumerate(nars):
         assert_same(got[i], O.chunk_descriptors(nar, *params, algo=algo), f"{params} nar{i} len={len(nar)}")
+
+
+def _dense_region(O, rng, prefix, nbytes, mask):
+    """Bytes that, appended to `prefix`, make about every 2nd-32nd position a candidate
+    for `mask` (each byte pair chosen among 65536 so the windowed hash after it has the
+    mask's bits clear): dense segments -- more candidates than the per-segment slots --
+    that the scan must mark and the walker rescan exactly."""
+    G = O.GEAR.astype(np.uint64)
+    pair = (np.uint64(2) * G[:, None] + G[None, :]).reshape(-1)
+    m64 = (1 << 64) - 1
+    h = 0
+    for x in prefix[-64:]:
+        h = (h * 2 + int(G[x])) & m64
+    out = np.empty(nbytes, np.uint8)
+    with np.errstate(over="ignore"):
+        for i in range(0, nbytes, 2):
+            cand = np.uint64((4 * h) & m64) + pair
+            ok = np.flatnonzero((cand & np.uint64(mask)) == 0)
+            k = int(ok[0]) if len(ok) else int(rng.integers(0, 65536))
+            out[i], out[i + 1] = k >> 8, k & 255
+            h = int(cand[k])
+    return out
+
+
+@pytest.mark.parametrize("params", [D, S], ids=["D_flat", "S_kscan"])
+def test_dense_candidate_segments(ca, O, params):
+    """Adversarial bytes with candidates at a large fraction of positions, for the
+    L mask past the chunk's center and for the S mask before it: every such 4 KiB
+    segment overflows its candidate slots, the scan (k_scan_flat at D, k_scan at S)
+    marks it dense and the walker re-scans it exactly."""
+    import math
+
+    rng = np.random.default_rng(77)
+    bits = round(math.log2(params[1]))
+    ms, ml = int(O.MASKS[bits + 1]), int(O.MASKS[bits - 1])
+    a = rng.integers(0, 256, params[1] + params[1] // 3, dtype=np.uint8)  # past center: L region
+    b = _dense_region(O, rng, a, 48 * 1024, ml)
+    c = rng.integers(0, 256, params[0] + 5000, dtype=np.uint8)
+    d = _dense_region(O, rng, np.concatenate([a, b, c]), 24 * 1024, ms)  # S candidates
+    e = rng.integers(0, 256, 2 * params[2], dtype=np.uint8)
+    nar = np.concatenate([a, b, c, d, e])
+    # premise: the crafted regions hold far more candidates per 4 KiB than any slot list
+    m64, g = (1 << 64) - 1, [int(v) for v in O.GEAR]
+    for lo, hi, mask in ((len(a), len(a) + len(b), ml), (len(a) + len(b) + len(c), len(nar) - len(e), ms)):
+        h, hits = 0, 0
+        for p in range(lo - 64, lo + 4096):
+            h = (h * 2 + g[nar[p]]) & m64
+            hits += p >= lo and (h & mask) == 0
+        assert hits > 32, f"only {hits} candidates in the first crafted segment"  # slots: 16 here
+    for algo in (SHA, B3):
+        got = ca.chunk_descriptors_array(nar, *params, hash=algo)
+        assert_same(got, O.chunk_descriptors(nar, *params, algo=algo), f"algo={algo}")
