@@ -111,32 +111,38 @@ __device__ __forceinline__ void keccak_f(uint32_t lo[25], uint32_t hi[25]) {
 // half.  ~120 VALU per round instead of ~180, so the longest span's chain is ~1.5x
 // shorter.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t partner(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
+// The partner's value (quad_perm [1,0,3,2]).  A v_mov_b32 -- DPP or not -- issues in ~8
+// clocks on gfx950 against ~4.9 for a DPP ALU op (scripts/diag_ops.py,
+// profiles/r02_v7_diag_ops_mov.json), so the move is written as an add of an opaque
+// zero, which the compiler's DPP combine turns into one v_add_u32_dpp.
+__device__ __forceinline__ uint32_t partner(uint32_t v, uint32_t zero) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true) + zero;
 }
 
 template <int R>
-__device__ __forceinline__ uint32_t rot_pair(uint32_t own) {
+__device__ __forceinline__ uint32_t rot_pair(uint32_t own, uint32_t zero) {
     if constexpr (R == 0) {
         return own;
     } else if constexpr (R < 32) {
-        return __builtin_amdgcn_alignbit(own, partner(own), 32 - R);
+        return __builtin_amdgcn_alignbit(own, partner(own, zero), 32 - R);
     } else if constexpr (R == 32) {
-        return partner(own);
+        return partner(own, zero);
     } else {
-        return __builtin_amdgcn_alignbit(partner(own), own, 64 - R);
+        return __builtin_amdgcn_alignbit(partner(own, zero), own, 64 - R);
     }
 }
 
 template <int I>
-__device__ __forceinline__ void rho_pi_pair(const uint32_t *a, uint32_t *b) {
+__device__ __forceinline__ void rho_pi_pair(const uint32_t *a, uint32_t *b, uint32_t zero) {
     constexpr int x = I % 5, y = I / 5, j = y + 5 * ((2 * x + 3 * y) % 5);
-    b[j] = rot_pair<KR(I)>(a[I]);
-    if constexpr (I < 24) rho_pi_pair<I + 1>(a, b);
+    b[j] = rot_pair<KR(I)>(a[I], zero);
+    if constexpr (I < 24) rho_pi_pair<I + 1>(a, b, zero);
 }
 
 // hmask = 0 on the low lane, ~0 on the high lane
 __device__ __forceinline__ void keccak_f_pair(uint32_t a[25], uint32_t hmask) {
+    uint32_t zero = 0;
+    asm volatile("" : "+v"(zero));  // a VGPR the compiler cannot fold away (see partner)
 #pragma unroll
     for (int round = 0; round < 24; ++round) {
         uint32_t c[5], b[25];
@@ -144,11 +150,11 @@ __device__ __forceinline__ void keccak_f_pair(uint32_t a[25], uint32_t hmask) {
         for (int x = 0; x < 5; ++x) c[x] = x3(x3(a[x], a[x + 5], a[x + 10]), a[x + 15], a[x + 20]);
 #pragma unroll
         for (int x = 0; x < 5; ++x) {
-            const uint32_t d = rot_pair<1>(c[(x + 1) % 5]);
+            const uint32_t d = rot_pair<1>(c[(x + 1) % 5], zero);
 #pragma unroll
             for (int y = 0; y < 5; ++y) a[x + 5 * y] = x3(a[x + 5 * y], c[(x + 4) % 5], d);
         }
-        rho_pi_pair<0>(a, b);
+        rho_pi_pair<0>(a, b, zero);
 #pragma unroll
         for (int y = 0; y < 5; ++y)
 #pragma unroll

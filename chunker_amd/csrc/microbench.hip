@@ -252,7 +252,8 @@ extern "C" float cg_diag_read_pattern(const uint8_t *d_data, uint32_t run_log2, 
 // kind: 0 v_add_u32, 1 v_lshl_add_u64, 2 v_perm_b32, 3 v_add_co_u32+v_addc_co_u32
 // pair (counted as 2), 4 v_alignbit_b32, 5 v_bitop3_b32, 6 v_lshlrev_b64,
 // 7 v_mov_b32_dpp quad_perm, 8 v_add3_u32, 9 v_cndmask_b32, 10 dependent v_lshl_add_u64
-// chain (one chain), 11 dependent v_add_u32 chain (one chain).
+// chain (one chain), 11 dependent v_add_u32 chain (one chain), 12 v_xor_b32_dpp quad_perm,
+// 13 v_add_u32_dpp row_shl:4, 14 v_mov_b32_dpp row_shl:4, 15 plain v_mov_b32.
 // ---------------------------------------------------------------------------
 namespace cg {
 template <int KIND>
@@ -277,6 +278,12 @@ __device__ __forceinline__ void op16(uint32_t (&r)[16], uint64_t (&q)[8]) {
             if constexpr (KIND == 9) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(r[c]) : "v"(r[c + 8]));
             if constexpr (KIND == 10) asm volatile("v_lshl_add_u64 %0, %0, 1, %1" : "+v"(q[0]) : "v"(q[1 + (c & 1)]));
             if constexpr (KIND == 11) asm volatile("v_add_u32 %0, %0, %1" : "+v"(r[0]) : "v"(r[c + 8]));
+            if constexpr (KIND == 12)
+                asm volatile("v_xor_b32_dpp %0, %1, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"(r[c]) : "v"(r[c + 8]));
+            if constexpr (KIND == 13)
+                asm volatile("v_add_u32_dpp %0, %1, %0 row_shl:4 row_mask:0xf bank_mask:0xf" : "+v"(r[c]) : "v"(r[c + 8]));
+            if constexpr (KIND == 14) asm volatile("v_mov_b32_dpp %0, %1 row_shl:4 row_mask:0xf bank_mask:0xf" : "=v"(r[c]) : "v"(r[c + 8]));
+            if constexpr (KIND == 15) asm volatile("v_mov_b32 %0, %1" : "=v"(r[c]) : "v"(r[c + 8]));
         }
     }
 }
@@ -309,10 +316,11 @@ extern "C" int cg_diag_ops(int kind, uint32_t iters, uint32_t threads, unsigned 
     unsigned long long *d_c = nullptr;
     if (hipMalloc(&d_out, threads * 4) != hipSuccess) return 2;
     if (hipMalloc(&d_c, waves * 8) != hipSuccess) return 2;
-    void (*ks[12])(uint32_t, uint32_t *, unsigned long long *) = {
-        cg::k_diag_ops<0>, cg::k_diag_ops<1>, cg::k_diag_ops<2>, cg::k_diag_ops<3>, cg::k_diag_ops<4>,  cg::k_diag_ops<5>,
-        cg::k_diag_ops<6>, cg::k_diag_ops<7>, cg::k_diag_ops<8>, cg::k_diag_ops<9>, cg::k_diag_ops<10>, cg::k_diag_ops<11>};
-    if (kind < 0 || kind > 11) return 1;
+    void (*ks[16])(uint32_t, uint32_t *, unsigned long long *) = {
+        cg::k_diag_ops<0>,  cg::k_diag_ops<1>,  cg::k_diag_ops<2>,  cg::k_diag_ops<3>, cg::k_diag_ops<4>,  cg::k_diag_ops<5>,
+        cg::k_diag_ops<6>,  cg::k_diag_ops<7>,  cg::k_diag_ops<8>,  cg::k_diag_ops<9>, cg::k_diag_ops<10>, cg::k_diag_ops<11>,
+        cg::k_diag_ops<12>, cg::k_diag_ops<13>, cg::k_diag_ops<14>, cg::k_diag_ops<15>};
+    if (kind < 0 || kind > 15) return 1;
     hipLaunchKernelGGL(ks[kind], dim3(1), dim3(threads), 0, 0, iters, d_out, d_c);
     hipLaunchKernelGGL(ks[kind], dim3(1), dim3(threads), 0, 0, iters, d_out, d_c);
     (void)hipDeviceSynchronize();

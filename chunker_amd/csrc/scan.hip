@@ -291,6 +291,12 @@ static_assert(CG_SEG % FLAT_ROW == 0, "whole rows per segment");
 __device__ __forceinline__ uint32_t wave_ror1(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, DPP_WAVE_ROR1, 0xf, 0xf, false);
 }
+// The same rotation as one v_add_u32_dpp of an opaque zero: a v_mov_b32 (DPP or not)
+// issues in ~8 clocks on gfx950, a DPP ALU op in ~4.9 (profiles/r02_v7_diag_ops_mov.json).
+__device__ __forceinline__ uint32_t wave_ror1_add(uint32_t v, uint32_t zero) {
+    // bound_ctrl set (no lane of a rotation lacks a source) so the DPP combine applies
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, DPP_WAVE_ROR1, 0xf, 0xf, true) + zero;
+}
 
 
 // the 16 table entries of one lane's 16-byte block
@@ -368,6 +374,8 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan_flat(const uint8_t *data, uint
     const uint64_t ms = mask_s << SCAN_SHIFT, ml = mask_l << SCAN_SHIFT;
     const uint32_t mh = (uint32_t)((mask_s & mask_l) >> (32 - SCAN_SHIFT));
     const uint32_t m0 = lane == 0 ? 0xffffffffu : 0u;  // lane-0 select mask (bitop3 0xCA: m ? a : b)
+    uint32_t zero = 0;
+    asm volatile("" : "+v"(zero));  // a VGPR the compiler cannot fold away (wave_ror1_add)
     const uint32_t ms_lo = (uint32_t)ms, ms_hi = (uint32_t)(ms >> 32), ml_lo = (uint32_t)ml, ml_hi = (uint32_t)(ml >> 32);
     const uint64_t end_rel = n - r0;  // rows reaching past it hold the batch end (a partial block)
 
@@ -393,15 +401,15 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan_flat(const uint8_t *data, uint
             block_lookups(gbase, ad, ring[u], g);
             const uint64_t P = block_partial(g);
             // P_{L-1}, P_{L-2}, low dword of P_{L-3}; lanes 0.. take the previous row's
-            const uint32_t a_lo = wave_ror1((uint32_t)P), a_hi = wave_ror1((uint32_t)(P >> 32));
+            const uint32_t a_lo = wave_ror1_add((uint32_t)P, zero), a_hi = wave_ror1_add((uint32_t)(P >> 32), zero);
             const uint32_t p1_lo = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)R1, a_lo, 0xCA);
             const uint32_t p1_hi = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)(R1 >> 32), a_hi, 0xCA);
             R1 = ((uint64_t)a_hi << 32) | a_lo;
-            const uint32_t b_lo = wave_ror1(p1_lo), b_hi = wave_ror1(p1_hi);
+            const uint32_t b_lo = wave_ror1_add(p1_lo, zero), b_hi = wave_ror1_add(p1_hi, zero);
             const uint32_t p2_lo = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)R2, b_lo, 0xCA);
             const uint32_t p2_hi = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)(R2 >> 32), b_hi, 0xCA);
             R2 = ((uint64_t)b_hi << 32) | b_lo;
-            const uint32_t c_lo = wave_ror1(p2_lo);
+            const uint32_t c_lo = wave_ror1_add(p2_lo, zero);
             const uint32_t p3_lo = __builtin_amdgcn_bitop3_b32(m0, R3, c_lo, 0xCA);
             R3 = c_lo;
             // C = P_{L-1} + (P_{L-2} << 16) + (P_{L-3} << 32), the shifted P_{L-2} by dwords

@@ -5,6 +5,7 @@ import os
 os.environ["CHUNKER_AMD_DIAG"] = "1"  # load libchunker_amd_diag.so (make -C chunker_amd/csrc diag)
 os.environ.setdefault("CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR", "1")
 import ctypes
+import argparse
 import json
 import sys
 
@@ -16,11 +17,17 @@ from chunker_amd._lib import lib  # noqa: E402
 
 NAMES = ["v_add_u32", "v_lshl_add_u64", "v_perm_b32", "v_add_co+v_addc_co", "v_alignbit_b32", "v_bitop3_b32",
          "v_lshlrev_b64", "v_mov_b32_dpp", "v_add3_u32", "v_cndmask_b32", "dep_chain v_lshl_add_u64",
-         "dep_chain v_add_u32"]
+         "dep_chain v_add_u32", "v_xor_b32_dpp quad_perm", "v_add_u32_dpp row_shl:4", "v_mov_b32_dpp row_shl:4",
+         "v_mov_b32"]
 lib.cg_diag_ops.argtypes = [ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+ap = argparse.ArgumentParser()
+ap.add_argument("--kinds", default="", help="comma-separated kind indices (default: all)")
+args = ap.parse_args()
 it = 500
 res = {}
-for k, name in enumerate(NAMES):
+kinds = [int(k) for k in args.kinds.split(",")] if args.kinds else range(len(NAMES))
+for k in kinds:
+    name = NAMES[k]
     row = {}
     for threads in [64, 256, 512, 1024]:
         w = threads // 64
