@@ -284,6 +284,9 @@ __device__ __forceinline__ void op16(uint32_t (&r)[16], uint64_t (&q)[8]) {
                 asm volatile("v_add_u32_dpp %0, %1, %0 row_shl:4 row_mask:0xf bank_mask:0xf" : "+v"(r[c]) : "v"(r[c + 8]));
             if constexpr (KIND == 14) asm volatile("v_mov_b32_dpp %0, %1 row_shl:4 row_mask:0xf bank_mask:0xf" : "=v"(r[c]) : "v"(r[c + 8]));
             if constexpr (KIND == 15) asm volatile("v_mov_b32 %0, %1" : "=v"(r[c]) : "v"(r[c + 8]));
+            if constexpr (KIND == 16)
+                asm volatile("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2" : "+v"(r[c]) : "v"(r[c + 8]));
+            if constexpr (KIND == 17) asm volatile("v_perm_b32 %0, %1, %0, %2" : "+v"(r[c]) : "v"(r[c + 8]), "v"(r[(c + 9) & 15]));
         }
     }
 }
@@ -316,11 +319,12 @@ extern "C" int cg_diag_ops(int kind, uint32_t iters, uint32_t threads, unsigned 
     unsigned long long *d_c = nullptr;
     if (hipMalloc(&d_out, threads * 4) != hipSuccess) return 2;
     if (hipMalloc(&d_c, waves * 8) != hipSuccess) return 2;
-    void (*ks[16])(uint32_t, uint32_t *, unsigned long long *) = {
+    void (*ks[18])(uint32_t, uint32_t *, unsigned long long *) = {
         cg::k_diag_ops<0>,  cg::k_diag_ops<1>,  cg::k_diag_ops<2>,  cg::k_diag_ops<3>, cg::k_diag_ops<4>,  cg::k_diag_ops<5>,
         cg::k_diag_ops<6>,  cg::k_diag_ops<7>,  cg::k_diag_ops<8>,  cg::k_diag_ops<9>, cg::k_diag_ops<10>, cg::k_diag_ops<11>,
-        cg::k_diag_ops<12>, cg::k_diag_ops<13>, cg::k_diag_ops<14>, cg::k_diag_ops<15>};
-    if (kind < 0 || kind > 15) return 1;
+        cg::k_diag_ops<12>, cg::k_diag_ops<13>, cg::k_diag_ops<14>, cg::k_diag_ops<15>,
+        cg::k_diag_ops<16>, cg::k_diag_ops<17>};
+    if (kind < 0 || kind > 17) return 1;
     hipLaunchKernelGGL(ks[kind], dim3(1), dim3(threads), 0, 0, iters, d_out, d_c);
     hipLaunchKernelGGL(ks[kind], dim3(1), dim3(threads), 0, 0, iters, d_out, d_c);
     (void)hipDeviceSynchronize();

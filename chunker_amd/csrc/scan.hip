@@ -323,7 +323,12 @@ __device__ __forceinline__ uint64_t block_partial(const uint64_t (&g)[4][4]) {
     return P;
 }
 
-template <uint32_t FLAT_D, bool NT>
+// FORM 0 (product) issues a ring slot's next load after the row; FORM 1 (diagnostics) as soon
+// as the row's lookup addresses have consumed its bytes (in flight during the row's hash work:
+// measured the same, with 123 VGPRs instead of 114); FORM 2 (diagnostics) loads the rows and
+// hashes nothing -- the ceiling of this read schedule (6.6-6.7 TB/s,
+// profiles/r02_v8_diag_scan_forms.json).
+template <uint32_t FLAT_D, bool NT, int FORM = 0>
 __global__ __launch_bounds__(SCAN2_T) void k_scan_flat(const uint8_t *data, uint64_t n,
                                                       const uint64_t *__restrict__ gear_g, uint64_t mask_s,
                                                       uint64_t mask_l, uint32_t cap, uint32_t *__restrict__ seg_count,
@@ -392,13 +397,20 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan_flat(const uint8_t *data, uint
     }
 
     uint32_t segc = 0;  // wave-uniform: candidates of the open segment so far
+    uint32_t sink = 0;  // FORM 2: the loaded bytes, kept live
 #pragma unroll 1
     for (uint64_t r = 0; r < nrow64; r += FLAT_D) {
 #pragma unroll
         for (uint32_t u = 0; u < FLAT_D; ++u) {
             const uint64_t row = r + u;
+            const uint64_t next = row + FLAT_D < nrow64 ? row + FLAT_D : nrow64 - 1;
+            if constexpr (FORM == 2) {
+                sink ^= ring[u].x ^ ring[u].y ^ ring[u].z ^ ring[u].w;
+                ring[u] = blk(next);
+            } else {
             uint64_t g[4][4];
             block_lookups(gbase, ad, ring[u], g);
+            if constexpr (FORM == 1) ring[u] = blk(next);
             const uint64_t P = block_partial(g);
             // P_{L-1}, P_{L-2}, low dword of P_{L-3}; lanes 0.. take the previous row's
             const uint32_t a_lo = wave_ror1_add((uint32_t)P, zero), a_hi = wave_ror1_add((uint32_t)(P >> 32), zero);
@@ -488,7 +500,8 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan_flat(const uint8_t *data, uint
                 segc += total;
             }
             }
-            ring[u] = blk(row + FLAT_D < nrow64 ? row + FLAT_D : nrow64 - 1);
+            if constexpr (FORM == 0) ring[u] = blk(next);
+            }  // FORM != 2
             if (u % FLAT_RPS == FLAT_RPS - 1) {  // segment end: flush its slots and count
                 const uint64_t seg = seg0 + row / FLAT_RPS;
                 if (seg < nseg) {
@@ -499,6 +512,8 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan_flat(const uint8_t *data, uint
             }
         }
     }
+    if constexpr (FORM == 2)
+        if (sink == 0x9e3779b9u && lane == 0) seg_count[seg0] = sink;  // never true for the diag inputs
 }
 
 #ifdef CG_DIAG
@@ -1277,11 +1292,14 @@ void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint
     const uint64_t wgs = (waves + SCAN2_T / 64 - 1) / (SCAN2_T / 64);
     auto k = k_scan_flat<8, true>;
 #ifdef CG_DIAG
-    // variant 5: g_scan_diag bit 0 non-temporal loads, bit 1 16 rows in flight (else 8)
+    // variant 5: g_scan_diag bit 0 non-temporal loads, bit 1 16 rows in flight (else 8);
+    // 4: non-temporal, 8 rows, next load issued before the row's hash (FORM 1); 5: loads only
     if (g_scan_variant == 5)
         k = g_scan_diag == 1   ? k_scan_flat<8, true>
             : g_scan_diag == 2 ? k_scan_flat<16, false>
             : g_scan_diag == 3 ? k_scan_flat<16, true>
+            : g_scan_diag == 4 ? k_scan_flat<8, true, 1>
+            : g_scan_diag == 5 ? k_scan_flat<8, true, 2>
                                : k_scan_flat<8, false>;
 #endif
     hipLaunchKernelGGL(k, dim3((uint32_t)wgs), dim3(SCAN2_T), 0, st, d_data, n, d_gear, mask_s, mask_l, cap,

@@ -38,7 +38,9 @@ res = {}
 for name, n, size, params in [("c2", 256, 4 << 20, (256 << 10, 1 << 20, 4 << 20)),
                               ("c4", 4, 1 << 30, (64 << 10, 256 << 10, 1 << 20)),
                               ("c4full", 16, 1 << 30, (64 << 10, 256 << 10, 1 << 20)),
-                              ("c5full", 16, 1 << 30, (256 << 10, 1 << 20, 4 << 20))]:
+                              ("c5full", 16, 1 << 30, (256 << 10, 1 << 20, 4 << 20)),
+                              ("c2x4", 1024, 4 << 20, (256 << 10, 1 << 20, 4 << 20)),
+                              ("c5one", 1, 1 << 30, (256 << 10, 1 << 20, 4 << 20))]:
     if name not in args.configs.split(","):
         continue
     d, offs = synth_nars_device(np.full(n, size, np.uint64))
