@@ -287,6 +287,16 @@ __device__ __forceinline__ void op16(uint32_t (&r)[16], uint64_t (&q)[8]) {
             if constexpr (KIND == 16)
                 asm volatile("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2" : "+v"(r[c]) : "v"(r[c + 8]));
             if constexpr (KIND == 17) asm volatile("v_perm_b32 %0, %1, %0, %2" : "+v"(r[c]) : "v"(r[c + 8]), "v"(r[(c + 9) & 15]));
+            if constexpr (KIND == 18) asm volatile("v_and_b32 %0, %0, %1" : "+v"(r[c]) : "v"(r[c + 8]));
+            if constexpr (KIND == 19) asm volatile("v_lshlrev_b32 %0, 3, %0" : "+v"(r[c]));
+            if constexpr (KIND == 20) asm volatile("v_lshl_or_b32 %0, %0, 3, %1" : "+v"(r[c]) : "v"(r[c + 8]));
+            if constexpr (KIND == 21) asm volatile("v_min3_u32 %0, %0, %1, %2" : "+v"(r[c]) : "v"(r[c + 8]), "v"(r[(c + 9) & 15]));
+            if constexpr (KIND == 22) asm volatile("v_min_u32 %0, %0, %1" : "+v"(r[c]) : "v"(r[c + 8]));
+            if constexpr (KIND == 23) asm volatile("v_bfe_u32 %0, %0, 8, 8" : "+v"(r[c]));
+            if constexpr (KIND == 24) asm volatile("v_and_or_b32 %0, %0, %1, %2" : "+v"(r[c]) : "v"(r[c + 8]), "v"(r[(c + 9) & 15]));
+            if constexpr (KIND == 25) asm volatile("v_add_co_u32 %0, vcc, %0, %1" : "+v"(r[c]) : "v"(r[c + 8]) : "vcc");
+            if constexpr (KIND == 26) asm volatile("v_lshl_add_u32 %0, %0, 1, %1" : "+v"(r[c]) : "v"(r[c + 8]));
+            if constexpr (KIND == 27) asm volatile("v_cmp_eq_u32_e64 s[40:41], %0, %1" :: "v"(r[c]), "v"(r[c + 8]) : "s40", "s41");
         }
     }
 }
@@ -319,12 +329,14 @@ extern "C" int cg_diag_ops(int kind, uint32_t iters, uint32_t threads, unsigned 
     unsigned long long *d_c = nullptr;
     if (hipMalloc(&d_out, threads * 4) != hipSuccess) return 2;
     if (hipMalloc(&d_c, waves * 8) != hipSuccess) return 2;
-    void (*ks[18])(uint32_t, uint32_t *, unsigned long long *) = {
+    void (*ks[28])(uint32_t, uint32_t *, unsigned long long *) = {
         cg::k_diag_ops<0>,  cg::k_diag_ops<1>,  cg::k_diag_ops<2>,  cg::k_diag_ops<3>, cg::k_diag_ops<4>,  cg::k_diag_ops<5>,
         cg::k_diag_ops<6>,  cg::k_diag_ops<7>,  cg::k_diag_ops<8>,  cg::k_diag_ops<9>, cg::k_diag_ops<10>, cg::k_diag_ops<11>,
         cg::k_diag_ops<12>, cg::k_diag_ops<13>, cg::k_diag_ops<14>, cg::k_diag_ops<15>,
-        cg::k_diag_ops<16>, cg::k_diag_ops<17>};
-    if (kind < 0 || kind > 17) return 1;
+        cg::k_diag_ops<16>, cg::k_diag_ops<17>, cg::k_diag_ops<18>, cg::k_diag_ops<19>, cg::k_diag_ops<20>,
+        cg::k_diag_ops<21>, cg::k_diag_ops<22>, cg::k_diag_ops<23>, cg::k_diag_ops<24>, cg::k_diag_ops<25>,
+        cg::k_diag_ops<26>, cg::k_diag_ops<27>};
+    if (kind < 0 || kind > 27) return 1;
     hipLaunchKernelGGL(ks[kind], dim3(1), dim3(threads), 0, 0, iters, d_out, d_c);
     hipLaunchKernelGGL(ks[kind], dim3(1), dim3(threads), 0, 0, iters, d_out, d_c);
     (void)hipDeviceSynchronize();
