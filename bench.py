@@ -23,7 +23,9 @@ from __future__ import annotations
 
 import argparse
 import json
+
 import os
+import re
 import socket
 import subprocess
 import sys
@@ -306,13 +308,13 @@ def sha_chain_floor(descs, n_nars, total_bytes, params, dig_ms):
 
 def scan_kernel_name(ca, avg):
     """The K1 kernel launch_scan (scan.hip) picks for these params: k_scan_flat when the
-    prefilter sees >= 15 bits of mask_s & mask_l above bit 15, else k_scan."""
+    prefilter sees >= 14 bits of mask_s & mask_l above bit 15, else k_scan."""
     import math
 
     _, masks = ca.get_cdc_tables()
     bits = round(math.log2(avg))
     both = int(masks[bits + 1]) & int(masks[bits - 1])
-    return "k_scan_flat" if bin(both >> 16).count("1") >= 15 else "k_scan"
+    return "k_scan_flat" if bin(both >> 16).count("1") >= 14 else "k_scan"
 
 
 def pmc_traffic(config, kernels):
@@ -320,7 +322,9 @@ def pmc_traffic(config, kernels):
     this config (profiles/*pmc_<config>.json, written by scripts/pmc_summary.py from
     scripts/gpu_pmc.sh passes): FETCH_SIZE x 2 (gfx950 correction, MI355X_MICROARCH.md
     §HBM) + WRITE_SIZE.  (None, None) when no summary has been committed."""
-    files = sorted(ROOT.glob(f"profiles/*pmc_{config}.json"))
+    # newest = highest (round, version): natural order, so r02_v10 sorts after r02_v3
+    files = sorted(ROOT.glob(f"profiles/*pmc_{config}.json"),
+                   key=lambda f: [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", f.name)])
     if not files:
         return None, None
     rows = json.loads(files[-1].read_text())

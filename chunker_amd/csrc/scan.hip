@@ -281,7 +281,14 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan(const uint8_t *__restrict__ da
 //    the load ring exactly), and every 4th row flushes the finished segment's slots and
 //    count.
 // Per byte: 1 SDWA mov + 1 ds_read_b64 + 2 v_lshl_add_u64 + 1 v_and_b32 + 1/2 v_min3_u32,
-// plus 5 DPP movs + 5 selects + ~4 VALU per 16 bytes.
+// plus 5 DPP adds + 5 selects + ~4 VALU per 16 bytes.
+// Product form (FORM 5): the 16 steps as split chains (split_partials: 6 + 4 dependent
+// v_lshl_add_u64 per row instead of 15 + 16), rows handled in pairs -- both rows' lookups,
+// chains and prefilters, then ONE wave-uniform verdict branch; the rare exact path redoes
+// a row's lookups from its ring slot, so only C stays live across the branch -- an 8-row
+// ring re-issued after each pair, runs of <= 32 segments per wave (launch_scan): config 2
+// 0.237 -> 0.203-0.206 ms per GiB, 5.2-5.8 TB/s on configs 2, 4 and 5
+// (profiles/r02_v10_diag_scan_split.json).
 // ---------------------------------------------------------------------------
 #define FLAT_ROW 1024u  // bytes per wave row (64 lanes x 16 B)
 #define FLAT_RPS (CG_SEG / FLAT_ROW)  // rows per segment
@@ -323,13 +330,42 @@ __device__ __forceinline__ uint64_t block_partial(const uint64_t (&g)[4][4]) {
     return P;
 }
 
-// FORM 0 (product) issues a ring slot's next load after the row; FORM 1 (diagnostics) as soon
+// (a << S) + b, S in 1..4 (the shift range of v_lshl_add_u64)
+template <int S>
+__device__ __forceinline__ uint64_t shl_add(uint64_t a, uint64_t b) {
+    static_assert(S >= 1 && S <= 4, "v_lshl_add_u64 shifts by 1..4");
+    uint64_t r;
+    asm("v_lshl_add_u64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "n"(S), "v"(b));
+    return r;
+}
+
+// Split chains: the 16 steps of a lane block as four independent 4-byte chains.
+// q[k][b] = sum_{i<=b} GEAR'[byte 4k+i] << (b-i) (q[k][0] = g[k][0]); the block partial
+// P = ((q0 << 4 + q1) << 4 + q2) << 4 + q3 (the [3] entries), and from the incoming state C
+// the hash after byte 4k+b is (E_{k-1} << (b+1)) + q[k][b] with E_{-1} = C and
+// E_k = (E_{k-1} << 4) + q[k][3] -- the same 31 v_lshl_add_u64 as two 16-step chains, but
+// 6 + 4 deep instead of 15 + 16.
+__device__ __forceinline__ void split_partials(uint64_t (&q)[4][4]) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        q[k][1] = shl1_add(q[k][0], q[k][1]);
+        q[k][2] = shl1_add(q[k][1], q[k][2]);
+        q[k][3] = shl1_add(q[k][2], q[k][3]);
+    }
+}
+__device__ __forceinline__ uint64_t split_block(const uint64_t (&q)[4][4]) {
+    return shl_add<4>(shl_add<4>(shl_add<4>(q[0][3], q[1][3]), q[2][3]), q[3][3]);
+}
+
+// FORM 0 (round-2 v3..v8 product) issues a ring slot's next load after the row; FORM 1 (diagnostics) as soon
 // as the row's lookup addresses have consumed its bytes (in flight during the row's hash work:
 // measured the same, with 123 VGPRs instead of 114); FORM 2 (diagnostics) loads the rows and
 // hashes nothing -- the ceiling of this read schedule (6.6-6.7 TB/s,
-// profiles/r02_v8_diag_scan_forms.json).
+// profiles/r02_v8_diag_scan_forms.json); FORM 3 is FORM 0 with split hash chains
+// (split_partials), FORM 4 FORM 1 with split chains, FORM 5 (the product) split chains in
+// row pairs with one verdict branch per pair, FORM 6 the same in row quads.
 template <uint32_t FLAT_D, bool NT, int FORM = 0>
-__global__ __launch_bounds__(SCAN2_T) void k_scan_flat(const uint8_t *data, uint64_t n,
+__global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat(const uint8_t *data, uint64_t n,
                                                       const uint64_t *__restrict__ gear_g, uint64_t mask_s,
                                                       uint64_t mask_l, uint32_t cap, uint32_t *__restrict__ seg_count,
                                                       uint32_t *__restrict__ seg_cand, uint64_t nseg, uint32_t spw) {
@@ -398,117 +434,201 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan_flat(const uint8_t *data, uint
 
     uint32_t segc = 0;  // wave-uniform: candidates of the open segment so far
     uint32_t sink = 0;  // FORM 2: the loaded bytes, kept live
-#pragma unroll 1
-    for (uint64_t r = 0; r < nrow64; r += FLAT_D) {
+    struct RowState {
+        uint64_t g[4][4];  // Gear' entries of the lane's 16 bytes (FORM >= 3: split partials q)
+        uint64_t C;        // hash state entering the lane's block
+        uint32_t acc;      // prefilter: min over the block of (H bits 16..47) & mh
+    };
+    // the hash after byte j of a lane block, for j = 0, 1, .. in order, x starting at the
+    // state entering the block (FORM >= 3: x is E_{k-1})
+    auto step = [&](const uint64_t(&g)[4][4], uint64_t &x, uint32_t j) -> uint64_t {
+        if constexpr (FORM >= 3) {
+            const uint64_t qj = g[j >> 2][j & 3];
+            switch (j & 3) {
+            case 0: return shl_add<1>(x, qj);
+            case 1: return shl_add<2>(x, qj);
+            case 2: return shl_add<3>(x, qj);
+            default: return x = shl_add<4>(x, qj);
+            }
+        } else {
+            return x = shl1_add(x, g[j >> 2][j & 3]);
+        }
+    };
+    auto next_row = [&](uint64_t row) { return row + FLAT_D < nrow64 ? row + FLAT_D : nrow64 - 1; };
+    // lookups, block partial, the cross-lane state C and the prefilter of ring slot u (= row)
+    auto front = [&](uint32_t u, uint64_t row, RowState &st) {
+        block_lookups(gbase, ad, ring[u], st.g);
+        if constexpr (FORM == 1 || FORM == 4) ring[u] = blk(next_row(row));
+        uint64_t P;
+        if constexpr (FORM >= 3) {
+            split_partials(st.g);  // g[k][b] now holds q[k][b]
+            P = split_block(st.g);
+        } else {
+            P = block_partial(st.g);
+        }
+        // P_{L-1}, P_{L-2}, low dword of P_{L-3}; lanes 0.. take the previous row's
+        const uint32_t a_lo = wave_ror1_add((uint32_t)P, zero), a_hi = wave_ror1_add((uint32_t)(P >> 32), zero);
+        const uint32_t p1_lo = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)R1, a_lo, 0xCA);
+        const uint32_t p1_hi = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)(R1 >> 32), a_hi, 0xCA);
+        R1 = ((uint64_t)a_hi << 32) | a_lo;
+        const uint32_t b_lo = wave_ror1_add(p1_lo, zero), b_hi = wave_ror1_add(p1_hi, zero);
+        const uint32_t p2_lo = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)R2, b_lo, 0xCA);
+        const uint32_t p2_hi = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)(R2 >> 32), b_hi, 0xCA);
+        R2 = ((uint64_t)b_hi << 32) | b_lo;
+        const uint32_t c_lo = wave_ror1_add(p2_lo, zero);
+        const uint32_t p3_lo = __builtin_amdgcn_bitop3_b32(m0, R3, c_lo, 0xCA);
+        R3 = c_lo;
+        // C = P_{L-1} + (P_{L-2} << 16) + (P_{L-3} << 32), the shifted P_{L-2} by dwords
+        const uint32_t s_hi = __builtin_amdgcn_alignbit(p2_hi, p2_lo, 16) + p3_lo;
+        st.C = (((uint64_t)p1_hi << 32) | p1_lo) + (((uint64_t)s_hi << 32) | (p2_lo << 16));
+        uint32_t acc = 0xffffffffu;
+        if constexpr (FORM >= 3) {
+            uint64_t E = st.C;
 #pragma unroll
-        for (uint32_t u = 0; u < FLAT_D; ++u) {
-            const uint64_t row = r + u;
-            const uint64_t next = row + FLAT_D < nrow64 ? row + FLAT_D : nrow64 - 1;
-            if constexpr (FORM == 2) {
-                sink ^= ring[u].x ^ ring[u].y ^ ring[u].z ^ ring[u].w;
-                ring[u] = blk(next);
-            } else {
-            uint64_t g[4][4];
-            block_lookups(gbase, ad, ring[u], g);
-            if constexpr (FORM == 1) ring[u] = blk(next);
-            const uint64_t P = block_partial(g);
-            // P_{L-1}, P_{L-2}, low dword of P_{L-3}; lanes 0.. take the previous row's
-            const uint32_t a_lo = wave_ror1_add((uint32_t)P, zero), a_hi = wave_ror1_add((uint32_t)(P >> 32), zero);
-            const uint32_t p1_lo = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)R1, a_lo, 0xCA);
-            const uint32_t p1_hi = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)(R1 >> 32), a_hi, 0xCA);
-            R1 = ((uint64_t)a_hi << 32) | a_lo;
-            const uint32_t b_lo = wave_ror1_add(p1_lo, zero), b_hi = wave_ror1_add(p1_hi, zero);
-            const uint32_t p2_lo = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)R2, b_lo, 0xCA);
-            const uint32_t p2_hi = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)(R2 >> 32), b_hi, 0xCA);
-            R2 = ((uint64_t)b_hi << 32) | b_lo;
-            const uint32_t c_lo = wave_ror1_add(p2_lo, zero);
-            const uint32_t p3_lo = __builtin_amdgcn_bitop3_b32(m0, R3, c_lo, 0xCA);
-            R3 = c_lo;
-            // C = P_{L-1} + (P_{L-2} << 16) + (P_{L-3} << 32), the shifted P_{L-2} by dwords
-            const uint32_t s_hi = __builtin_amdgcn_alignbit(p2_hi, p2_lo, 16) + p3_lo;
-            const uint64_t C = (((uint64_t)p1_hi << 32) | p1_lo) + (((uint64_t)s_hi << 32) | (p2_lo << 16));
-            uint64_t h = C;
-            uint32_t acc = 0xffffffffu;
+            for (int k = 0; k < 4; ++k) {
+                const uint64_t h0 = shl_add<1>(E, st.g[k][0]), h1 = shl_add<2>(E, st.g[k][1]);
+                const uint64_t h2 = shl_add<3>(E, st.g[k][2]), h3 = shl_add<4>(E, st.g[k][3]);
+                acc = min(min(acc, (uint32_t)(h0 >> 32) & mh), (uint32_t)(h1 >> 32) & mh);
+                acc = min(min(acc, (uint32_t)(h2 >> 32) & mh), (uint32_t)(h3 >> 32) & mh);
+                E = h3;
+            }
+        } else {
+            uint64_t h = st.C;
 #pragma unroll
             for (int i = 0; i < 16; i += 2) {
-                h = shl1_add(h, g[i >> 2][i & 3]);
+                h = shl1_add(h, st.g[i >> 2][i & 3]);
                 const uint32_t t0 = (uint32_t)(h >> 32) & mh;
-                h = shl1_add(h, g[(i + 1) >> 2][(i + 1) & 3]);
+                h = shl1_add(h, st.g[(i + 1) >> 2][(i + 1) & 3]);
                 const uint32_t t1 = (uint32_t)(h >> 32) & mh;
                 acc = min(min(acc, t0), t1);  // v_min3_u32
             }
-            const bool tail = (row + 1) * FLAT_ROW > end_rel;  // uniform
-            if (__builtin_amdgcn_ballot_w64(acc == 0) != 0 || tail) {
-            bool exact = tail;
-            if (!tail) {
-                // the prefilter fired somewhere in the row (mostly on bits below 16 it cannot
-                // see): does any byte pass the full S or L mask?  2 VALU per mask per byte
-                uint32_t ex = 0xffffffffu;
-                uint64_t hx = C;
+        }
+        st.acc = acc;
+    };
+    // the row's verdict: a fired prefilter (or the batch's last rows) is checked against
+    // the full masks and, if a candidate exists, re-walked exactly into the slot list
+    auto back = [&](uint32_t u, uint64_t row, RowState &st) {
+        const bool tail = (row + 1) * FLAT_ROW > end_rel;  // uniform
+        if (__builtin_amdgcn_ballot_w64(st.acc == 0) == 0 && !tail) return;
+        if constexpr (FORM >= 5) {  // the group forms keep only C: redo the row's lookups
+            block_lookups(gbase, ad, ring[u], st.g);
+            split_partials(st.g);
+        }
+        bool exact = tail;
+        if (!tail) {
+            // the prefilter fired somewhere in the row (mostly on bits below 16 it cannot
+            // see): does any byte pass the full S or L mask?  2 VALU per mask per byte
+            uint32_t ex = 0xffffffffu;
+            uint64_t x = st.C;
 #pragma unroll
-                for (uint32_t j = 0; j < 16; ++j) {
-                    hx = shl1_add(hx, g[j >> 2][j & 3]);
-                    const uint32_t lo = (uint32_t)hx, hi = (uint32_t)(hx >> 32);
-                    ex = min(ex, min((lo & ms_lo) | (hi & ms_hi), (lo & ml_lo) | (hi & ml_hi)));
-                }
-                exact = __builtin_amdgcn_ballot_w64(ex == 0) != 0;
+            for (uint32_t j = 0; j < 16; ++j) {
+                const uint64_t hx = step(st.g, x, j);
+                const uint32_t lo = (uint32_t)hx, hi = (uint32_t)(hx >> 32);
+                ex = min(ex, min((lo & ms_lo) | (hi & ms_hi), (lo & ml_lo) | (hi & ml_hi)));
             }
-            if (exact) {
-                // exact pass from C over the 16 entries still in registers: per-lane bit
-                // masks of the S / L positions (no branches, no LDS), a wave prefix sum
-                // (ballot + mbcnt when no lane holds two), candidates into the slot list in
-                // (row, lane, byte) = position order
-                const uint64_t prel = row * FLAT_ROW + 16u * lane;
-                const uint32_t nb = prel < end_rel ? (end_rel - prel < 16 ? (uint32_t)(end_rel - prel) : 16u) : 0u;
-                uint32_t sm = 0, lm = 0;
-                h = C;
+            exact = __builtin_amdgcn_ballot_w64(ex == 0) != 0;
+        }
+        if (!exact) return;
+        // exact pass from C over the 16 entries still in registers: per-lane bit masks of
+        // the S / L positions (no branches, no LDS), a wave prefix sum (ballot + mbcnt when
+        // no lane holds two), candidates into the slot list in (row, lane, byte) = position
+        // order
+        const uint64_t prel = row * FLAT_ROW + 16u * lane;
+        const uint32_t nb = prel < end_rel ? (end_rel - prel < 16 ? (uint32_t)(end_rel - prel) : 16u) : 0u;
+        uint32_t sm = 0, lm = 0;
+        uint64_t x = st.C;
 #pragma unroll
-                for (uint32_t j = 0; j < 16; ++j) {
-                    h = shl1_add(h, g[j >> 2][j & 3]);
-                    const uint64_t zs = h & ms, zl = h & ml;
-                    const uint32_t ts = (uint32_t)zs | (uint32_t)(zs >> 32), tl = (uint32_t)zl | (uint32_t)(zl >> 32);
-                    sm |= (1u - min(ts, 1u)) << j;
-                    lm |= (1u - min(tl, 1u)) << j;
+        for (uint32_t j = 0; j < 16; ++j) {
+            const uint64_t hx = step(st.g, x, j);
+            const uint64_t zs = hx & ms, zl = hx & ml;
+            const uint32_t ts = (uint32_t)zs | (uint32_t)(zs >> 32), tl = (uint32_t)zl | (uint32_t)(zl >> 32);
+            sm |= (1u - min(ts, 1u)) << j;
+            lm |= (1u - min(tl, 1u)) << j;
+        }
+        const uint32_t vm = nb >= 16 ? 0xffffu : (1u << nb) - 1u;
+        sm &= vm;
+        lm &= vm;
+        const uint32_t any = sm | lm, c = (uint32_t)__builtin_popcount(any);
+        uint32_t excl, total;
+        if (__builtin_amdgcn_ballot_w64(c > 1) == 0) {
+            const uint64_t bal = __builtin_amdgcn_ballot_w64(c != 0);
+            excl = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+            total = (uint32_t)__builtin_popcountll(bal);
+        } else {
+            uint32_t incl = c;
+#pragma unroll
+            for (uint32_t d = 1; d < 64; d <<= 1) {
+                const uint32_t y = (uint32_t)__shfl_up((int)incl, d, 64);
+                if (lane >= d) incl += y;
+            }
+            excl = incl - c;
+            total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        }
+        const uint32_t pos0 = (uint32_t)(row % FLAT_RPS) * FLAT_ROW + 16u * lane;
+        uint32_t idx = segc + excl;
+        for (uint32_t m = any; m; m &= m - 1) {
+            const uint32_t j = (uint32_t)__builtin_ctz(m);
+            const uint32_t f = (((sm >> j) & 1u) * CG_FLAG_S) | (((lm >> j) & 1u) * CG_FLAG_L);
+            if (idx < cap) slots[idx] = ((pos0 + j) << 2) | f;
+            ++idx;
+        }
+        segc += total;
+    };
+    // after ring slot u's row: at a segment end, flush its slots and count
+    auto flush = [&](uint32_t u, uint64_t row) {
+        if (u % FLAT_RPS == FLAT_RPS - 1) {
+            const uint64_t seg = seg0 + row / FLAT_RPS;
+            if (seg < nseg) {
+                if (lane < min(segc, cap)) seg_cand[seg * cap + lane] = slots[lane];
+                if (lane == 0) seg_count[seg] = segc;
+            }
+            segc = 0;
+        }
+    };
+    static_assert(FLAT_RPS % 2 == 0, "row pairs never straddle a segment");
+#pragma unroll 1
+    for (uint64_t r = 0; r < nrow64; r += FLAT_D) {
+        if constexpr (FORM >= 5) {
+            // row groups (pairs, FORM 6 quads): the rows' lookups and chains before one
+            // combined verdict branch; the rare exact path redoes a row's lookups from its
+            // ring slot, re-issued only after the group
+            constexpr uint32_t GRP = FORM == 6 ? 4u : 2u;
+            static_assert(FLAT_D % GRP == 0 && FLAT_RPS % GRP == 0, "groups never straddle a segment");
+#pragma unroll
+            for (uint32_t u = 0; u < FLAT_D; u += GRP) {
+                RowState st[GRP];
+                uint32_t acc = 0xffffffffu;
+#pragma unroll
+                for (uint32_t i = 0; i < GRP; ++i) {
+                    front(u + i, r + u + i, st[i]);
+                    acc = min(acc, st[i].acc);
                 }
-                const uint32_t vm = nb >= 16 ? 0xffffu : (1u << nb) - 1u;
-                sm &= vm;
-                lm &= vm;
-                const uint32_t any = sm | lm, c = (uint32_t)__builtin_popcount(any);
-                uint32_t excl, total;
-                if (__builtin_amdgcn_ballot_w64(c > 1) == 0) {
-                    const uint64_t bal = __builtin_amdgcn_ballot_w64(c != 0);
-                    excl = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
-                    total = (uint32_t)__builtin_popcountll(bal);
-                } else {
-                    uint32_t incl = c;
+                const bool tail = (r + u + GRP) * FLAT_ROW > end_rel;
+                if (__builtin_amdgcn_ballot_w64(acc == 0) != 0 || tail) {
 #pragma unroll
-                    for (uint32_t d = 1; d < 64; d <<= 1) {
-                        const uint32_t y = (uint32_t)__shfl_up((int)incl, d, 64);
-                        if (lane >= d) incl += y;
+                    for (uint32_t i = 0; i < GRP; ++i) {
+                        back(u + i, r + u + i, st[i]);
+                        if (i + 1 < GRP) flush(u + i, r + u + i);
                     }
-                    excl = incl - c;
-                    total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
                 }
-                const uint32_t pos0 = (uint32_t)(row % FLAT_RPS) * FLAT_ROW + 16u * lane;
-                uint32_t idx = segc + excl;
-                for (uint32_t m = any; m; m &= m - 1) {
-                    const uint32_t j = (uint32_t)__builtin_ctz(m);
-                    const uint32_t f = (((sm >> j) & 1u) * CG_FLAG_S) | (((lm >> j) & 1u) * CG_FLAG_L);
-                    if (idx < cap) slots[idx] = ((pos0 + j) << 2) | f;
-                    ++idx;
-                }
-                segc += total;
+#pragma unroll
+                for (uint32_t i = 0; i < GRP; ++i) ring[u + i] = blk(next_row(r + u + i));
+                flush(u + GRP - 1, r + u + GRP - 1);
             }
-            }
-            if constexpr (FORM == 0) ring[u] = blk(next);
-            }  // FORM != 2
-            if (u % FLAT_RPS == FLAT_RPS - 1) {  // segment end: flush its slots and count
-                const uint64_t seg = seg0 + row / FLAT_RPS;
-                if (seg < nseg) {
-                    if (lane < min(segc, cap)) seg_cand[seg * cap + lane] = slots[lane];
-                    if (lane == 0) seg_count[seg] = segc;
+        } else {
+#pragma unroll
+            for (uint32_t u = 0; u < FLAT_D; ++u) {
+                const uint64_t row = r + u;
+                if constexpr (FORM == 2) {
+                    sink ^= ring[u].x ^ ring[u].y ^ ring[u].z ^ ring[u].w;
+                    ring[u] = blk(next_row(row));
+                } else {
+                    RowState st;
+                    front(u, row, st);
+                    back(u, row, st);
+                    if constexpr (FORM == 0 || FORM == 3) ring[u] = blk(next_row(row));
                 }
-                segc = 0;
+                flush(u, row);
             }
         }
     }
@@ -1266,31 +1386,28 @@ void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint
     }
 #endif
     // k_scan_flat re-walks a whole 1 KiB row whenever its prefilter fires, k_scan only the
-    // lane's 64-B piece: with 14 prefilter bits (one firing per 16 rows) the two measure
-    // the same (config 4: 3.80 vs 3.86 ms per 16 GiB), with 16 (config 2) flat is 15 %
-    // faster (0.23 vs 0.27 ms per GiB; profiles/r02_v3_diag_scan.json)
-    bool flat = __builtin_popcountll((mask_s & mask_l) >> SCAN_SHIFT) >= 15;
-#ifdef CG_DIAG
-    if (g_scan_variant == 5) flat = pre;
-#endif
-    if (!flat) {
-        hipLaunchKernelGGL(pre ? k_scan<true> : k_scan<false>, dim3((uint32_t)blocks), dim3(SCAN2_T), 0, st, d_data,
-                           n, d_gear, mask_s, mask_l, cap, d_seg_count, d_seg_cand, nseg);
+    // lane's 64-B piece; with split chains the flat kernel is faster at 16 prefilter bits
+    // (config 2: 0.205 vs 0.27 ms per GiB) and at 14 (config 4: 0.20 vs 0.237;
+    // profiles/r02_v10_diag_scan_split.json), so k_scan only takes the dense masks
+    if (!pre) {
+        hipLaunchKernelGGL(k_scan<false>, dim3((uint32_t)blocks), dim3(SCAN2_T), 0, st, d_data, n, d_gear, mask_s,
+                           mask_l, cap, d_seg_count, d_seg_cand, nseg);
         return;
     }
-    // segments per wave: 4..64 -- enough waves for 16 per CU on 256 CUs, but runs of at most
-    // 256 KiB, so that the waves in flight (one stream each, advancing together) stay
-    // within a window of ~1 GiB rather than spread at a power-of-two stride of several MiB
-    // (measured: 4 MiB runs at config 4 read ~20 % slower)
+    // segments per wave: 4..32 -- two or more waves per SIMD-slot on 256 CUs at 1 GiB, and runs
+    // of at most 128 KiB, so that the waves in flight (one stream each, advancing together)
+    // stay within a window of ~0.5 GiB rather than spread at a power-of-two stride of several
+    // MiB (measured: 4 MiB runs at config 4 read ~20 % slower; 256 KiB runs 2-5 % slower
+    // than 128 KiB at configs 2 and 5)
     uint64_t spw = (nseg + 4095) / 4096;
-    uint64_t spw_max = 64;
+    uint64_t spw_max = 32;
 #ifdef CG_DIAG
     if (g_scan_spw_max) spw_max = g_scan_spw_max;
 #endif
     spw = spw < 4 ? 4 : (spw > spw_max ? spw_max : (spw + 3) & ~3ull);
     const uint64_t waves = (nseg + spw - 1) / spw;
     const uint64_t wgs = (waves + SCAN2_T / 64 - 1) / (SCAN2_T / 64);
-    auto k = k_scan_flat<8, true>;
+    auto k = k_scan_flat<8, true, 5>;
 #ifdef CG_DIAG
     // variant 5: g_scan_diag bit 0 non-temporal loads, bit 1 16 rows in flight (else 8);
     // 4: non-temporal, 8 rows, next load issued before the row's hash (FORM 1); 5: loads only
@@ -1300,6 +1417,16 @@ void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint
             : g_scan_diag == 3 ? k_scan_flat<16, true>
             : g_scan_diag == 4 ? k_scan_flat<8, true, 1>
             : g_scan_diag == 5 ? k_scan_flat<8, true, 2>
+            : g_scan_diag == 6 ? k_scan_flat<8, true, 3>
+            : g_scan_diag == 7 ? k_scan_flat<4, true, 3>
+            : g_scan_diag == 8 ? k_scan_flat<16, true, 3>
+            : g_scan_diag == 9 ? k_scan_flat<4, true, 4>
+            : g_scan_diag == 10 ? k_scan_flat<4, true, 2>
+            : g_scan_diag == 11 ? k_scan_flat<4, false, 3>
+            : g_scan_diag == 12 ? k_scan_flat<4, true, 5>
+            : g_scan_diag == 13 ? k_scan_flat<8, true, 5>
+            : g_scan_diag == 14 ? k_scan_flat<8, true, 6>
+            : g_scan_diag == 15 ? k_scan_flat<4, true, 6>
                                : k_scan_flat<8, false>;
 #endif
     hipLaunchKernelGGL(k, dim3((uint32_t)wgs), dim3(SCAN2_T), 0, st, d_data, n, d_gear, mask_s, mask_l, cap,

@@ -29,6 +29,7 @@ ap.add_argument("--spw", default="0", help="k_scan_flat segments-per-wave caps t
 ap.add_argument("--mode-variant", type=int, default=1, help="variant the --modes apply to (5: bit 0 nt, bit 1 16 rows)")
 ap.add_argument("--configs", default="c2,c4")
 ap.add_argument("--no-pattern", action="store_true")
+ap.add_argument("--hash", type=int, default=0, help="digest between the timed scans: 0 BLAKE3, 1 SHA-256 (the bench's pipeline)")
 args = ap.parse_args()
 lib = ca.lib
 lib.cg_diag_scan_mode.argtypes = [ctypes.c_uint32]
@@ -57,7 +58,7 @@ for name, n, size, params in [("c2", 256, 4 << 20, (256 << 10, 1 << 20, 4 << 20)
         ms = []
         for it in range(6):
             lib.cg_set_profiling(1)
-            ca.chunk_batch_device(d.data_ptr(), offs, out.data_ptr(), cap, *params, hash=0, stream=sp)
+            ca.chunk_batch_device(d.data_ptr(), offs, out.data_ptr(), cap, *params, hash=args.hash, stream=sp)
             lib.cg_last_stage_times(buf, 5)
             if it >= 2:
                 ms.append(buf[0])
