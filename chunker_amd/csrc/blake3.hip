@@ -162,9 +162,16 @@ __device__ __forceinline__ void b3_leaf(const uint8_t *p, uint32_t n, uint64_t c
     }
 }
 
+// Leaves per lane in k_b3_groups: a lane hashes B3_LPL consecutive leaves and folds
+// them itself (full exec mask), so a wave covers a 64 x B3_LPL-leaf subtree and its
+// shuffle fold (6 levels, one wave-wide compression each, mostly idle lanes) is paid
+// once per 256 leaves instead of once per 64 (the fold was ~23 % of the
+// stage with one leaf per lane).
+#define B3_LPL 4u
+template <uint32_t LPL>
 __device__ __forceinline__ uint64_t b3_groups_of(uint64_t len) {
     const uint64_t leaves = len ? (len + 1023) / 1024 : 1;
-    return (leaves + 63) / 64;
+    return (leaves + 64 * LPL - 1) / (64 * LPL);
 }
 
 __device__ __forceinline__ void store_digest(uint8_t *dst, const uint32_t cv[8]) {
@@ -173,17 +180,21 @@ __device__ __forceinline__ void store_digest(uint8_t *dst, const uint32_t cv[8])
     o[1] = make_uint4(cv[4], cv[5], cv[6], cv[7]);
 }
 
+template <uint32_t LPL>
 __global__ void k_b3_count(const DescRaw *__restrict__ desc, const uint64_t *__restrict__ total_p,
                            uint64_t max_chunks, uint32_t *__restrict__ gcount) {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (g >= max_chunks) return;
     uint64_t total = *total_p;
-    gcount[g] = g < total ? (uint32_t)b3_groups_of(desc[g].length) : 0u;
+    gcount[g] = g < total ? (uint32_t)b3_groups_of<LPL>(desc[g].length) : 0u;
 }
 
 // Fold the chaining values held one per lane (lanes 0..count-1) level by level,
 // the odd last node carried up (BLAKE3's left-complete tree); ROOT on the final
-// parent when `root`.  Pure register shuffles: no LDS, no barriers.
+// parent when `root`.  Pure register shuffles: no LDS, no barriers.  FULL: every lane
+// compresses (the surplus lanes' results are dropped by a select), so the levels run
+// under a full exec mask -- partial masks slow a VALU chain on gfx950.
+template <bool FULL = false>
 __device__ __forceinline__ void b3_wave_fold(uint32_t cv[8], uint32_t count, bool root, uint32_t lane) {
     while (count > 1) {
         const uint32_t half = count >> 1;
@@ -193,7 +204,13 @@ __device__ __forceinline__ void b3_wave_fold(uint32_t cv[8], uint32_t count, boo
             l[i] = __shfl(cv[i], (int)(2 * lane) & 63, 64);
             r[i] = __shfl(cv[i], (int)(2 * lane + 1) & 63, 64);
         }
-        if (lane < half) {
+        if constexpr (FULL) {
+            uint32_t p[8];
+            b3_parent(l, r, root && count == 2, p);
+            const bool take = lane < half, carry = (count & 1u) && lane == half;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) cv[i] = take ? p[i] : (carry ? l[i] : cv[i]);
+        } else if (lane < half) {
             b3_parent(l, r, root && count == 2, cv);
         } else if ((count & 1u) && lane == half) {
 #pragma unroll
@@ -216,8 +233,39 @@ __global__ __launch_bounds__(256) void k_b3_map(const uint64_t *__restrict__ gro
     for (uint64_t g = group_base[c]; g < group_base[c + 1]; ++g) gmap[g] = (uint32_t)c;
 }
 
-// One wave per 64-leaf group (4 waves per workgroup for occupancy).
-template <bool NOLOAD = false>
+// The chaining value of leaves [leaf0, leaf0 + r) of a chunk (r = 1..4, the subtree of
+// one lane): leaf CVs folded pairwise, the odd third leaf paired last (left-complete);
+// ROOT on the last compression when the chunk is this subtree (`root`).
+template <bool NOLOAD>
+__device__ __forceinline__ void b3_lane4(const uint8_t *chunk, uint64_t len, uint64_t leaf0, uint32_t r, bool root,
+                                         uint32_t cv[8]) {
+    auto leaf = [&](uint32_t k, uint32_t out[8]) {
+        const uint64_t off = (leaf0 + k) * 1024;
+        const uint32_t n = (uint32_t)((len - off) < 1024 ? (len - off) : 1024);
+        b3_leaf<NOLOAD>(chunk + off, len ? n : 0u, leaf0 + k, root && r == 1, out);
+    };
+    leaf(0, cv);
+    if (r == 1) return;
+    uint32_t c1[8];
+    leaf(1, c1);
+    b3_parent(cv, c1, root && r == 2, cv);
+    if (r == 2) return;
+    uint32_t c2[8];
+    leaf(2, c2);
+    if (r == 3) {
+        b3_parent(cv, c2, root, cv);
+        return;
+    }
+    uint32_t c3[8];
+    leaf(3, c3);
+    b3_parent(c2, c3, false, c2);
+    b3_parent(cv, c2, root, cv);
+}
+
+// One wave per group of 64 x LPL leaves (4 waves per workgroup for occupancy).  MODE
+// (diagnostics): bit 0 no leaf loads (compress register words: garbage digests), bit 1
+// the full-exec fold, bit 2 no fold at all (garbage digests: the fold's share of the time).
+template <int MODE = 0, uint32_t LPL = B3_LPL>
 __global__ __launch_bounds__(64 * B3_WAVES) void k_b3_groups(const uint8_t *__restrict__ data,
                                                              const uint64_t *__restrict__ abs,
                                                              const DescRaw *__restrict__ desc,
@@ -236,21 +284,29 @@ __global__ __launch_bounds__(64 * B3_WAVES) void k_b3_groups(const uint8_t *__re
     const uint64_t ngroups = group_base[c + 1] - group_base[c];
     const uint64_t leaves = len ? (len + 1023) / 1024 : 1;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t count0 = (uint32_t)((leaves - gi * 64) < 64 ? (leaves - gi * 64) : 64);
-    const uint64_t leaf = gi * 64 + lane;
+    static_assert(LPL == 1 || LPL == 4, "one leaf per lane or a 4-leaf lane subtree");
+    const uint64_t gleaves64 = leaves - gi * 64 * LPL;
+    const uint32_t gleaves = (uint32_t)(gleaves64 < 64 * LPL ? gleaves64 : 64 * LPL);
+    const uint32_t count0 = (gleaves + LPL - 1) / LPL;  // lanes holding a subtree
+    const uint64_t leaf = (gi * 64 + lane) * LPL;
     const uint8_t *chunk = data + abs[c];
     uint32_t cv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (lane < count0) {
-        const uint64_t off = leaf * 1024;
-        const uint32_t n = (uint32_t)((len - off) < 1024 ? (len - off) : 1024);
-        b3_leaf<NOLOAD>(chunk + off, len ? n : 0u, leaf, leaves == 1, cv);
+        if constexpr (LPL == 1) {
+            const uint64_t off = leaf * 1024;
+            const uint32_t n = (uint32_t)((len - off) < 1024 ? (len - off) : 1024);
+            b3_leaf<(MODE & 1) != 0>(chunk + off, len ? n : 0u, leaf, leaves == 1, cv);
+        } else {
+            const uint32_t r = gleaves - lane * LPL < LPL ? gleaves - lane * LPL : LPL;
+            b3_lane4<(MODE & 1) != 0>(chunk, len, leaf, r, leaves <= LPL, cv);
+        }
     }
-    if (leaves == 1) {
+    if (leaves <= LPL) {  // the chunk is lane 0's subtree: cv is its digest
         if (lane == 0) store_digest(hash_base + c * stride, cv);
         return;
     }
     const bool whole = ngroups == 1;
-    b3_wave_fold(cv, count0, whole, lane);
+    if constexpr ((MODE & 4) == 0) b3_wave_fold<(MODE & 2) != 0>(cv, count0, whole, lane);
     if (lane == 0) {
         if (whole) {
             store_digest(hash_base + c * stride, cv);
@@ -326,9 +382,97 @@ __global__ __launch_bounds__(64) void k_b3_top(const DescRaw *__restrict__ desc,
 
 #ifdef CG_DIAG
 uint32_t g_b3_diag = 0;  // set by cg_diag_b3_mode (diagnostics build only)
+
+// Compression throughput microbenchmark (diagnostics): K independent compression chains
+// per lane, interleaved op by op, no memory traffic.
+template <int K>
+__device__ __forceinline__ void b3_compress_k(uint32_t (&cv)[K][8], const uint32_t (&mm)[K][16], uint32_t ctr) {
+    uint32_t v[K][16];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            v[k][i] = cv[k][i];
+            v[k][i + 8] = B3_IV[i];
+        }
+        v[k][12] = ctr;
+        v[k][13] = 0;
+        v[k][14] = 64;
+        v[k][15] = 0;
+    }
+    auto g = [&](int a, int b, int c, int d, int x, int y) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) v[k][a] = v[k][a] + v[k][b] + mm[k][x];
+#pragma unroll
+        for (int k = 0; k < K; ++k) v[k][d] = rotr32b(v[k][d] ^ v[k][a], 16);
+#pragma unroll
+        for (int k = 0; k < K; ++k) v[k][c] = v[k][c] + v[k][d];
+#pragma unroll
+        for (int k = 0; k < K; ++k) v[k][b] = rotr32b(v[k][b] ^ v[k][c], 12);
+#pragma unroll
+        for (int k = 0; k < K; ++k) v[k][a] = v[k][a] + v[k][b] + mm[k][y];
+#pragma unroll
+        for (int k = 0; k < K; ++k) v[k][d] = rotr32b(v[k][d] ^ v[k][a], 8);
+#pragma unroll
+        for (int k = 0; k < K; ++k) v[k][c] = v[k][c] + v[k][d];
+#pragma unroll
+        for (int k = 0; k < K; ++k) v[k][b] = rotr32b(v[k][b] ^ v[k][c], 7);
+    };
+#pragma unroll
+    for (int r = 0; r < 7; ++r) {
+        const uint8_t *s = B3S.s[r];
+        g(0, 4, 8, 12, s[0], s[1]);
+        g(1, 5, 9, 13, s[2], s[3]);
+        g(2, 6, 10, 14, s[4], s[5]);
+        g(3, 7, 11, 15, s[6], s[7]);
+        g(0, 5, 10, 15, s[8], s[9]);
+        g(1, 6, 11, 12, s[10], s[11]);
+        g(2, 7, 8, 13, s[12], s[13]);
+        g(3, 4, 9, 14, s[14], s[15]);
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) cv[k][i] = v[k][i] ^ v[k][i + 8];
+}
+
+template <int K>
+__global__ void k_diag_b3_chain(uint32_t iters, uint32_t *out) {
+    uint32_t cv[K][8], mm[K][16];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) cv[k][i] = threadIdx.x * 0x9E3779B9u + i + 131 * k;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) mm[k][i] = (threadIdx.x ^ blockIdx.x) * 0x85EBCA6Bu + i * 0x01010101u + k;
+    }
+    for (uint32_t it = 0; it < iters; ++it) b3_compress_k<K>(cv, mm, it);
+    uint32_t x = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x ^= cv[k][i];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
+
+// the macro-interleaved product compression (B3_G4), one chain per lane
+__global__ void k_diag_b3_chain_g4(uint32_t iters, uint32_t *out) {
+    uint32_t cv[8], m[16];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) cv[i] = threadIdx.x * 0x9E3779B9u + i;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m[i] = (threadIdx.x ^ blockIdx.x) * 0x85EBCA6Bu + i * 0x01010101u;
+    for (uint32_t it = 0; it < iters; ++it) b3_compress(cv, m, it, 64, 0);
+    uint32_t x = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x ^= cv[i];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = x;
+}
 #endif
 
-size_t blake3_group_bound(uint64_t total_bytes, uint64_t max_chunks) { return total_bytes / 65536 + max_chunks + 1; }
+size_t blake3_group_bound(uint64_t total_bytes, uint64_t max_chunks) {
+    return total_bytes / 65536 + max_chunks + 1;  // an upper bound for every leaves-per-lane setting
+}
 
 void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
                    uint64_t max_chunks, uint64_t total_bytes, uint8_t *d_hash_base, size_t hash_stride,
@@ -337,15 +481,28 @@ void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
     if (max_chunks == 0) return;
     const DescRaw *desc = (const DescRaw *)d_desc;
     const uint32_t cblocks = (uint32_t)((max_chunks + 255) / 256);
-    hipLaunchKernelGGL(k_b3_count, dim3(cblocks), dim3(256), 0, st, desc, d_total, max_chunks, d_gcount_u32);
+    auto count = k_b3_count<B3_LPL>;
+    auto groups = k_b3_groups<0>;
+    uint64_t gbound = total_bytes / (65536 * B3_LPL) + max_chunks + 1;
+#ifdef CG_DIAG
+    // bit 3: one leaf per lane (the round-2 v11 kernel)
+    if (g_b3_diag & 8u) {
+        count = k_b3_count<1>;
+        gbound = total_bytes / 65536 + max_chunks + 1;
+    }
+    switch (g_b3_diag) {
+    case 1: groups = k_b3_groups<1>; break;
+    case 2: groups = k_b3_groups<2>; break;
+    case 4: groups = k_b3_groups<4>; break;
+    case 8: groups = k_b3_groups<0, 1>; break;
+    case 10: groups = k_b3_groups<2, 1>; break;
+    case 12: groups = k_b3_groups<4, 1>; break;
+    default: break;
+    }
+#endif
+    hipLaunchKernelGGL(count, dim3(cblocks), dim3(256), 0, st, desc, d_total, max_chunks, d_gcount_u32);
     launch_exclusive_scan_u32(d_gcount_u32, d_group_base, max_chunks, 0, d_scan_tmp, st);
     hipLaunchKernelGGL(k_b3_map, dim3(cblocks), dim3(256), 0, st, d_group_base, d_total, max_chunks, d_gmap);
-    const uint64_t gbound = blake3_group_bound(total_bytes, max_chunks);
-#ifdef CG_DIAG
-    auto groups = g_b3_diag ? k_b3_groups<true> : k_b3_groups<false>;
-#else
-    auto groups = k_b3_groups<false>;
-#endif
     hipLaunchKernelGGL(groups,
                        dim3((uint32_t)((gbound + B3_WAVES - 1) / B3_WAVES)), dim3(64 * B3_WAVES), 0, st, d_data, d_abs, desc, d_total, max_chunks, d_group_base, d_gmap, d_hash_base, hash_stride,
                        d_gcv);
@@ -354,3 +511,30 @@ void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
 }
 
 }  // namespace cg
+
+#ifdef CG_DIAG
+// ms for `blocks` x `threads` lanes each running `iters` x K compressions (kind 0: the
+// product's B3_G4 compression, K = 1; kind K = 1, 2, 4: K interleaved chains)
+extern "C" float cg_diag_b3_chain(int kind, uint32_t blocks, uint32_t threads, uint32_t iters) {
+    uint32_t *d_out = nullptr;
+    if (hipMalloc(&d_out, (size_t)blocks * threads * 4) != hipSuccess) return -1.f;
+    auto k = kind == 0 ? cg::k_diag_b3_chain_g4
+             : kind == 1 ? cg::k_diag_b3_chain<1>
+             : kind == 2 ? cg::k_diag_b3_chain<2>
+                         : cg::k_diag_b3_chain<4>;
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(threads), 0, 0, iters / 8 + 1, d_out);
+    (void)hipEventRecord(a, 0);
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(threads), 0, 0, iters, d_out);
+    (void)hipEventRecord(b, 0);
+    (void)hipEventSynchronize(b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    (void)hipFree(d_out);
+    return ms;
+}
+#endif

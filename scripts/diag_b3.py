@@ -26,7 +26,7 @@ out = torch.empty(cap * 48, dtype=torch.uint8, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
 buf = (ctypes.c_double * 5)()
 res = {}
-for mode in (0, 1, 0, 1):
+for mode in [int(m) for m in (sys.argv[1] if len(sys.argv) > 1 else "0,1,0,1").split(",")]:
     lib.cg_diag_b3_mode(mode)
     lib.cg_set_profiling(1)
     ts = []
@@ -36,5 +36,9 @@ for mode in (0, 1, 0, 1):
         ts.append(buf[4])
     lib.cg_set_profiling(0)
     res.setdefault(f"mode{mode}", []).append(round(float(np.median(ts)), 4))
+    got = out.cpu().numpy()
+    if mode == 0:
+        ref = got
+    res[f"mode{mode}_same_digests_as_mode0"] = bool(np.array_equal(got, ref))
 lib.cg_diag_b3_mode(0)
 print(json.dumps(res))

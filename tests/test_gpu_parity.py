@@ -357,7 +357,10 @@ def test_digest_spans_all_lengths(ca, O):
     rng = np.random.default_rng(5)
     data = rng.integers(0, 256, 3 << 20, dtype=np.uint8)
     lens = list(range(0, 300)) + [511, 512, 513, 1023, 1024, 1025, 2047, 2048, 2049, 4095, 4096, 4097, 65535,
-                                  65536, 65537, 65536 * 3 + 1, 1 << 20, (1 << 20) + 3, 3 << 20]
+                                  65536, 65537, 65536 * 3 + 1, 1 << 20, (1 << 20) + 3, 3 << 20,
+                                  # BLAKE3 lane subtrees (4 leaves) and wave groups (256 leaves)
+                                  3071, 3072, 3073, 5119, 5120, 5121, 7169, 8192, 261120, 262143, 262144, 262145,
+                                  263168, 266241, 524289, 786432 + 2049]
     offs = [int(rng.integers(0, len(data) - n + 1)) for n in lens]
     d = torch.from_numpy(data).cuda()
     o = torch.tensor(offs, dtype=torch.int64).cuda()
