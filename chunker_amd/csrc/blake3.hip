@@ -265,7 +265,12 @@ __device__ __forceinline__ void b3_lane4(const uint8_t *chunk, uint64_t len, uin
 // One wave per group of 64 x LPL leaves (4 waves per workgroup for occupancy).  MODE
 // (diagnostics): bit 0 no leaf loads (compress register words: garbage digests), bit 1
 // the full-exec fold, bit 2 no fold at all (garbage digests: the fold's share of the time).
-template <int MODE = 0, uint32_t LPL = B3_LPL>
+//
+// DEFER (the product, one leaf per lane): no fold here -- each lane stores its leaf's
+// chaining value into lcv (64 per group) and k_b3_fold folds 16 groups per wave with
+// every lane busy.  The in-wave fold costs six wave-wide compressions per 64-leaf group
+// (with 32, 16, .. 1 lanes doing useful work) against 16 for the leaves.
+template <int MODE = 0, uint32_t LPL = B3_LPL, bool DEFER = false>
 __global__ __launch_bounds__(64 * B3_WAVES) void k_b3_groups(const uint8_t *__restrict__ data,
                                                              const uint64_t *__restrict__ abs,
                                                              const DescRaw *__restrict__ desc,
@@ -273,7 +278,7 @@ __global__ __launch_bounds__(64 * B3_WAVES) void k_b3_groups(const uint8_t *__re
                                                              const uint64_t *__restrict__ group_base,
                                                              const uint32_t *__restrict__ gmap,
                                                              uint8_t *__restrict__ hash_base, size_t stride,
-                                                             uint32_t *__restrict__ gcv) {
+                                                             uint32_t *__restrict__ gcv, uint32_t *__restrict__ lcv) {
     uint64_t total = *total_p;
     if (total > max_chunks) total = max_chunks;
     const uint64_t G = (uint64_t)blockIdx.x * B3_WAVES + (threadIdx.x >> 6);
@@ -305,6 +310,15 @@ __global__ __launch_bounds__(64 * B3_WAVES) void k_b3_groups(const uint8_t *__re
         if (lane == 0) store_digest(hash_base + c * stride, cv);
         return;
     }
+    if constexpr (DEFER) {
+        static_assert(LPL == 1, "deferred folds take one leaf per lane");
+        if (lane < count0) {
+            uint4 *o = reinterpret_cast<uint4 *>(lcv + (G * 64 + lane) * 8);
+            o[0] = make_uint4(cv[0], cv[1], cv[2], cv[3]);
+            o[1] = make_uint4(cv[4], cv[5], cv[6], cv[7]);
+        }
+        return;
+    }
     const bool whole = ngroups == 1;
     if constexpr ((MODE & 4) == 0) b3_wave_fold<(MODE & 2) != 0>(cv, count0, whole, lane);
     if (lane == 0) {
@@ -313,6 +327,96 @@ __global__ __launch_bounds__(64 * B3_WAVES) void k_b3_groups(const uint8_t *__re
         } else {
 #pragma unroll
             for (int i = 0; i < 8; ++i) gcv[G * 8 + i] = cv[i];
+        }
+    }
+}
+
+// Fold the leaf chaining values of B3_FOLD_G consecutive 64-leaf groups per wave, level
+// by level in LDS: at each level every (group, parent) slot is a lane, so a level of the
+// 16 groups costs (16 x parents) / 64 wave-wide compressions instead of one per group
+// (~17 compressions per 16 groups against 6 per group in b3_wave_fold).  Same pairing
+// as b3_wave_fold (odd node carried up; ROOT on the last parent of a single-group chunk);
+// the group's value goes to the digest (single-group chunks) or gcv (k_b3_top).
+#define B3_FOLD_G 16u
+__global__ __launch_bounds__(64) void k_b3_fold(const DescRaw *__restrict__ desc, const uint64_t *__restrict__ total_p,
+                                                uint64_t max_chunks, const uint64_t *__restrict__ group_base,
+                                                const uint32_t *__restrict__ gmap, const uint32_t *__restrict__ lcv,
+                                                uint8_t *__restrict__ hash_base, size_t stride,
+                                                uint32_t *__restrict__ gcv) {
+    __shared__ uint32_t s_node[B3_FOLD_G][64][9];  // 9: a CV's 8 words + 1 (bank spread)
+    __shared__ uint32_t s_cnt[B3_FOLD_G];          // nodes at the current level (0: skip)
+    __shared__ uint32_t s_whole[B3_FOLD_G];
+    uint64_t total = *total_p;
+    if (total > max_chunks) total = max_chunks;
+    const uint64_t ng = group_base[total];
+    const uint64_t g0 = (uint64_t)blockIdx.x * B3_FOLD_G;
+    if (g0 >= ng) return;
+    const uint32_t lane = threadIdx.x;
+    if (lane < B3_FOLD_G) {
+        const uint64_t g = g0 + lane;
+        uint32_t cnt = 0, whole = 0;
+        if (g < ng) {
+            const uint64_t c = gmap[g];
+            const uint64_t len = desc[c].length;
+            const uint64_t leaves = len ? (len + 1023) / 1024 : 1;
+            const uint64_t left = leaves - (g - group_base[c]) * 64;
+            // a one-leaf chunk was digested by k_b3_groups
+            cnt = leaves == 1 ? 0u : (uint32_t)(left < 64 ? left : 64);
+            whole = group_base[c + 1] - group_base[c] == 1;
+        }
+        s_cnt[lane] = cnt;
+        s_whole[lane] = whole;
+    }
+    __syncthreads();
+#pragma unroll 1
+    for (uint32_t gl = 0; gl < B3_FOLD_G; ++gl) {
+        const uint32_t cnt = s_cnt[gl];
+        if (lane < cnt) {
+            const uint4 *q = reinterpret_cast<const uint4 *>(lcv + ((g0 + gl) * 64 + lane) * 8);
+            const uint4 a = q[0], b = q[1];
+            uint32_t *d = s_node[gl][lane];
+            d[0] = a.x, d[1] = a.y, d[2] = a.z, d[3] = a.w, d[4] = b.x, d[5] = b.y, d[6] = b.z, d[7] = b.w;
+        }
+    }
+    __syncthreads();
+    // level L has (64 >> L) parent slots per group, B3_FOLD_G << (6 - L) slots in all
+#pragma unroll 1
+    for (uint32_t lvl = 1; lvl <= 6; ++lvl) {
+        const uint32_t per = 64u >> lvl;
+        const uint32_t slots = B3_FOLD_G * per;
+#pragma unroll 1
+        for (uint32_t base = 0; base < slots; base += 64) {
+            const uint32_t sl = base + lane, gl = sl / per, j = sl % per;
+            const uint32_t cnt = sl < slots ? s_cnt[gl] : 0u;
+            uint32_t l[8], r[8], p[8];
+            const bool pair = j < cnt / 2, carry = (cnt & 1u) && j == cnt / 2 && cnt > 1;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                l[i] = s_node[gl % B3_FOLD_G][(2 * j) & 63][i];
+                r[i] = s_node[gl % B3_FOLD_G][(2 * j + 1) & 63][i];
+            }
+            // every lane compresses (full exec mask); pair lanes keep the result
+            b3_parent(l, r, s_whole[gl % B3_FOLD_G] && cnt == 2, p);
+            __syncthreads();
+            if (pair || carry)
+#pragma unroll
+                for (int i = 0; i < 8; ++i) s_node[gl][j][i] = pair ? p[i] : l[i];
+            __syncthreads();
+        }
+        if (lane < B3_FOLD_G) s_cnt[lane] = (s_cnt[lane] + 1) >> 1;
+        __syncthreads();
+    }
+    if (lane < B3_FOLD_G) {
+        const uint64_t g = g0 + lane;
+        if (g < ng && s_cnt[lane]) {  // 1 node left
+            const uint32_t *v = s_node[lane][0];
+            const uint32_t cv[8] = {v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]};
+            if (s_whole[lane]) {
+                store_digest(hash_base + (uint64_t)gmap[g] * stride, cv);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) gcv[g * 8 + i] = cv[i];
+            }
         }
     }
 }
@@ -473,30 +577,41 @@ __global__ void k_diag_b3_chain_g4(uint32_t iters, uint32_t *out) {
 size_t blake3_group_bound(uint64_t total_bytes, uint64_t max_chunks) {
     return total_bytes / 65536 + max_chunks + 1;  // an upper bound for every leaves-per-lane setting
 }
+// group chaining values (gcv), then 64 leaf chaining values per group (lcv, the deferred
+// folds of launch_blake3 with with_lcv)
+size_t blake3_cv_bytes(uint64_t total_bytes, uint64_t max_chunks, bool with_lcv) {
+    return (blake3_group_bound(total_bytes, max_chunks) + 1) * 32 * (with_lcv ? 65 : 1);
+}
 
 void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
                    uint64_t max_chunks, uint64_t total_bytes, uint8_t *d_hash_base, size_t hash_stride,
                    uint32_t *d_gmap, uint64_t *d_group_base, uint32_t *d_gcount_u32, uint64_t *d_scan_tmp,
-                   uint32_t *d_gcv, hipStream_t st) {
+                   uint32_t *d_gcv, bool with_lcv, hipStream_t st) {
     if (max_chunks == 0) return;
     const DescRaw *desc = (const DescRaw *)d_desc;
     const uint32_t cblocks = (uint32_t)((max_chunks + 255) / 256);
-    auto count = k_b3_count<B3_LPL>;
-    auto groups = k_b3_groups<0>;
-    uint64_t gbound = total_bytes / (65536 * B3_LPL) + max_chunks + 1;
+    // product: one leaf per lane, folds deferred to k_b3_fold when the caller sized d_gcv
+    // for the leaf values (with_lcv), else folded in-wave
+    auto count = k_b3_count<1>;
+    bool defer = with_lcv;
+    auto groups = defer ? k_b3_groups<0, 1, true> : k_b3_groups<0, 1>;
+    uint64_t gbound = blake3_group_bound(total_bytes, max_chunks);
+    uint32_t *d_lcv = d_gcv + (gbound + 1) * 8;
 #ifdef CG_DIAG
-    // bit 3: one leaf per lane (the round-2 v11 kernel)
-    if (g_b3_diag & 8u) {
-        count = k_b3_count<1>;
-        gbound = total_bytes / 65536 + max_chunks + 1;
-    }
+    // 1 / 5: no leaf loads (deferred / in-wave fold); 2 / 4: in-wave fold, full-exec / none;
+    // 8: in-wave fold (round-2 v11); 16: 4-leaf lane subtrees + in-wave fold
+    if (g_b3_diag) defer = with_lcv && g_b3_diag == 1;
     switch (g_b3_diag) {
-    case 1: groups = k_b3_groups<1>; break;
-    case 2: groups = k_b3_groups<2>; break;
-    case 4: groups = k_b3_groups<4>; break;
+    case 1: groups = defer ? k_b3_groups<1, 1, true> : k_b3_groups<1, 1>; break;
+    case 2: groups = k_b3_groups<2, 1>; break;
+    case 4: groups = k_b3_groups<4, 1>; break;
+    case 5: groups = k_b3_groups<1, 1>; break;
     case 8: groups = k_b3_groups<0, 1>; break;
-    case 10: groups = k_b3_groups<2, 1>; break;
-    case 12: groups = k_b3_groups<4, 1>; break;
+    case 16:
+        groups = k_b3_groups<0, 4>;
+        count = k_b3_count<4>;
+        gbound = total_bytes / (65536 * 4) + max_chunks + 1;
+        break;
     default: break;
     }
 #endif
@@ -504,8 +619,11 @@ void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
     launch_exclusive_scan_u32(d_gcount_u32, d_group_base, max_chunks, 0, d_scan_tmp, st);
     hipLaunchKernelGGL(k_b3_map, dim3(cblocks), dim3(256), 0, st, d_group_base, d_total, max_chunks, d_gmap);
     hipLaunchKernelGGL(groups,
-                       dim3((uint32_t)((gbound + B3_WAVES - 1) / B3_WAVES)), dim3(64 * B3_WAVES), 0, st, d_data, d_abs, desc, d_total, max_chunks, d_group_base, d_gmap, d_hash_base, hash_stride,
-                       d_gcv);
+                       dim3((uint32_t)((gbound + B3_WAVES - 1) / B3_WAVES)), dim3(64 * B3_WAVES), 0, st, d_data, d_abs,
+                       desc, d_total, max_chunks, d_group_base, d_gmap, d_hash_base, hash_stride, d_gcv, d_lcv);
+    if (defer)
+        hipLaunchKernelGGL(k_b3_fold, dim3((uint32_t)((gbound + B3_FOLD_G - 1) / B3_FOLD_G)), dim3(64), 0, st, desc,
+                           d_total, max_chunks, d_group_base, d_gmap, d_lcv, d_hash_base, hash_stride, d_gcv);
     hipLaunchKernelGGL(k_b3_top, dim3((uint32_t)max_chunks), dim3(64), 0, st, desc, d_total, max_chunks,
                        d_group_base, d_gcv, d_hash_base, hash_stride);
 }

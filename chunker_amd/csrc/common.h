@@ -97,8 +97,9 @@ void launch_manifest_spans(const uint64_t *d_first, uint64_t n_nars, uint64_t *d
 void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
                    uint64_t max_chunks, uint64_t total_bytes, uint8_t *d_hash_base, size_t hash_stride,
                    uint32_t *d_gmap, uint64_t *d_group_base, uint32_t *d_gcount_u32,
-                   uint64_t *d_scan_tmp, uint32_t *d_gcv, hipStream_t st);
+                   uint64_t *d_scan_tmp, uint32_t *d_gcv, bool with_lcv, hipStream_t st);
 size_t blake3_group_bound(uint64_t total_bytes, uint64_t max_chunks);
+size_t blake3_cv_bytes(uint64_t total_bytes, uint64_t max_chunks, bool with_lcv);  // launch_blake3's d_gcv
 
 void launch_spans_to_desc(const uint64_t *d_off, const uint64_t *d_len, uint64_t n, uint64_t *d_abs, void *d_desc,
                           uint64_t *d_total, hipStream_t st);

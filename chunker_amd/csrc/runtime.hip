@@ -356,7 +356,7 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
     if (algo == CG_BLAKE3) {
         if ((rc = ws->b3_gcount.ensure((chunk_bound + 1) * 4, "b3_gcount"))) return rc;
         if ((rc = ws->b3_gbase.ensure((chunk_bound + 1) * 8, "b3_gbase"))) return rc;
-        if ((rc = ws->b3_gcv.ensure((cg::blake3_group_bound(total_len, chunk_bound) + 1) * 32, "b3_gcv"))) return rc;
+        if ((rc = ws->b3_gcv.ensure(cg::blake3_cv_bytes(total_len, chunk_bound, true), "b3_gcv"))) return rc;
         if ((rc = ws->b3_gmap.ensure((cg::blake3_group_bound(total_len, chunk_bound) + 1) * 4, "b3_gmap"))) return rc;
     }
 
@@ -420,7 +420,8 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
     } else {
         cg::launch_blake3(d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, total_len, hash_base,
                           sizeof(cg_desc), ws->b3_gmap.as<uint32_t>(), ws->b3_gbase.as<uint64_t>(),
-                          ws->b3_gcount.as<uint32_t>(), ws->scan_tmp.as<uint64_t>(), ws->b3_gcv.as<uint32_t>(), st);
+                          ws->b3_gcount.as<uint32_t>(), ws->scan_tmp.as<uint64_t>(), ws->b3_gcv.as<uint32_t>(), true,
+                          st);
     }
     if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_DIGEST], st));
     if (d_chunk_ids) HIP_TRY(hipStreamWaitEvent(st, ws->ev_join, 0));
@@ -584,11 +585,11 @@ int hash_spans(Workspace *ws, const uint8_t *d_data, const uint64_t *d_offsets, 
         const uint64_t gb = cg::blake3_group_bound(tb, n);
         if ((rc = ws->b3_gcount.ensure((n + 1) * 4, "b3_gcount"))) return rc;
         if ((rc = ws->b3_gbase.ensure((n + 1) * 8, "b3_gbase"))) return rc;
-        if ((rc = ws->b3_gcv.ensure((gb + 1) * 32, "b3_gcv"))) return rc;
+        if ((rc = ws->b3_gcv.ensure(cg::blake3_cv_bytes(tb, n, false), "b3_gcv"))) return rc;
         if ((rc = ws->b3_gmap.ensure((gb + 1) * 4, "b3_gmap"))) return rc;
         cg::launch_blake3(d_data, ws->chunk_abs.as<uint64_t>(), ws->out.p, d_total, n, tb, hb, sizeof(cg_desc),
                           ws->b3_gmap.as<uint32_t>(), ws->b3_gbase.as<uint64_t>(), ws->b3_gcount.as<uint32_t>(),
-                          ws->scan_tmp.as<uint64_t>(), ws->b3_gcv.as<uint32_t>(), st);
+                          ws->scan_tmp.as<uint64_t>(), ws->b3_gcv.as<uint32_t>(), false, st);
     }
     HIP_TRY(hipMemcpy2DAsync(d_digests, 32, hb, sizeof(cg_desc), 32, n, hipMemcpyDeviceToDevice, st));
     HIP_TRY(hipGetLastError());
@@ -715,12 +716,12 @@ int push_drain(cg_push *h, bool eof, cg_desc *out, size_t out_cap, size_t *n_out
             const uint64_t gb = cg::blake3_group_bound(len, n);
             if ((rc = ws->b3_gcount.ensure((n + 1) * 4, "b3_gcount"))) return rc;
             if ((rc = ws->b3_gbase.ensure((n + 1) * 8, "b3_gbase"))) return rc;
-            if ((rc = ws->b3_gcv.ensure((gb + 1) * 32, "b3_gcv"))) return rc;
+            if ((rc = ws->b3_gcv.ensure(cg::blake3_cv_bytes(len, n, true), "b3_gcv"))) return rc;
             if ((rc = ws->b3_gmap.ensure((gb + 1) * 4, "b3_gmap"))) return rc;
             cg::launch_blake3(d_in, ws->chunk_abs.as<uint64_t>(), d_out, d_total, n, len, hb,
                               sizeof(cg_desc), ws->b3_gmap.as<uint32_t>(), ws->b3_gbase.as<uint64_t>(),
                               ws->b3_gcount.as<uint32_t>(), ws->scan_tmp.as<uint64_t>(), ws->b3_gcv.as<uint32_t>(),
-                              st);
+                              true, st);
         }
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipMemcpyAsync(out, d_out, n * sizeof(cg_desc), hipMemcpyDeviceToHost, st));

@@ -163,12 +163,12 @@ int launch_open(cg_stream *h) {
         const uint64_t gb = cg::blake3_group_bound(g.bytes, n);
         if ((rc = l.b3_gcount.ensure((n + 1) * 4, "b3_gcount"))) return rc;
         if ((rc = l.b3_gbase.ensure((n + 1) * 8, "b3_gbase"))) return rc;
-        if ((rc = l.b3_gcv.ensure((gb + 1) * 32, "b3_gcv"))) return rc;
+        if ((rc = l.b3_gcv.ensure(cg::blake3_cv_bytes(g.bytes, n, true), "b3_gcv"))) return rc;
         if ((rc = l.b3_gmap.ensure((gb + 1) * 4, "b3_gmap"))) return rc;
         if ((rc = l.scan_tmp.ensure(cg::exclusive_scan_tmp_elems(n) * 8 + 64, "scan_tmp"))) return rc;
         cg::launch_blake3(base, l.abs.as<uint64_t>(), l.desc.p, d_total, n, g.bytes, hb, sizeof(cg_desc),
                           l.b3_gmap.as<uint32_t>(), l.b3_gbase.as<uint64_t>(), l.b3_gcount.as<uint32_t>(),
-                          l.scan_tmp.as<uint64_t>(), l.b3_gcv.as<uint32_t>(), l.st);
+                          l.scan_tmp.as<uint64_t>(), l.b3_gcv.as<uint32_t>(), true, l.st);
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(stg, l.desc.p, nd, hipMemcpyDeviceToHost, l.st));

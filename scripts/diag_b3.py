@@ -1,4 +1,5 @@
-"""Diagnostic: BLAKE3 digest stage on config 3 with and without leaf loads
+"""Diagnostic: BLAKE3 digest stage on config 3 by cg_diag_b3_mode (blake3.hip launch_blake3: 0 product, 1 no leaf loads,
+2 / 4 / 8 in-wave fold full-exec / none / plain, 16 4-leaf lane subtrees); with and without leaf loads
 (cg_diag_b3_mode 1 compresses register words instead: digests garbage), so the
 compression's own time and the load path's share can be read apart."""
 import os
@@ -26,7 +27,7 @@ out = torch.empty(cap * 48, dtype=torch.uint8, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
 buf = (ctypes.c_double * 5)()
 res = {}
-for mode in [int(m) for m in (sys.argv[1] if len(sys.argv) > 1 else "0,1,0,1").split(",")]:
+for mode in [int(m) for m in (sys.argv[1] if len(sys.argv) > 1 else "0,8,0,8").split(",")]:
     lib.cg_diag_b3_mode(mode)
     lib.cg_set_profiling(1)
     ts = []
