@@ -307,14 +307,14 @@ def sha_chain_floor(descs, n_nars, total_bytes, params, dig_ms):
 
 
 def scan_kernel_name(ca, avg):
-    """The K1 kernel launch_scan (scan.hip) picks for these params: k_scan_flat when the
+    """The K1 kernel launch_scan (scan.hip) picks for these params: k_scan_flat32 when the
     prefilter sees >= 14 bits of mask_s & mask_l above bit 15, else k_scan."""
     import math
 
     _, masks = ca.get_cdc_tables()
     bits = round(math.log2(avg))
     both = int(masks[bits + 1]) & int(masks[bits - 1])
-    return "k_scan_flat" if bin(both >> 16).count("1") >= 14 else "k_scan"
+    return "k_scan_flat32" if bin(both >> 16).count("1") >= 14 else "k_scan"
 
 
 def pmc_traffic(config, kernels):

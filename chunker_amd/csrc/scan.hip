@@ -282,7 +282,8 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan(const uint8_t *__restrict__ da
 //    count.
 // Per byte: 1 SDWA mov + 1 ds_read_b64 + 2 v_lshl_add_u64 + 1 v_and_b32 + 1/2 v_min3_u32,
 // plus 5 DPP adds + 5 selects + ~4 VALU per 16 bytes.
-// Product form (FORM 5): the 16 steps as split chains (split_partials: 6 + 4 dependent
+// Round-2 v11/v12 product form (FORM 5; since v13 the product is k_scan_flat32, below,
+// which takes the same steps over 32-byte lane blocks): the 16 steps as split chains (split_partials: 6 + 4 dependent
 // v_lshl_add_u64 per row instead of 15 + 16), rows handled in pairs -- both rows' lookups,
 // chains and prefilters, then ONE wave-uniform verdict branch; the rare exact path redoes
 // a row's lookups from its ring slot, so only C stays live across the branch -- an 8-row
@@ -634,6 +635,228 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat(const uint8_t *data, u
     }
     if constexpr (FORM == 2)
         if (sink == 0x9e3779b9u && lane == 0) seg_count[seg0] = sink;  // never true for the diag inputs
+}
+
+// ---------------------------------------------------------------------------
+// K1, the product kernel for prefilterable masks (launch_scan; k_scan<false> takes the
+// dense ones): flat form with 32-byte lane blocks (2 KiB rows, lane L: bytes [32 L, 32 L + 32) as
+// two dwordx4).  The 48-byte window then spans one and a half lane blocks, so the state
+// entering lane L's block is C_L = P_{L-1} + (P_{L-2} << 32) -- three DPP rotations and
+// three selects per 32 bytes instead of five and five (plus the dword shuffle) per 16 --
+// and a row's verdict branch covers 2 KiB, as a row pair of k_scan_flat did.  A 2-row
+// ring (4 KiB per wave in flight), each slot re-issued as soon as its lookup addresses are
+// formed; split chains as k_scan_flat's FORM 3+.  Same-box A/B vs the v12 row pairs:
+// config 2 0.229 -> 0.218 ms, one 1 GiB NAR 0.226 -> 0.213, config 4 shape equal
+// (profiles/r02_v13_diag_scan_flat32.json).
+// VALU per 32 bytes: 32 SDWA addresses, 24 + 7 (partials, P), 32 (hashes), 32 ands +
+// 16 min3 (prefilter), 7 (exchange) ~= 150, against ~186 for two 16-byte blocks.
+// ---------------------------------------------------------------------------
+#define F32_ROW 2048u
+#define F32_RPS (CG_SEG / F32_ROW)  // rows per segment
+static_assert(CG_SEG % F32_ROW == 0 && F32_RPS == 2, "two 2 KiB rows per segment");
+
+template <uint32_t RING, bool NT>
+__global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data, uint64_t n,
+                                                          const uint64_t *__restrict__ gear_g, uint64_t mask_s,
+                                                          uint64_t mask_l, uint32_t cap,
+                                                          uint32_t *__restrict__ seg_count,
+                                                          uint32_t *__restrict__ seg_cand, uint64_t nseg, uint32_t spw) {
+    __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * GEAR_COPIES];
+    __shared__ uint32_t s_slots[SCAN2_T / 64][64];  // the open segment's candidate slots, per wave
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t seg0 = ((uint64_t)blockIdx.x * (SCAN2_T / 64) + (threadIdx.x >> 6)) * spw;
+    const bool active = seg0 < nseg;  // whole wave (uniform)
+    const uint64_t r0 = seg0 * CG_SEG;
+    const uint64_t nrow = (uint64_t)spw * F32_RPS;  // a multiple of RING (spw a multiple of 4)
+    static_assert(RING % F32_RPS == 0 && 8 % RING == 0, "ring trips end on segment boundaries");
+    const uint64_t last_abs = (n - 1) & ~(uint64_t)15;
+    typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+    auto ld = [&](uint64_t a) {
+        const u32x4_t *q = reinterpret_cast<const u32x4_t *>(data + (a < last_abs ? a : last_abs));
+        const u32x4_t x = NT ? __builtin_nontemporal_load(q) : *q;
+        return uint4{x.x, x.y, x.z, x.w};
+    };
+    auto blk = [&](uint64_t row, uint4 (&v)[2]) {
+        const uint64_t a = r0 + row * F32_ROW + 32u * lane;
+        v[0] = ld(a);
+        v[1] = ld(a + 16);
+    };
+    static_assert(SCAN2_T == 2 * 256 && GEAR_COPIES == 32, "two threads per Gear entry, 16 copies each");
+    const uint32_t ge = threadIdx.x >> 1;
+    const uint64_t gv = gear_g[ge] << SCAN_SHIFT;
+    uint4 ring[RING][2];
+#pragma unroll
+    for (uint32_t i = 0; i < RING; ++i) blk(active ? i : 0, ring[i]);
+    const bool has_pro = active && r0 >= F32_ROW;
+    uint4 pro[2];
+    {
+        const uint64_t a = has_pro ? r0 - F32_ROW + 32u * lane : 0;
+        pro[0] = *reinterpret_cast<const uint4 *>(data + a);
+        pro[1] = *reinterpret_cast<const uint4 *>(data + a + 16);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) s_gear[ge * GEAR_COPIES + (((threadIdx.x & 1u) * 16u + j + ge) & 31u)] = gv;
+    __syncthreads();
+    if (!active) return;
+    const char *gbase = reinterpret_cast<const char *>(s_gear);
+    uint32_t *slots = s_slots[threadIdx.x >> 6];
+    const uint32_t lo8 = (threadIdx.x & 31u) * 8u;
+    uint32_t ad[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) ad[i][b] = lo8;
+    const uint64_t ms = mask_s << SCAN_SHIFT, ml = mask_l << SCAN_SHIFT;
+    const uint32_t mh = (uint32_t)((mask_s & mask_l) >> (32 - SCAN_SHIFT));
+    const uint32_t m0 = lane == 0 ? 0xffffffffu : 0u;
+    uint32_t zero = 0;
+    asm volatile("" : "+v"(zero));
+    const uint32_t ms_lo = (uint32_t)ms, ms_hi = (uint32_t)(ms >> 32), ml_lo = (uint32_t)ml, ml_hi = (uint32_t)(ml >> 32);
+    const uint64_t end_rel = n - r0;
+
+    // q[k][b]: split partials of the lane's 8 dwords (k), byte b
+    auto partials = [&](const uint4 (&v)[2], uint64_t (&q)[8][4]) {
+        lookup4(gbase, ad[0], v[0].x, q[0]);
+        lookup4(gbase, ad[0], v[0].y, q[1]);
+        lookup4(gbase, ad[0], v[0].z, q[2]);
+        lookup4(gbase, ad[0], v[0].w, q[3]);
+        lookup4(gbase, ad[0], v[1].x, q[4]);
+        lookup4(gbase, ad[0], v[1].y, q[5]);
+        lookup4(gbase, ad[0], v[1].z, q[6]);
+        lookup4(gbase, ad[0], v[1].w, q[7]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            q[k][1] = shl1_add(q[k][0], q[k][1]);
+            q[k][2] = shl1_add(q[k][1], q[k][2]);
+            q[k][3] = shl1_add(q[k][2], q[k][3]);
+        }
+    };
+    auto block_p = [&](const uint64_t (&q)[8][4]) {
+        uint64_t P = q[0][3];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) P = shl_add<4>(P, q[k][3]);
+        return P;
+    };
+    // zero state at the batch start, as the crate's hash restart
+    uint64_t R1 = 0;
+    uint32_t R2 = 0;
+    if (has_pro) {
+        uint64_t q[8][4];
+        partials(pro, q);
+        const uint64_t P = block_p(q);
+        R1 = ((uint64_t)wave_ror1((uint32_t)(P >> 32)) << 32) | wave_ror1((uint32_t)P);
+        R2 = wave_ror1((uint32_t)R1);
+    }
+    uint32_t segc = 0;
+#pragma unroll 1
+    for (uint64_t r = 0; r < nrow; r += RING) {
+#pragma unroll
+        for (uint32_t u = 0; u < RING; ++u) {
+            const uint64_t row = r + u;
+            const uint64_t next = row + RING < nrow ? row + RING : nrow - 1;
+            uint64_t q[8][4];
+            partials(ring[u], q);
+            blk(next, ring[u]);  // the slot's bytes are in the lookups: re-issue it now
+            const uint64_t P = block_p(q);
+            const uint32_t a_lo = wave_ror1_add((uint32_t)P, zero), a_hi = wave_ror1_add((uint32_t)(P >> 32), zero);
+            const uint32_t p1_lo = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)R1, a_lo, 0xCA);
+            const uint32_t p1_hi = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)(R1 >> 32), a_hi, 0xCA);
+            R1 = ((uint64_t)a_hi << 32) | a_lo;
+            const uint32_t b_lo = wave_ror1_add(p1_lo, zero);
+            const uint32_t p2_lo = __builtin_amdgcn_bitop3_b32(m0, R2, b_lo, 0xCA);
+            R2 = b_lo;
+            // C = P_{L-1} + (P_{L-2} << 32)
+            const uint64_t C = ((uint64_t)(p1_hi + p2_lo) << 32) | p1_lo;
+            uint32_t acc = 0xffffffffu;
+            {
+                uint64_t E = C;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const uint64_t h0 = shl_add<1>(E, q[k][0]), h1 = shl_add<2>(E, q[k][1]);
+                    const uint64_t h2 = shl_add<3>(E, q[k][2]), h3 = shl_add<4>(E, q[k][3]);
+                    acc = min(min(acc, (uint32_t)(h0 >> 32) & mh), (uint32_t)(h1 >> 32) & mh);
+                    acc = min(min(acc, (uint32_t)(h2 >> 32) & mh), (uint32_t)(h3 >> 32) & mh);
+                    E = h3;
+                }
+            }
+            auto step = [&](uint64_t &x, uint32_t j) -> uint64_t {
+                const uint64_t qj = q[j >> 2][j & 3];
+                switch (j & 3) {
+                case 0: return shl_add<1>(x, qj);
+                case 1: return shl_add<2>(x, qj);
+                case 2: return shl_add<3>(x, qj);
+                default: return x = shl_add<4>(x, qj);
+                }
+            };
+            const bool tail = (row + 1) * F32_ROW > end_rel;  // uniform
+            if (__builtin_amdgcn_ballot_w64(acc == 0) != 0 || tail) {
+                bool exact = tail;
+                if (!tail) {
+                    uint32_t ex = 0xffffffffu;
+                    uint64_t x = C;
+#pragma unroll
+                    for (uint32_t j = 0; j < 32; ++j) {
+                        const uint64_t hx = step(x, j);
+                        const uint32_t lo = (uint32_t)hx, hi = (uint32_t)(hx >> 32);
+                        ex = min(ex, min((lo & ms_lo) | (hi & ms_hi), (lo & ml_lo) | (hi & ml_hi)));
+                    }
+                    exact = __builtin_amdgcn_ballot_w64(ex == 0) != 0;
+                }
+                if (exact) {
+                    const uint64_t prel = row * F32_ROW + 32u * lane;
+                    const uint32_t nb = prel < end_rel ? (end_rel - prel < 32 ? (uint32_t)(end_rel - prel) : 32u) : 0u;
+                    uint32_t sm = 0, lm = 0;
+                    uint64_t x = C;
+#pragma unroll
+                    for (uint32_t j = 0; j < 32; ++j) {
+                        const uint64_t hx = step(x, j);
+                        const uint64_t zs = hx & ms, zl = hx & ml;
+                        const uint32_t ts = (uint32_t)zs | (uint32_t)(zs >> 32), tl = (uint32_t)zl | (uint32_t)(zl >> 32);
+                        sm |= (1u - min(ts, 1u)) << j;
+                        lm |= (1u - min(tl, 1u)) << j;
+                    }
+                    const uint32_t vm = nb >= 32 ? 0xffffffffu : (1u << nb) - 1u;
+                    sm &= vm;
+                    lm &= vm;
+                    const uint32_t any = sm | lm, c = (uint32_t)__builtin_popcount(any);
+                    uint32_t excl, total;
+                    if (__builtin_amdgcn_ballot_w64(c > 1) == 0) {
+                        const uint64_t bal = __builtin_amdgcn_ballot_w64(c != 0);
+                        excl = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+                        total = (uint32_t)__builtin_popcountll(bal);
+                    } else {
+                        uint32_t incl = c;
+#pragma unroll
+                        for (uint32_t d = 1; d < 64; d <<= 1) {
+                            const uint32_t y = (uint32_t)__shfl_up((int)incl, d, 64);
+                            if (lane >= d) incl += y;
+                        }
+                        excl = incl - c;
+                        total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                    }
+                    const uint32_t pos0 = (uint32_t)(row % F32_RPS) * F32_ROW + 32u * lane;
+                    uint32_t idx = segc + excl;
+                    for (uint32_t m = any; m; m &= m - 1) {
+                        const uint32_t j = (uint32_t)__builtin_ctz(m);
+                        const uint32_t f = (((sm >> j) & 1u) * CG_FLAG_S) | (((lm >> j) & 1u) * CG_FLAG_L);
+                        if (idx < cap) slots[idx] = ((pos0 + j) << 2) | f;
+                        ++idx;
+                    }
+                    segc += total;
+                }
+            }
+            if (u % F32_RPS == F32_RPS - 1) {  // segment end: flush its slots and count
+                const uint64_t seg = seg0 + row / F32_RPS;
+                if (seg < nseg) {
+                    if (lane < min(segc, cap)) seg_cand[seg * cap + lane] = slots[lane];
+                    if (lane == 0) seg_count[seg] = segc;
+                }
+                segc = 0;
+            }
+        }
+    }
 }
 
 #ifdef CG_DIAG
@@ -1407,27 +1630,35 @@ void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint
     spw = spw < 4 ? 4 : (spw > spw_max ? spw_max : (spw + 3) & ~3ull);
     const uint64_t waves = (nseg + spw - 1) / spw;
     const uint64_t wgs = (waves + SCAN2_T / 64 - 1) / (SCAN2_T / 64);
-    auto k = k_scan_flat<8, true, 5>;
+    // product: 32-byte lane blocks in 2 KiB rows (k_scan_flat32; the 16-byte row forms of
+    // k_scan_flat are the diagnostics build's A/B)
+    auto k = k_scan_flat32<2, true>;
 #ifdef CG_DIAG
-    // variant 5: g_scan_diag bit 0 non-temporal loads, bit 1 16 rows in flight (else 8);
-    // 4: non-temporal, 8 rows, next load issued before the row's hash (FORM 1); 5: loads only
-    if (g_scan_variant == 5)
-        k = g_scan_diag == 1   ? k_scan_flat<8, true>
-            : g_scan_diag == 2 ? k_scan_flat<16, false>
-            : g_scan_diag == 3 ? k_scan_flat<16, true>
-            : g_scan_diag == 4 ? k_scan_flat<8, true, 1>
-            : g_scan_diag == 5 ? k_scan_flat<8, true, 2>
-            : g_scan_diag == 6 ? k_scan_flat<8, true, 3>
-            : g_scan_diag == 7 ? k_scan_flat<4, true, 3>
-            : g_scan_diag == 8 ? k_scan_flat<16, true, 3>
-            : g_scan_diag == 9 ? k_scan_flat<4, true, 4>
+    // variant 5 by g_scan_diag: k_scan_flat<ring rows, nt, FORM> (1: <8, nt>, 2: <16, cached>,
+    // 3: <16, nt>, 4: <8, nt, 1>, 5: <8, nt, 2> loads only, 6-8: split chains <8|4|16, nt, 3>,
+    // 9: <4, nt, 4>, 10: <4, nt, 2>, 11: <4, cached, 3>, 12-15: row pairs / quads <4|8, nt, 5|6>,
+    // other: <8, cached>), 20-22: k_scan_flat32 <2, nt> (product) / <4, nt> / <2, cached>
+    if (g_scan_variant == 5 && g_scan_diag >= 20) {
+        k = g_scan_diag == 20 ? k_scan_flat32<2, true> : g_scan_diag == 21 ? k_scan_flat32<4, true>
+                                                                         : k_scan_flat32<2, false>;
+    } else if (g_scan_variant == 5) {
+        k = g_scan_diag == 1    ? k_scan_flat<8, true>
+            : g_scan_diag == 2  ? k_scan_flat<16, false>
+            : g_scan_diag == 3  ? k_scan_flat<16, true>
+            : g_scan_diag == 4  ? k_scan_flat<8, true, 1>
+            : g_scan_diag == 5  ? k_scan_flat<8, true, 2>
+            : g_scan_diag == 6  ? k_scan_flat<8, true, 3>
+            : g_scan_diag == 7  ? k_scan_flat<4, true, 3>
+            : g_scan_diag == 8  ? k_scan_flat<16, true, 3>
+            : g_scan_diag == 9  ? k_scan_flat<4, true, 4>
             : g_scan_diag == 10 ? k_scan_flat<4, true, 2>
             : g_scan_diag == 11 ? k_scan_flat<4, false, 3>
             : g_scan_diag == 12 ? k_scan_flat<4, true, 5>
             : g_scan_diag == 13 ? k_scan_flat<8, true, 5>
             : g_scan_diag == 14 ? k_scan_flat<8, true, 6>
             : g_scan_diag == 15 ? k_scan_flat<4, true, 6>
-                               : k_scan_flat<8, false>;
+                                : k_scan_flat<8, false>;
+    }
 #endif
     hipLaunchKernelGGL(k, dim3((uint32_t)wgs), dim3(SCAN2_T), 0, st, d_data, n, d_gear, mask_s, mask_l, cap,
                        d_seg_count, d_seg_cand, nseg, (uint32_t)spw);
