@@ -338,11 +338,13 @@ __global__ __launch_bounds__(64 * B3_WAVES) void k_b3_groups(const uint8_t *__re
 // as b3_wave_fold (odd node carried up; ROOT on the last parent of a single-group chunk);
 // the group's value goes to the digest (single-group chunks) or gcv (k_b3_top).
 #define B3_FOLD_G 16u
-__global__ __launch_bounds__(64) void k_b3_fold(const DescRaw *__restrict__ desc, const uint64_t *__restrict__ total_p,
-                                                uint64_t max_chunks, const uint64_t *__restrict__ group_base,
-                                                const uint32_t *__restrict__ gmap, const uint32_t *__restrict__ lcv,
-                                                uint8_t *__restrict__ hash_base, size_t stride,
-                                                uint32_t *__restrict__ gcv) {
+#define B3_FOLD_T 256u  // 4 waves: the node loads all in flight at once, level slots over 4 waves
+__global__ __launch_bounds__(B3_FOLD_T) void k_b3_fold(const DescRaw *__restrict__ desc,
+                                                       const uint64_t *__restrict__ total_p, uint64_t max_chunks,
+                                                       const uint64_t *__restrict__ group_base,
+                                                       const uint32_t *__restrict__ gmap,
+                                                       const uint32_t *__restrict__ lcv, uint8_t *__restrict__ hash_base,
+                                                       size_t stride, uint32_t *__restrict__ gcv) {
     __shared__ uint32_t s_node[B3_FOLD_G][64][9];  // 9: a CV's 8 words + 1 (bank spread)
     __shared__ uint32_t s_cnt[B3_FOLD_G];          // nodes at the current level (0: skip)
     __shared__ uint32_t s_whole[B3_FOLD_G];
@@ -350,10 +352,10 @@ __global__ __launch_bounds__(64) void k_b3_fold(const DescRaw *__restrict__ desc
     if (total > max_chunks) total = max_chunks;
     const uint64_t ng = group_base[total];
     const uint64_t g0 = (uint64_t)blockIdx.x * B3_FOLD_G;
-    if (g0 >= ng) return;
-    const uint32_t lane = threadIdx.x;
-    if (lane < B3_FOLD_G) {
-        const uint64_t g = g0 + lane;
+    if (g0 >= ng) return;  // uniform over the block
+    const uint32_t t = threadIdx.x;
+    if (t < B3_FOLD_G) {
+        const uint64_t g = g0 + t;
         uint32_t cnt = 0, whole = 0;
         if (g < ng) {
             const uint64_t c = gmap[g];
@@ -364,54 +366,69 @@ __global__ __launch_bounds__(64) void k_b3_fold(const DescRaw *__restrict__ desc
             cnt = leaves == 1 ? 0u : (uint32_t)(left < 64 ? left : 64);
             whole = group_base[c + 1] - group_base[c] == 1;
         }
-        s_cnt[lane] = cnt;
-        s_whole[lane] = whole;
+        s_cnt[t] = cnt;
+        s_whole[t] = whole;
     }
     __syncthreads();
-#pragma unroll 1
-    for (uint32_t gl = 0; gl < B3_FOLD_G; ++gl) {
-        const uint32_t cnt = s_cnt[gl];
-        if (lane < cnt) {
-            const uint4 *q = reinterpret_cast<const uint4 *>(lcv + ((g0 + gl) * 64 + lane) * 8);
-            const uint4 a = q[0], b = q[1];
-            uint32_t *d = s_node[gl][lane];
-            d[0] = a.x, d[1] = a.y, d[2] = a.z, d[3] = a.w, d[4] = b.x, d[5] = b.y, d[6] = b.z, d[7] = b.w;
+    constexpr uint32_t PER_T = B3_FOLD_G * 64 / B3_FOLD_T;  // nodes loaded per thread
+    uint4 v[PER_T][2];
+#pragma unroll
+    for (uint32_t i = 0; i < PER_T; ++i) {
+        const uint32_t k = t + B3_FOLD_T * i, gl = k / 64, j = k % 64;
+        if (j < s_cnt[gl]) {
+            const uint4 *q = reinterpret_cast<const uint4 *>(lcv + ((g0 + gl) * 64 + j) * 8);
+            v[i][0] = q[0];
+            v[i][1] = q[1];
+        }
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < PER_T; ++i) {
+        const uint32_t k = t + B3_FOLD_T * i, gl = k / 64, j = k % 64;
+        if (j < s_cnt[gl]) {
+            uint32_t *d = s_node[gl][j];
+            d[0] = v[i][0].x, d[1] = v[i][0].y, d[2] = v[i][0].z, d[3] = v[i][0].w;
+            d[4] = v[i][1].x, d[5] = v[i][1].y, d[6] = v[i][1].z, d[7] = v[i][1].w;
         }
     }
     __syncthreads();
-    // level L has (64 >> L) parent slots per group, B3_FOLD_G << (6 - L) slots in all
+    // level L has (64 >> L) parent slots per group, B3_FOLD_G << (6 - L) in all
 #pragma unroll 1
     for (uint32_t lvl = 1; lvl <= 6; ++lvl) {
         const uint32_t per = 64u >> lvl;
         const uint32_t slots = B3_FOLD_G * per;
 #pragma unroll 1
-        for (uint32_t base = 0; base < slots; base += 64) {
-            const uint32_t sl = base + lane, gl = sl / per, j = sl % per;
+        for (uint32_t base = 0; base < slots; base += B3_FOLD_T) {
+            const uint32_t sl = base + t, gl = (sl / per) % B3_FOLD_G, j = sl % per;
             const uint32_t cnt = sl < slots ? s_cnt[gl] : 0u;
-            uint32_t l[8], r[8], p[8];
             const bool pair = j < cnt / 2, carry = (cnt & 1u) && j == cnt / 2 && cnt > 1;
+            uint32_t l[8], p[8];
+            // waves wholly past the level's slots skip the compression (uniform per wave)
+            const bool wave_live = base + (t & ~63u) < slots;
+            if (wave_live) {
+                uint32_t r[8];
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                l[i] = s_node[gl % B3_FOLD_G][(2 * j) & 63][i];
-                r[i] = s_node[gl % B3_FOLD_G][(2 * j + 1) & 63][i];
+                for (int i = 0; i < 8; ++i) {
+                    l[i] = s_node[gl][(2 * j) & 63][i];
+                    r[i] = s_node[gl][(2 * j + 1) & 63][i];
+                }
+                // every lane of a live wave compresses (full exec mask); pair lanes keep it
+                b3_parent(l, r, s_whole[gl] && cnt == 2, p);
             }
-            // every lane compresses (full exec mask); pair lanes keep the result
-            b3_parent(l, r, s_whole[gl % B3_FOLD_G] && cnt == 2, p);
             __syncthreads();
             if (pair || carry)
 #pragma unroll
                 for (int i = 0; i < 8; ++i) s_node[gl][j][i] = pair ? p[i] : l[i];
             __syncthreads();
         }
-        if (lane < B3_FOLD_G) s_cnt[lane] = (s_cnt[lane] + 1) >> 1;
+        if (t < B3_FOLD_G) s_cnt[t] = (s_cnt[t] + 1) >> 1;
         __syncthreads();
     }
-    if (lane < B3_FOLD_G) {
-        const uint64_t g = g0 + lane;
-        if (g < ng && s_cnt[lane]) {  // 1 node left
-            const uint32_t *v = s_node[lane][0];
-            const uint32_t cv[8] = {v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7]};
-            if (s_whole[lane]) {
+    if (t < B3_FOLD_G) {
+        const uint64_t g = g0 + t;
+        if (g < ng && s_cnt[t]) {  // 1 node left
+            const uint32_t *w = s_node[t][0];
+            const uint32_t cv[8] = {w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7]};
+            if (s_whole[t]) {
                 store_digest(hash_base + (uint64_t)gmap[g] * stride, cv);
             } else {
 #pragma unroll
@@ -622,7 +639,7 @@ void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
                        dim3((uint32_t)((gbound + B3_WAVES - 1) / B3_WAVES)), dim3(64 * B3_WAVES), 0, st, d_data, d_abs,
                        desc, d_total, max_chunks, d_group_base, d_gmap, d_hash_base, hash_stride, d_gcv, d_lcv);
     if (defer)
-        hipLaunchKernelGGL(k_b3_fold, dim3((uint32_t)((gbound + B3_FOLD_G - 1) / B3_FOLD_G)), dim3(64), 0, st, desc,
+        hipLaunchKernelGGL(k_b3_fold, dim3((uint32_t)((gbound + B3_FOLD_G - 1) / B3_FOLD_G)), dim3(B3_FOLD_T), 0, st, desc,
                            d_total, max_chunks, d_group_base, d_gmap, d_lcv, d_hash_base, hash_stride, d_gcv);
     hipLaunchKernelGGL(k_b3_top, dim3((uint32_t)max_chunks), dim3(64), 0, st, desc, d_total, max_chunks,
                        d_group_base, d_gcv, d_hash_base, hash_stride);
