@@ -30,12 +30,14 @@ ap.add_argument("--mode-variant", type=int, default=1, help="variant the --modes
 ap.add_argument("--configs", default="c2,c4")
 ap.add_argument("--no-pattern", action="store_true")
 ap.add_argument("--hash", type=int, default=0, help="digest between the timed scans: 0 BLAKE3, 1 SHA-256 (the bench's pipeline)")
+ap.add_argument("--flush", action="store_true", help="read a 2 GiB scratch buffer before every timed scan (evicts the batch from the 256 MB MALL)")
 args = ap.parse_args()
 lib = ca.lib
 lib.cg_diag_scan_mode.argtypes = [ctypes.c_uint32]
 lib.cg_diag_scan_variant.argtypes = [ctypes.c_uint32]
 lib.cg_diag_scan_spw_max.argtypes = [ctypes.c_uint32]
 res = {}
+scratch = torch.zeros(1 << 29, dtype=torch.int32, device="cuda") if args.flush else None
 for name, n, size, params in [("c2", 256, 4 << 20, (256 << 10, 1 << 20, 4 << 20)),
                               ("c4", 4, 1 << 30, (64 << 10, 256 << 10, 1 << 20)),
                               ("c4full", 16, 1 << 30, (64 << 10, 256 << 10, 1 << 20)),
@@ -58,6 +60,9 @@ for name, n, size, params in [("c2", 256, 4 << 20, (256 << 10, 1 << 20, 4 << 20)
         ms = []
         for it in range(6):
             lib.cg_set_profiling(1)
+            if args.flush:
+                scratch.add_(1)  # 2 GiB read + written: the MALL holds none of the batch afterwards
+                torch.cuda.synchronize()
             ca.chunk_batch_device(d.data_ptr(), offs, out.data_ptr(), cap, *params, hash=args.hash, stream=sp)
             lib.cg_last_stage_times(buf, 5)
             if it >= 2:
