@@ -113,3 +113,63 @@ def test_sharded_batch_reassembles_single_process_result(n_total):
         first.append(first[-1] + len(d))
     assert got_first == first
     assert got_bytes == np.concatenate(want).tobytes()
+
+
+def _gpu_shard_worker(rank, world, port, n_total, params, q):
+    """One rank of bench.py's sharded step on the GPU engine: its shard synthesised in
+    HBM, chunked + digested by cg_chunk_batch_device, gathered to rank 0 (gloo over host
+    copies here: two ranks share the box's one GPU, where RCCL needs one GPU per rank)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.setdefault("CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR", "1")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import chunker_amd as ca
+    from chunker_amd.dist import gather_batch
+    from chunker_amd.nar import synth_nars_device
+
+    torch.cuda.set_device(0)
+    mine = shard_nars(n_total, world, rank)
+    sizes = np.array([300_000 + 8 * (i % 7) for i in mine], np.uint64)
+    if len(sizes):
+        d, offs = synth_nars_device(sizes, first_index=mine.start)
+        cap = ca.chunking.batch_capacity(offs, params[0])
+        out = torch.empty(cap * DESC_BYTES, dtype=torch.uint8, device="cuda")
+        first = ca.chunk_batch_device(d.data_ptr(), offs, out.data_ptr(), cap, *params, hash=1,
+                                      stream=torch.cuda.current_stream().cuda_stream)
+        host = out[: int(first[-1]) * DESC_BYTES].cpu()
+    else:
+        first, host = np.zeros(1, np.uint64), torch.zeros(0, dtype=torch.uint8)
+    res = gather_batch(torch.cat([host, torch.zeros(96, dtype=torch.uint8)]), first)
+    if rank == 0:
+        q.put((res[0].numpy().tobytes(), res[1].tolist()))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_total", [9, 1])
+def test_gpu_sharded_batch_matches_oracle(n_total):
+    """Two ranks of the sharded device pipeline (shard_nars -> synth in HBM ->
+    cg_chunk_batch_device -> gather_batch) reassemble exactly the oracle's descriptors
+    over all NARs; n_total = 1 leaves rank 1 without a NAR."""
+    from chunker_amd.nar import synth_nars
+    from oracle import oracle as O
+
+    world, params = 2, (8192, 32768, 131072)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_shard_worker, args=(r, world, port, n_total, params, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got_bytes, got_first = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sizes = [300_000 + 8 * (i % 7) for i in range(n_total)]
+    data, offs = synth_nars(sizes, first_index=0)
+    want, first = [], [0]
+    for i in range(n_total):
+        dsc = O.chunk_descriptors(data[offs[i]:offs[i + 1]], *params, algo=1, nthreads=1)
+        want.append(dsc)
+        first.append(first[-1] + len(dsc))
+    assert got_first == first
+    assert got_bytes == np.concatenate(want).tobytes()
