@@ -360,15 +360,22 @@ def cpu_baseline(args, n_per, nar_bytes, params, algo):
     host, offs = synth_nars(np.full(k, nar_bytes, np.uint64), zeros=args.zeros, first_index=0)
     nars = [host[int(offs[i]):int(offs[i + 1])] for i in range(k)]
     O.chunk_descriptors(nars[0][: 8 << 20], *params, algo=algo, nthreads=nt)  # warm
-    t0 = time.perf_counter()
-    for nar in nars:
-        O.chunk_descriptors(nar, *params, algo=algo, nthreads=nt)
-    dt = time.perf_counter() - t0
+    reps = 3  # median of three passes over the sample (~1-3 s of CPU work in all)
+    dts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        for nar in nars:
+            O.chunk_descriptors(nar, *params, algo=algo, nthreads=nt)
+        dts.append(time.perf_counter() - t0)
+    dt = float(np.median(dts))
     nbytes = int(offs[-1])
     with ThreadPoolExecutor(nt) as ex:
-        t1 = time.perf_counter()
-        list(ex.map(lambda a: O.chunk_descriptors(a, *params, algo=algo, nthreads=1), nars))
-        dt_par = time.perf_counter() - t1
+        dps = []
+        for _ in range(reps):
+            t1 = time.perf_counter()
+            list(ex.map(lambda a: O.chunk_descriptors(a, *params, algo=algo, nthreads=1), nars))
+            dps.append(time.perf_counter() - t1)
+        dt_par = float(np.median(dps))
 
     def chunk_data(buf):  # chunk_data_with_hash: descriptors + an owned payload copy per chunk
         return [(bytes(buf[int(d["offset"]):int(d["offset"] + d["length"])]), d)
@@ -388,7 +395,7 @@ def cpu_baseline(args, n_per, nar_bytes, params, algo):
     c1["published_zeros"] = PUBLISHED_CHUNK_DATA_ZEROS
     return {"value": round(nbytes / dt / GIB, 4), "unit": "GiB/s", "cores": nt, "kind": "port",
             "sample": f"{k} NAR(s) ({nbytes / GIB:.3f} GiB) of the same workload, one chunk_descriptors call "
-                      f"per NAR, SHA-NI={'yes' if O.lib().or_sha256_uses_shani() else 'no'}",
+                      f"per NAR, median of {reps} passes, SHA-NI={'yes' if O.lib().or_sha256_uses_shani() else 'no'}",
             "seconds": round(dt, 3),
             "nar_parallel": round(nbytes / dt_par / GIB, 4),
             "config1_chunk_data_10MiB_D_sha256": c1,
