@@ -338,14 +338,17 @@ __global__ __launch_bounds__(64 * B3_WAVES) void k_b3_groups(const uint8_t *__re
 // as b3_wave_fold (odd node carried up; ROOT on the last parent of a single-group chunk);
 // the group's value goes to the digest (single-group chunks) or gcv (k_b3_top).
 #define B3_FOLD_G 16u
-#define B3_FOLD_T 256u  // 4 waves: the node loads all in flight at once, level slots over 4 waves
+#define B3_FOLD_T 256u  // 4 waves: level-1 loads all in flight at once, level slots over 4 waves
 __global__ __launch_bounds__(B3_FOLD_T) void k_b3_fold(const DescRaw *__restrict__ desc,
                                                        const uint64_t *__restrict__ total_p, uint64_t max_chunks,
                                                        const uint64_t *__restrict__ group_base,
                                                        const uint32_t *__restrict__ gmap,
                                                        const uint32_t *__restrict__ lcv, uint8_t *__restrict__ hash_base,
                                                        size_t stride, uint32_t *__restrict__ gcv) {
-    __shared__ uint32_t s_node[B3_FOLD_G][64][9];  // 9: a CV's 8 words + 1 (bank spread)
+    // level-1 results only (32 per group): level 1 reads its children straight from lcv,
+    // so the block needs 18 KiB of LDS and a CU holds six blocks (one dispatch round at
+    // 1 GiB; the 64-node layout took 37 KiB and two rounds)
+    __shared__ uint32_t s_node[B3_FOLD_G][32][9];  // 9: a CV's 8 words + 1 (bank spread)
     __shared__ uint32_t s_cnt[B3_FOLD_G];          // nodes at the current level (0: skip)
     __shared__ uint32_t s_whole[B3_FOLD_G];
     uint64_t total = *total_p;
@@ -370,30 +373,52 @@ __global__ __launch_bounds__(B3_FOLD_T) void k_b3_fold(const DescRaw *__restrict
         s_whole[t] = whole;
     }
     __syncthreads();
-    constexpr uint32_t PER_T = B3_FOLD_G * 64 / B3_FOLD_T;  // nodes loaded per thread
-    uint4 v[PER_T][2];
+    // level 1: slot (group gl, parent j) pairs leaves 2j and 2j + 1 of lcv
+    constexpr uint32_t L1 = B3_FOLD_G * 32 / B3_FOLD_T;  // slots per thread
+    uint4 lv[L1][2][2];
 #pragma unroll
-    for (uint32_t i = 0; i < PER_T; ++i) {
-        const uint32_t k = t + B3_FOLD_T * i, gl = k / 64, j = k % 64;
-        if (j < s_cnt[gl]) {
-            const uint4 *q = reinterpret_cast<const uint4 *>(lcv + ((g0 + gl) * 64 + j) * 8);
-            v[i][0] = q[0];
-            v[i][1] = q[1];
+    for (uint32_t i = 0; i < L1; ++i) {
+        const uint32_t sl = t + B3_FOLD_T * i, gl = sl / 32, j = sl % 32, cnt = s_cnt[gl];
+#pragma unroll
+        for (uint32_t h = 0; h < 2; ++h) {
+            if (2 * j + h < cnt) {
+                const uint4 *q = reinterpret_cast<const uint4 *>(lcv + ((g0 + gl) * 64 + 2 * j + h) * 8);
+                lv[i][h][0] = q[0];
+                lv[i][h][1] = q[1];
+            } else {
+                lv[i][h][0] = lv[i][h][1] = make_uint4(0u, 0u, 0u, 0u);
+            }
         }
     }
 #pragma unroll
-    for (uint32_t i = 0; i < PER_T; ++i) {
-        const uint32_t k = t + B3_FOLD_T * i, gl = k / 64, j = k % 64;
-        if (j < s_cnt[gl]) {
-            uint32_t *d = s_node[gl][j];
-            d[0] = v[i][0].x, d[1] = v[i][0].y, d[2] = v[i][0].z, d[3] = v[i][0].w;
-            d[4] = v[i][1].x, d[5] = v[i][1].y, d[6] = v[i][1].z, d[7] = v[i][1].w;
-        }
+    for (uint32_t i = 0; i < L1; ++i) {
+        const uint32_t sl = t + B3_FOLD_T * i, gl = sl / 32, j = sl % 32, cnt = s_cnt[gl];
+        const uint32_t l[8] = {lv[i][0][0].x, lv[i][0][0].y, lv[i][0][0].z, lv[i][0][0].w,
+                               lv[i][0][1].x, lv[i][0][1].y, lv[i][0][1].z, lv[i][0][1].w};
+        const uint32_t r[8] = {lv[i][1][0].x, lv[i][1][0].y, lv[i][1][0].z, lv[i][1][0].w,
+                               lv[i][1][1].x, lv[i][1][1].y, lv[i][1][1].z, lv[i][1][1].w};
+        uint32_t p[8];
+        b3_parent(l, r, s_whole[gl] && cnt == 2, p);  // every lane (full exec mask)
+        const bool pair = j < cnt / 2, carry = (cnt & 1u) && j == cnt / 2 && cnt > 1;
+        if (pair || carry)
+#pragma unroll
+            for (int k = 0; k < 8; ++k) s_node[gl][j][k] = pair ? p[k] : l[k];
     }
     __syncthreads();
-    // level L has (64 >> L) parent slots per group, B3_FOLD_G << (6 - L) in all
+    if (t < B3_FOLD_G) {
+        const uint32_t c0 = s_cnt[t];
+        if (c0 == 1) {  // a one-leaf group (a chunk's last 1 KiB) has no level-1 parent: its leaf is node 0
+            const uint4 *q = reinterpret_cast<const uint4 *>(lcv + (g0 + t) * 64 * 8);
+            const uint4 x = q[0], y = q[1];
+            uint32_t *d = s_node[t][0];
+            d[0] = x.x, d[1] = x.y, d[2] = x.z, d[3] = x.w, d[4] = y.x, d[5] = y.y, d[6] = y.z, d[7] = y.w;
+        }
+        s_cnt[t] = c0 > 1 ? (c0 + 1) >> 1 : c0;
+    }
+    __syncthreads();
+    // levels 2..6 in LDS: (32 >> (L - 1)) parent slots per group
 #pragma unroll 1
-    for (uint32_t lvl = 1; lvl <= 6; ++lvl) {
+    for (uint32_t lvl = 2; lvl <= 6; ++lvl) {
         const uint32_t per = 64u >> lvl;
         const uint32_t slots = B3_FOLD_G * per;
 #pragma unroll 1
@@ -408,8 +433,8 @@ __global__ __launch_bounds__(B3_FOLD_T) void k_b3_fold(const DescRaw *__restrict
                 uint32_t r[8];
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
-                    l[i] = s_node[gl][(2 * j) & 63][i];
-                    r[i] = s_node[gl][(2 * j + 1) & 63][i];
+                    l[i] = s_node[gl][(2 * j) & 31][i];
+                    r[i] = s_node[gl][(2 * j + 1) & 31][i];
                 }
                 // every lane of a live wave compresses (full exec mask); pair lanes keep it
                 b3_parent(l, r, s_whole[gl] && cnt == 2, p);

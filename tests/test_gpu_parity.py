@@ -584,3 +584,16 @@ def test_dense_candidate_segments(ca, O, params):
     for algo in (SHA, B3):
         got = ca.chunk_descriptors_array(nar, *params, hash=algo)
         assert_same(got, O.chunk_descriptors(nar, *params, algo=algo), f"algo={algo}")
+
+
+@pytest.mark.parametrize("mx", [1024, 2048, 3072, 65536, 66560, 132096, 196608, 4 << 20])
+def test_blake3_tree_shapes(ca, O, mx):
+    """All-zero data cuts every chunk at max (the reference's published-bench regime), so
+    max picks the BLAKE3 tree each chunk gets: 1-3 leaves (root at k_b3_fold's first or
+    second level), one full 64-leaf group, a group plus a one-leaf group (65 leaves), and
+    several groups folded by k_b3_top; the ragged tail chunk adds one more shape."""
+    data = np.zeros(5 * mx + 777, np.uint8)
+    params = (max(64, mx // 4), max(256, mx // 2), mx)
+    got = ca.chunk_batch([data], *params, hash=B3)[0]
+    want = O.chunk_descriptors(data, *params, algo=B3)
+    assert_same(got, want, f"max={mx}")
