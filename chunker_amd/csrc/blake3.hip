@@ -116,36 +116,64 @@ __device__ __forceinline__ void b3_leaf(const uint8_t *p, uint32_t n, uint64_t c
     const uint32_t nblk = n ? (n + 63) / 64 : 1;
     const uint32_t nfull = n / 64;  // blocks with all 64 bytes inside the leaf
     const uint8_t *endp = p + n;
-    u32x4_a4 nx[4];
-    uint32_t nx16 = 0;
-    auto fetch = [&](uint32_t j) {
-        const uint32_t *q = base + 16 * j;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) nx[i] = *reinterpret_cast<const u32x4_a4 *>(q + 4 * i);
-        // the dword after the block starts inside the leaf whenever shift != 0
-        nx16 = shift ? q[16] : 0u;
-    };
-    if (!NOLOAD && nfull) fetch(0);
-    for (uint32_t j = 0; j < nblk; ++j) {
-        const uint32_t *q = base + 16 * j;
+    auto flags_of = [&](uint32_t j) {
         const bool last = j + 1 == nblk;
-        const uint32_t blen = last ? n - 64 * j : 64u;
+        return (j == 0 ? B3_CHUNK_START : 0u) | (last ? B3_CHUNK_END : 0u) | (root && last ? B3_ROOT : 0u);
+    };
+    auto fetch = [&](u32x4_a4 (&v)[4], uint32_t &v16, const uint32_t *q) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = *reinterpret_cast<const u32x4_a4 *>(q + 4 * i);
+        // the dword after the block starts inside the leaf whenever shift != 0 (and is ignored
+        // by the realignment when shift == 0: the load then re-reads the block's last dword,
+        // never one past the buffer); unconditional, so every block issues the same five loads
+        v16 = q[shift ? 16 : 15];
+    };
+    if (nfull) {
+        // Full blocks.  The loop body is one basic block: the next block's words load into
+        // nn on every iteration (the last re-reads its own block) and move into nx at the
+        // latch, after the compression, so the loads' wait sits there.  With the tail block
+        // inside the loop and a conditional prefetch, the compiler merged the paths before
+        // the compression and waited (vmcnt) for the just-issued loads there: one load
+        // latency per block, ~15 % of the stage (scripts/diag_b3.py, no-load mode).
+        u32x4_a4 nx[4], nn[4];
+        uint32_t nx16 = 0, nn16 = 0;
+        if (!NOLOAD) fetch(nx, nx16, base);
+#pragma unroll 1
+        for (uint32_t j = 0; j < nfull; ++j) {
+            uint32_t m[16];
+            if (NOLOAD) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) m[i] = (uint32_t)ctr * 0x9E3779B9u + (uint32_t)(i * 0x01010101) + j;
+            } else {
+                fetch(nn, nn16, base + 16 * (j + 1 < nfull ? j + 1 : j));
+                __builtin_amdgcn_sched_barrier(0);  // issued before the compression, not sunk after it
+                const uint32_t dw[17] = {nx[0].x, nx[0].y, nx[0].z, nx[0].w, nx[1].x, nx[1].y, nx[1].z, nx[1].w,
+                                         nx[2].x, nx[2].y, nx[2].z, nx[2].w, nx[3].x, nx[3].y, nx[3].z, nx[3].w,
+                                         nx16};
+#pragma unroll
+                for (int i = 0; i < 16; ++i) m[i] = __builtin_amdgcn_alignbyte(dw[i + 1], dw[i], shift);
+            }
+            b3_compress(cv, m, ctr, 64u, flags_of(j));
+            __builtin_amdgcn_sched_barrier(0);  // the move (and the wait it needs) after the compression
+            if (!NOLOAD) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) nx[i] = nn[i];
+                nx16 = nn16;
+                // opaque from here on: without it the compiler rotates the loop so that the
+                // loads are issued at the top of the iteration that consumes them and waited
+                // for at once (the prefetch undone); with it the wait stays here
+                asm volatile("" : "+v"(nx[0]), "+v"(nx[1]), "+v"(nx[2]), "+v"(nx[3]), "+v"(nx16));
+            }
+        }
+    }
+    if (nblk > nfull) {  // the partial last block (or the one empty block of n == 0)
+        const uint32_t j = nfull;
+        const uint32_t *q = base + 16 * j;
+        const uint32_t blen = n - 64 * j;
         uint32_t dw[17], m[16];
         if (NOLOAD) {
 #pragma unroll
             for (int i = 0; i < 16; ++i) m[i] = (uint32_t)ctr * 0x9E3779B9u + (uint32_t)(i * 0x01010101) + j;
-        } else if (j < nfull) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                dw[4 * i] = nx[i].x;
-                dw[4 * i + 1] = nx[i].y;
-                dw[4 * i + 2] = nx[i].z;
-                dw[4 * i + 3] = nx[i].w;
-            }
-            dw[16] = nx16;
-            if (!NOLOAD && j + 1 < nfull) fetch(j + 1);
-#pragma unroll
-            for (int i = 0; i < 16; ++i) m[i] = __builtin_amdgcn_alignbyte(dw[i + 1], dw[i], shift);
         } else {
 #pragma unroll
             for (int i = 0; i < 17; ++i) dw[i] = (reinterpret_cast<const uint8_t *>(q + i) < endp) ? q[i] : 0u;
@@ -156,9 +184,7 @@ __device__ __forceinline__ void b3_leaf(const uint8_t *p, uint32_t n, uint64_t c
                 m[i] = r >= 4 ? v : (r <= 0 ? 0u : (v & (0xffffffffu >> (32 - 8 * r))));
             }
         }
-        uint32_t flags = (j == 0 ? B3_CHUNK_START : 0u) | (last ? B3_CHUNK_END : 0u);
-        if (root && last) flags |= B3_ROOT;
-        b3_compress(cv, m, ctr, blen, flags);
+        b3_compress(cv, m, ctr, blen, flags_of(j));
     }
 }
 
