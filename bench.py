@@ -176,7 +176,7 @@ def main():
     dig_ms = stages_ms["digest"]
     scan_ms = stages_ms["scan"]
     roofline = {
-        "kernel": "k_sha256" if algo == 1 else "k_b3_groups+k_b3_top",
+        "kernel": "k_sha256" if algo == 1 else "k_b3_groups+k_b3_fold+k_b3_top",
         "bound": "hbm",
         "achieved": round(total_bytes / (dig_ms * 1e-3) / 1e9, 2),
         "peak": HBM_PEAK_GBS,
@@ -192,7 +192,7 @@ def main():
     }
     if algo == 1:
         roofline["latency_floor"] = sha_chain_floor(descs, len(mine), total_bytes, params, dig_ms)
-    dig_kernels = ["k_sha256"] if algo == 1 else ["k_b3_groups", "k_b3_top"]
+    dig_kernels = ["k_sha256"] if algo == 1 else ["k_b3_groups", "k_b3_fold", "k_b3_top"]
     traffic, src = pmc_traffic(args.config, dig_kernels)
     if traffic is not None:
         roofline["traffic"] = traffic
