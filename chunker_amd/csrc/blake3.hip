@@ -120,51 +120,68 @@ __device__ __forceinline__ void b3_leaf(const uint8_t *p, uint32_t n, uint64_t c
         const bool last = j + 1 == nblk;
         return (j == 0 ? B3_CHUNK_START : 0u) | (last ? B3_CHUNK_END : 0u) | (root && last ? B3_ROOT : 0u);
     };
-    auto fetch = [&](u32x4_a4 (&v)[4], uint32_t &v16, const uint32_t *q) {
+    // One full block: realigned and compressed.
+    auto full_block = [&](const u32x4_a4 *v, uint32_t v16, uint32_t j) {
+        uint32_t m[16];
+        if (NOLOAD) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = *reinterpret_cast<const u32x4_a4 *>(q + 4 * i);
-        // the dword after the block starts inside the leaf whenever shift != 0 (and is ignored
-        // by the realignment when shift == 0: the load then re-reads the block's last dword,
-        // never one past the buffer); unconditional, so every block issues the same five loads
-        v16 = q[shift ? 16 : 15];
+            for (int i = 0; i < 16; ++i) m[i] = (uint32_t)ctr * 0x9E3779B9u + (uint32_t)(i * 0x01010101) + j;
+        } else {
+            const uint32_t dw[17] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
+                                     v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w, v16};
+#pragma unroll
+            for (int i = 0; i < 16; ++i) m[i] = __builtin_amdgcn_alignbyte(dw[i + 1], dw[i], shift);
+        }
+        b3_compress(cv, m, ctr, 64u, flags_of(j));
     };
-    if (nfull) {
-        // Full blocks.  The loop body is one basic block: the next block's words load into
-        // nn on every iteration (the last re-reads its own block) and move into nx at the
-        // latch, after the compression, so the loads' wait sits there.  With the tail block
-        // inside the loop and a conditional prefetch, the compiler merged the paths before
-        // the compression and waited (vmcnt) for the just-issued loads there: one load
-        // latency per block, ~15 % of the stage (scripts/diag_b3.py, no-load mode).
-        u32x4_a4 nx[4], nn[4];
-        uint32_t nx16 = 0, nn16 = 0;
-        if (!NOLOAD) fetch(nx, nx16, base);
+    const uint32_t npair = nfull / 2;
+    if (npair) {
+        // Full blocks two at a time: a lane reads whole 128-byte lines (one block at a time left
+        // the other half of each line to a later read, often after L2 had dropped it: 1.55 GB
+        // fetched per 1.07 GB, profiles/r02_v15_pmc_c3.json).  The loop body is one basic
+        // block: the next pair loads into pn on every iteration (the last re-reads its own
+        // pair), pinned before the compressions by a sched_barrier, and moves into px after
+        // them behind another, so the loads' wait sits there; the empty asm on px keeps the
+        // compiler from rotating the loads to the top of the iteration that consumes them.
+        // (With the tail block inside the loop and a conditional prefetch the compiler had
+        // waited for the just-issued loads before every compression: ~15 % of the stage.)
+        u32x4_a4 px[8], pn[8];
+        uint32_t px32 = 0, pn32 = 0;
+        auto fetch2 = [&](u32x4_a4 (&v)[8], uint32_t &v32, const uint32_t *q) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) v[i] = *reinterpret_cast<const u32x4_a4 *>(q + 4 * i);
+            // the dword after the pair starts inside the leaf whenever shift != 0 (ignored by
+            // the realignment when shift == 0: the load re-reads the pair's last dword)
+            v32 = q[shift ? 32 : 31];
+        };
+        if (!NOLOAD) fetch2(px, px32, base);
 #pragma unroll 1
-        for (uint32_t j = 0; j < nfull; ++j) {
-            uint32_t m[16];
-            if (NOLOAD) {
-#pragma unroll
-                for (int i = 0; i < 16; ++i) m[i] = (uint32_t)ctr * 0x9E3779B9u + (uint32_t)(i * 0x01010101) + j;
-            } else {
-                fetch(nn, nn16, base + 16 * (j + 1 < nfull ? j + 1 : j));
-                __builtin_amdgcn_sched_barrier(0);  // issued before the compression, not sunk after it
-                const uint32_t dw[17] = {nx[0].x, nx[0].y, nx[0].z, nx[0].w, nx[1].x, nx[1].y, nx[1].z, nx[1].w,
-                                         nx[2].x, nx[2].y, nx[2].z, nx[2].w, nx[3].x, nx[3].y, nx[3].z, nx[3].w,
-                                         nx16};
-#pragma unroll
-                for (int i = 0; i < 16; ++i) m[i] = __builtin_amdgcn_alignbyte(dw[i + 1], dw[i], shift);
-            }
-            b3_compress(cv, m, ctr, 64u, flags_of(j));
-            __builtin_amdgcn_sched_barrier(0);  // the move (and the wait it needs) after the compression
+        for (uint32_t jp = 0; jp < npair; ++jp) {
+            if (!NOLOAD) fetch2(pn, pn32, base + 32 * (jp + 1 < npair ? jp + 1 : jp));
+            __builtin_amdgcn_sched_barrier(0);  // issued before the compressions, not sunk after them
+            full_block(px, px[4].x, 2 * jp);
+            full_block(px + 4, px32, 2 * jp + 1);
+            __builtin_amdgcn_sched_barrier(0);  // the move (and the wait it needs) after them
             if (!NOLOAD) {
 #pragma unroll
-                for (int i = 0; i < 4; ++i) nx[i] = nn[i];
-                nx16 = nn16;
-                // opaque from here on: without it the compiler rotates the loop so that the
-                // loads are issued at the top of the iteration that consumes them and waited
-                // for at once (the prefetch undone); with it the wait stays here
-                asm volatile("" : "+v"(nx[0]), "+v"(nx[1]), "+v"(nx[2]), "+v"(nx[3]), "+v"(nx16));
+                for (int i = 0; i < 8; ++i) px[i] = pn[i];
+                px32 = pn32;
+                asm volatile("" : "+v"(px[0]), "+v"(px[1]), "+v"(px[2]), "+v"(px[3]), "+v"(px[4]), "+v"(px[5]),
+                             "+v"(px[6]), "+v"(px[7]), "+v"(px32));
             }
         }
+    }
+    if (nfull & 1u) {  // an odd last full block
+        const uint32_t j = nfull - 1;
+        u32x4_a4 v[4];
+        uint32_t v16 = 0;
+        if (!NOLOAD) {
+            const uint32_t *q = base + 16 * j;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = *reinterpret_cast<const u32x4_a4 *>(q + 4 * i);
+            v16 = q[shift ? 16 : 15];
+        }
+        full_block(v, v16, j);
     }
     if (nblk > nfull) {  // the partial last block (or the one empty block of n == 0)
         const uint32_t j = nfull;
