@@ -43,8 +43,10 @@ void launch_exclusive_scan_u32(const uint32_t *d_in, uint64_t *d_out, uint64_t n
                                hipStream_t st);
 size_t exclusive_scan_tmp_elems(uint64_t n);
 
-void launch_compact(const uint32_t *d_seg_count, const uint32_t *d_seg_cand, const uint64_t *d_eoff, uint32_t cap,
-                    uint64_t nseg, uint64_t *d_entries, hipStream_t st);
+// Exclusive scan of the per-segment candidate counts into d_eoff fused with the compaction of
+// the candidate slots into the sorted entry list.
+void launch_scan_compact(const uint32_t *d_seg_count, const uint32_t *d_seg_cand, uint64_t *d_eoff, uint32_t cap,
+                         uint64_t nseg, uint64_t *d_entries, uint64_t *d_tmp, hipStream_t st);
 
 // Piece lists for the walk of large NARs (walk.hip, k_walk_pieces); np = 0: none.
 struct WalkPiecesHost {

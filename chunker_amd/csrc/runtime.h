@@ -103,9 +103,9 @@ struct Workspace {
     int device = -1;
     hipStream_t stream = nullptr;
     uint64_t gear_epoch = 0;
-    DevBuf gear, seg_count, seg_cand, eoff, scan_tmp, entries, nar_off, cap_base, wchunk, nar_nchunks, nar_first,
+    DevBuf gear, seg_count, seg_cand, eoff, scan_tmp, entries, nar_off, wchunk, nar_nchunks, nar_first,
         chunk_abs, b3_gcount, b3_gbase, b3_gcv, b3_gmap, in, out, span_off, span_len, order, cas_order, ids,
-        man_abs, man_desc, sha_err, pc_first, pc_nar, pc_base, pc_count, pc_exit, pc_starts;
+        man_abs, man_desc, sha_err, pc_first, pc_count, pc_exit, pc_starts;
     PinBuf stage, err_stage;
     hipEvent_t ev[EV_N] = {};
     // CAS ids run on side_stream, concurrently with the digest: both stages are bound by

@@ -318,18 +318,16 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
             }
         }
         s_pfirst[n_nars] = g;
-        if ((rc = ws->pc_first.ensure((n_nars + 1) * 8, "walk pieces"))) return rc;
-        if ((rc = ws->pc_base.ensure(np * 8, "walk pieces"))) return rc;
-        if ((rc = ws->pc_nar.ensure(np * 4, "walk pieces"))) return rc;
+        // first / base / nar in one device block, filled by one copy from the staging block
+        // they are laid out in contiguously
+        if ((rc = ws->pc_first.ensure((n_nars + 1) * 8 + np * 12, "walk pieces"))) return rc;
         if ((rc = ws->pc_count.ensure(np * 4, "walk pieces"))) return rc;
         if ((rc = ws->pc_exit.ensure(np * 8, "walk pieces"))) return rc;
         if ((rc = ws->pc_starts.ensure(std::max<uint64_t>(lb, pcap) * 8, "walk pieces"))) return rc;
-        HIP_TRY(hipMemcpyAsync(ws->pc_first.p, s_pfirst, (n_nars + 1) * 8, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemcpyAsync(ws->pc_base.p, s_pbase, np * 8, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipMemcpyAsync(ws->pc_nar.p, s_pnar, np * 4, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(ws->pc_first.p, s_pfirst, (n_nars + 1) * 8 + np * 12, hipMemcpyHostToDevice, st));
         pieces.first = ws->pc_first.as<uint64_t>();
-        pieces.nar = ws->pc_nar.as<uint32_t>();
-        pieces.base = ws->pc_base.as<uint64_t>();
+        pieces.base = pieces.first + (n_nars + 1);
+        pieces.nar = reinterpret_cast<uint32_t *>(ws->pc_first.as<uint64_t>() + (n_nars + 1) + np);
         pieces.count = ws->pc_count.as<uint32_t>();
         pieces.exit = ws->pc_exit.as<uint64_t>();
         pieces.starts = ws->pc_starts.as<uint64_t>();
@@ -347,8 +345,9 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
     const uint64_t scan_n = std::max<uint64_t>({nseg, (uint64_t)n_nars, total_cap, 1});
     if ((rc = ws->scan_tmp.ensure(cg::exclusive_scan_tmp_elems(scan_n) * 8 + 64, "scan_tmp"))) return rc;
     if ((rc = ws->entries.ensure((nseg * slots + 1) * 8, "entries"))) return rc;
-    if ((rc = ws->nar_off.ensure((n_nars + 1) * 8, "nar_off"))) return rc;
-    if ((rc = ws->cap_base.ensure((n_nars + 1) * 8, "cap_base"))) return rc;
+    // nar_off (n+1) then cap_base (n+1): one block, one copy (s_cap follows s_off in staging)
+    if ((rc = ws->nar_off.ensure(2 * (n_nars + 1) * 8, "nar_off"))) return rc;
+    const uint64_t *d_nar_off = ws->nar_off.as<uint64_t>(), *d_cap_base = d_nar_off + (n_nars + 1);
     if ((rc = ws->wchunk.ensure((total_cap + 1) * 16, "wchunk"))) return rc;
     if ((rc = ws->nar_nchunks.ensure((n_nars + 1) * 4, "nar_nchunks"))) return rc;
     if ((rc = ws->nar_first.ensure((n_nars + 1) * 8, "nar_first"))) return rc;
@@ -361,25 +360,22 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
     }
 
     const bool prof = g_profiling.load() != 0;
-    HIP_TRY(hipMemcpyAsync(ws->nar_off.p, s_off, (n_nars + 1) * 8, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(ws->cap_base.p, s_cap, (n_nars + 1) * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ws->nar_off.p, s_off, 2 * (n_nars + 1) * 8, hipMemcpyHostToDevice, st));
     if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_START], st));  // scan stage = the scan kernel alone
 
     cg::launch_scan(d_data, total_len, ws->gear.as<uint64_t>(), P.mask_s, P.mask_l, slots,
                     ws->seg_count.as<uint32_t>(), ws->seg_cand.as<uint32_t>(), nseg, st);
     if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_SCAN], st));
-    cg::launch_exclusive_scan_u32(ws->seg_count.as<uint32_t>(), ws->eoff.as<uint64_t>(), nseg, slots,
-                                  ws->scan_tmp.as<uint64_t>(), st);
-    cg::launch_compact(ws->seg_count.as<uint32_t>(), ws->seg_cand.as<uint32_t>(), ws->eoff.as<uint64_t>(), slots,
-                       nseg, ws->entries.as<uint64_t>(), st);
+    cg::launch_scan_compact(ws->seg_count.as<uint32_t>(), ws->seg_cand.as<uint32_t>(), ws->eoff.as<uint64_t>(), slots,
+                            nseg, ws->entries.as<uint64_t>(), ws->scan_tmp.as<uint64_t>(), st);
     if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_COMPACT], st));
     cg::launch_walk(d_data, ws->gear.as<uint64_t>(), ws->entries.as<uint64_t>(), ws->eoff.as<uint64_t>(), nseg,
-                    ws->nar_off.as<uint64_t>(), ws->cap_base.as<uint64_t>(), n_nars, P, ws->wchunk.as<uint64_t>(),
+                    d_nar_off, d_cap_base, n_nars, P, ws->wchunk.as<uint64_t>(),
                     ws->nar_nchunks.as<uint32_t>(), pieces, st);
     if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_WALK], st));
     cg::launch_exclusive_scan_u32(ws->nar_nchunks.as<uint32_t>(), ws->nar_first.as<uint64_t>(), n_nars, 0,
                                   ws->scan_tmp.as<uint64_t>(), st);
-    cg::launch_assemble(ws->nar_off.as<uint64_t>(), ws->cap_base.as<uint64_t>(), ws->wchunk.as<uint64_t>(),
+    cg::launch_assemble(d_nar_off, d_cap_base, ws->wchunk.as<uint64_t>(),
                         ws->nar_first.as<uint64_t>(), n_nars, d_out, out_cap, ws->chunk_abs.as<uint64_t>(), st);
     if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_ASSEMBLE], st));
     const uint64_t *d_total = ws->nar_first.as<uint64_t>() + n_nars;

@@ -1665,7 +1665,7 @@ void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint
 }
 
 // ---------------------------------------------------------------------------
-// Exclusive prefix sum u32 -> u64 (three launches: tile sums, top scan, apply).
+// Exclusive prefix sum u32 -> u64 (one launch for small inputs; tile sums + apply otherwise).
 // ---------------------------------------------------------------------------
 #define SCAN_T 256u
 #define SCAN_ITEMS 8u
@@ -1720,71 +1720,166 @@ __global__ __launch_bounds__(1024) void k_top_scan(uint64_t *__restrict__ tile_s
     if (threadIdx.x == 0) tile_sum[ntiles] = s_carry;
 }
 
+// Optional fused compaction: the scan input is the per-segment candidate count and the
+// output its entry offset, so the thread that owns a segment's offset also moves that
+// segment's candidate slots into the sorted entry list (what k_compact did in its own launch).
+struct CompactArgs {
+    const uint32_t *cand;  // nseg * cap candidate slots (scan.hip k_scan_flat32 / k_scan)
+    uint64_t *entries;     // sorted entry list (position << 2 | tier)
+};
+
+__device__ __forceinline__ void compact_segment(uint64_t seg, uint32_t count, uint64_t base, uint32_t cap,
+                                                const CompactArgs &ca) {
+    if (count == 0) return;
+    const uint64_t start = seg * CG_SEG;
+    if (count <= cap) {
+        for (uint32_t k = 0; k < count; ++k) {
+            const uint32_t e = ca.cand[seg * cap + k];
+            ca.entries[base + k] = ((start + (e >> 2)) << 2) | (e & 3u);
+        }
+    } else {
+        ca.entries[base] = start << 2;  // dense-segment marker
+    }
+}
+
+// Second pass of the tiled scan.  REDUCE: tile_sum holds each tile's own total (k_tile_sums)
+// and a block sums its predecessors' (at most SCAN_REDUCE_MAX tiles, all L2-resident), so
+// the single-block k_top_scan launch is not needed; otherwise tile_sum is already the
+// exclusive scan of the tiles with the total at [ntiles].
+#define SCAN_REDUCE_MAX 4096u
+template <bool COMPACT, bool REDUCE>
 __global__ __launch_bounds__(SCAN_T) void k_scan_apply(const uint32_t *__restrict__ in, uint64_t n, uint32_t cap,
                                                        const uint64_t *__restrict__ tile_sum,
-                                                       uint64_t *__restrict__ out, uint64_t ntiles) {
+                                                       uint64_t *__restrict__ out, uint64_t ntiles, CompactArgs ca) {
     __shared__ uint64_t s_wave[SCAN_T / 64];
+    __shared__ uint64_t s_pre;
+    uint64_t tile_pre;
+    if (REDUCE) {
+        uint64_t p = 0;
+        for (uint64_t i = threadIdx.x; i < blockIdx.x; i += SCAN_T) p += tile_sum[i];
+        const uint64_t incp = block_inclusive_scan(p, s_wave);
+        if (threadIdx.x == SCAN_T - 1) s_pre = incp;
+        __syncthreads();
+        tile_pre = s_pre;
+    } else {
+        tile_pre = tile_sum[blockIdx.x];
+    }
     const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_ITEMS;
+    uint32_t raw[SCAN_ITEMS];
     uint64_t v[SCAN_ITEMS];
     uint64_t s = 0;
 #pragma unroll
     for (uint32_t k = 0; k < SCAN_ITEMS; ++k) {
-        v[k] = base + k < n ? xform(in[base + k], cap) : 0;
+        raw[k] = base + k < n ? in[base + k] : 0u;
+        v[k] = xform(raw[k], cap);
         s += v[k];
     }
     const uint64_t inc = block_inclusive_scan(s, s_wave);
-    uint64_t run = tile_sum[blockIdx.x] + inc - s;
+    uint64_t run = tile_pre + inc - s;
 #pragma unroll
     for (uint32_t k = 0; k < SCAN_ITEMS; ++k) {
-        if (base + k < n) out[base + k] = run;
+        if (base + k < n) {
+            out[base + k] = run;
+            if (COMPACT) compact_segment(base + k, raw[k], run, cap, ca);
+        }
         run += v[k];
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = tile_sum[ntiles];
+    if (REDUCE) {
+        if (blockIdx.x == ntiles - 1 && threadIdx.x == SCAN_T - 1) out[n] = tile_pre + inc;
+    } else if (blockIdx.x == 0 && threadIdx.x == 0) {
+        out[n] = tile_sum[ntiles];
+    }
+}
+
+// Whole scan in one block (n up to SCAN_SMALL_MAX): 1024 threads × SCAN_ITEMS per pass,
+// carry between passes.  Used for the per-NAR chunk counts, the BLAKE3 group counts and
+// small batches' segment counts, where three launches cost more than the work.
+#define SCAN_SMALL_T 1024u
+#define SCAN_SMALL_MAX (4u * SCAN_SMALL_T * SCAN_ITEMS)
+template <bool COMPACT>
+__global__ __launch_bounds__(SCAN_SMALL_T) void k_scan_small(const uint32_t *__restrict__ in, uint64_t n, uint32_t cap,
+                                                             uint64_t *__restrict__ out, CompactArgs ca) {
+    __shared__ uint64_t s_wave[SCAN_SMALL_T / 64];
+    __shared__ uint64_t s_carry;
+    uint64_t carry = 0;
+    for (uint64_t b = 0; b < n; b += (uint64_t)SCAN_SMALL_T * SCAN_ITEMS) {
+        const uint64_t base = b + threadIdx.x * SCAN_ITEMS;
+        uint32_t raw[SCAN_ITEMS];
+        uint64_t v[SCAN_ITEMS];
+        uint64_t s = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < SCAN_ITEMS; ++k) {
+            raw[k] = base + k < n ? in[base + k] : 0u;
+            v[k] = xform(raw[k], cap);
+            s += v[k];
+        }
+        const uint64_t inc = block_inclusive_scan(s, s_wave);
+        uint64_t run = carry + inc - s;
+#pragma unroll
+        for (uint32_t k = 0; k < SCAN_ITEMS; ++k) {
+            if (base + k < n) {
+                out[base + k] = run;
+                if (COMPACT) compact_segment(base + k, raw[k], run, cap, ca);
+            }
+            run += v[k];
+        }
+        if (threadIdx.x == SCAN_SMALL_T - 1) s_carry = carry + inc;
+        __syncthreads();
+        carry = s_carry;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) out[n] = carry;
 }
 
 size_t exclusive_scan_tmp_elems(uint64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE + 1; }
 
-void launch_exclusive_scan_u32(const uint32_t *d_in, uint64_t *d_out, uint64_t n, uint32_t cap, uint64_t *d_tmp,
-                               hipStream_t st) {
-    const uint64_t ntiles = n ? (n + SCAN_TILE - 1) / SCAN_TILE : 0;
-    if (ntiles == 0) {
+// One launch for n ≤ SCAN_SMALL_MAX, two up to SCAN_REDUCE_MAX tiles, three beyond.
+// Test hook (cg_test_scan_path): 0 = by size, 1 = one block, 2 = tile sums + reducing
+// apply, 3 = tile sums + top scan + apply, so a test reaches every path at small sizes.
+uint32_t g_scan_path = 0;
+
+template <bool COMPACT>
+static void launch_scan_impl(const uint32_t *d_in, uint64_t *d_out, uint64_t n, uint32_t cap, uint64_t *d_tmp,
+                             CompactArgs ca, hipStream_t st) {
+    if (n == 0) {
         (void)hipMemsetAsync(d_out, 0, sizeof(uint64_t), st);
         return;
     }
+    const uint32_t path = g_scan_path;
+    if (path == 1 || (path == 0 && n <= SCAN_SMALL_MAX)) {
+        hipLaunchKernelGGL(k_scan_small<COMPACT>, dim3(1), dim3(SCAN_SMALL_T), 0, st, d_in, n, cap, d_out, ca);
+        return;
+    }
+    const uint64_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
     hipLaunchKernelGGL(k_tile_sums, dim3((uint32_t)ntiles), dim3(SCAN_T), 0, st, d_in, n, cap, d_tmp);
-    hipLaunchKernelGGL(k_top_scan, dim3(1), dim3(1024), 0, st, d_tmp, ntiles);
-    hipLaunchKernelGGL(k_scan_apply, dim3((uint32_t)ntiles), dim3(SCAN_T), 0, st, d_in, n, cap, d_tmp, d_out,
-                       ntiles);
-}
-
-// ---------------------------------------------------------------------------
-// Compaction: per-segment candidate slots -> one sorted entry list.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_compact(const uint32_t *__restrict__ seg_count,
-                                                 const uint32_t *__restrict__ seg_cand,
-                                                 const uint64_t *__restrict__ eoff, uint32_t cap, uint64_t nseg,
-                                                 uint64_t *__restrict__ entries) {
-    const uint64_t seg = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (seg >= nseg) return;
-    const uint32_t count = seg_count[seg];
-    if (count == 0) return;
-    const uint64_t base = eoff[seg];
-    const uint64_t start = seg * CG_SEG;
-    if (count <= cap) {
-        for (uint32_t k = 0; k < count; ++k) {
-            const uint32_t e = seg_cand[seg * cap + k];
-            entries[base + k] = ((start + (e >> 2)) << 2) | (e & 3u);
-        }
+    if (path == 2 || (path == 0 && ntiles <= SCAN_REDUCE_MAX)) {
+        hipLaunchKernelGGL((k_scan_apply<COMPACT, true>), dim3((uint32_t)ntiles), dim3(SCAN_T), 0, st, d_in, n, cap,
+                           d_tmp, d_out, ntiles, ca);
     } else {
-        entries[base] = start << 2;  // dense-segment marker
+        hipLaunchKernelGGL(k_top_scan, dim3(1), dim3(1024), 0, st, d_tmp, ntiles);
+        hipLaunchKernelGGL((k_scan_apply<COMPACT, false>), dim3((uint32_t)ntiles), dim3(SCAN_T), 0, st, d_in, n, cap,
+                           d_tmp, d_out, ntiles, ca);
     }
 }
 
-void launch_compact(const uint32_t *d_seg_count, const uint32_t *d_seg_cand, const uint64_t *d_eoff, uint32_t cap,
-                    uint64_t nseg, uint64_t *d_entries, hipStream_t st) {
-    if (nseg == 0) return;
-    hipLaunchKernelGGL(k_compact, dim3((uint32_t)((nseg + 255) / 256)), dim3(256), 0, st, d_seg_count, d_seg_cand,
-                       d_eoff, cap, nseg, d_entries);
+void launch_exclusive_scan_u32(const uint32_t *d_in, uint64_t *d_out, uint64_t n, uint32_t cap, uint64_t *d_tmp,
+                               hipStream_t st) {
+    launch_scan_impl<false>(d_in, d_out, n, cap, d_tmp, CompactArgs{nullptr, nullptr}, st);
+}
+
+// ---------------------------------------------------------------------------
+// Compaction: per-segment candidate slots -> one sorted entry list, fused into the
+// exclusive scan of the per-segment counts (eoff = each segment's first entry).
+// ---------------------------------------------------------------------------
+void launch_scan_compact(const uint32_t *d_seg_count, const uint32_t *d_seg_cand, uint64_t *d_eoff, uint32_t cap,
+                         uint64_t nseg, uint64_t *d_entries, uint64_t *d_tmp, hipStream_t st) {
+    launch_scan_impl<true>(d_seg_count, d_eoff, nseg, cap, d_tmp, CompactArgs{d_seg_cand, d_entries}, st);
 }
 
 }  // namespace cg
+
+extern "C" uint32_t cg_test_scan_path(uint32_t v) {
+    const uint32_t old = cg::g_scan_path;
+    cg::g_scan_path = v <= 3 ? v : 0;
+    return old;
+}

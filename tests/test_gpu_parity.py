@@ -597,3 +597,30 @@ def test_blake3_tree_shapes(ca, O, mx):
     got = ca.chunk_batch([data], *params, hash=B3)[0]
     want = O.chunk_descriptors(data, *params, algo=B3)
     assert_same(got, want, f"max={mx}")
+
+
+@pytest.mark.parametrize("path", [1, 2, 3], ids=["one_block", "reduce", "top_scan"])
+def test_scan_paths_agree(ca, O, path):
+    """Every exclusive-scan path (scan.hip launch_scan_impl: one block, tile sums + a
+    reducing apply, tile sums + top scan + apply), forced by the cg_test_scan_path hook at
+    sizes where the default would pick another, gives the oracle's descriptors: the segment
+    scan with its fused compaction (dense segments included), the per-NAR chunk counts and
+    the BLAKE3 group counts."""
+    rng = np.random.default_rng(31)
+    lens = [0, 1, 1025, 65_535, 333_333, 2_000_003, 7, 4_194_305, 3_000_001]
+    nars = [rng.integers(0, 256, n, dtype=np.uint8) for n in lens]
+    params = (4096, 16384, 65536)
+    bits = 14
+    a = rng.integers(0, 256, params[1] + params[1] // 3, dtype=np.uint8)
+    dense = np.concatenate([a, _dense_region(O, rng, a, 16 * 1024, int(O.MASKS[bits - 1])),
+                            rng.integers(0, 256, 3 * params[2], dtype=np.uint8)])
+    old = ca.lib.cg_test_scan_path(path)
+    try:
+        for algo in (SHA, B3):
+            got = ca.chunk_batch(nars, *params, hash=algo)
+            for i, nar in enumerate(nars):
+                assert_same(got[i], O.chunk_descriptors(nar, *params, algo=algo), f"path={path} nar{i} algo={algo}")
+            got = ca.chunk_descriptors_array(dense, *params, hash=algo)
+            assert_same(got, O.chunk_descriptors(dense, *params, algo=algo), f"path={path} dense algo={algo}")
+    finally:
+        ca.lib.cg_test_scan_path(old)
