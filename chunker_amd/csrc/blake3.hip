@@ -276,6 +276,50 @@ __global__ __launch_bounds__(256) void k_b3_map(const uint64_t *__restrict__ gro
     for (uint64_t g = group_base[c]; g < group_base[c + 1]; ++g) gmap[g] = (uint32_t)c;
 }
 
+// k_b3_count + the exclusive scan + k_b3_map in one single-block launch, for batches of
+// up to B3_PLAN_MAX chunk slots (config 3: ~4,400): 1024 threads, 8 consecutive chunks
+// each per pass, group counts scanned with a carry between passes, each thread then
+// writes its chunks' group -> chunk entries.  group_base[max_chunks] = the group total,
+// as the scan writes.  (Interleaving the chunks over the threads -- coalesced descriptor
+// loads, one chunk's entries per thread per 1024-chunk slice, 8 block scans per pass --
+// took 41 us per config-3 batch against this form's 12.6 and the three kernels' 14.)
+#define B3_PLAN_T 1024u
+#define B3_PLAN_ITEMS 8u
+#define B3_PLAN_MAX (4u * B3_PLAN_T * B3_PLAN_ITEMS)
+template <uint32_t LPL>
+__global__ __launch_bounds__(B3_PLAN_T) void k_b3_plan(const DescRaw *__restrict__ desc,
+                                                       const uint64_t *__restrict__ total_p, uint64_t max_chunks,
+                                                       uint64_t *__restrict__ group_base, uint32_t *__restrict__ gmap) {
+    __shared__ uint64_t s_wave[B3_PLAN_T / 64];
+    __shared__ uint64_t s_carry;
+    uint64_t total = *total_p;
+    if (total > max_chunks) total = max_chunks;
+    uint64_t carry = 0;
+    for (uint64_t b = 0; b < max_chunks; b += (uint64_t)B3_PLAN_T * B3_PLAN_ITEMS) {
+        const uint64_t c0 = b + threadIdx.x * B3_PLAN_ITEMS;
+        uint32_t cnt[B3_PLAN_ITEMS];
+        uint64_t s = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < B3_PLAN_ITEMS; ++k) {
+            cnt[k] = c0 + k < total ? (uint32_t)b3_groups_of<LPL>(desc[c0 + k].length) : 0u;
+            s += cnt[k];
+        }
+        const uint64_t inc = block_inclusive_scan(s, s_wave);
+        uint64_t run = carry + inc - s;
+#pragma unroll
+        for (uint32_t k = 0; k < B3_PLAN_ITEMS; ++k) {
+            if (c0 + k < max_chunks) group_base[c0 + k] = run;
+            for (uint32_t g = 0; g < cnt[k]; ++g) gmap[run + g] = (uint32_t)(c0 + k);
+            run += cnt[k];
+        }
+        if (threadIdx.x == B3_PLAN_T - 1) s_carry = carry + inc;
+        __syncthreads();
+        carry = s_carry;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) group_base[max_chunks] = carry;
+}
+
 // The chaining value of leaves [leaf0, leaf0 + r) of a chunk (r = 1..4, the subtree of
 // one lane): leaf CVs folded pairwise, the odd third leaf paired last (left-complete);
 // ROOT on the last compression when the chunk is this subtree (`root`).
@@ -678,6 +722,7 @@ void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
     // product: one leaf per lane, folds deferred to k_b3_fold when the caller sized d_gcv
     // for the leaf values (with_lcv), else folded in-wave
     auto count = k_b3_count<1>;
+    auto plan = k_b3_plan<1>;
     bool defer = with_lcv;
     auto groups = defer ? k_b3_groups<0, 1, true> : k_b3_groups<0, 1>;
     uint64_t gbound = blake3_group_bound(total_bytes, max_chunks);
@@ -695,14 +740,20 @@ void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
     case 16:
         groups = k_b3_groups<0, 4>;
         count = k_b3_count<4>;
+        plan = k_b3_plan<4>;
         gbound = total_bytes / (65536 * 4) + max_chunks + 1;
         break;
     default: break;
     }
 #endif
-    hipLaunchKernelGGL(count, dim3(cblocks), dim3(256), 0, st, desc, d_total, max_chunks, d_gcount_u32);
-    launch_exclusive_scan_u32(d_gcount_u32, d_group_base, max_chunks, 0, d_scan_tmp, st);
-    hipLaunchKernelGGL(k_b3_map, dim3(cblocks), dim3(256), 0, st, d_group_base, d_total, max_chunks, d_gmap);
+    // (a forced scan path, cg_test_scan_path, takes the three-kernel form so tests reach it)
+    if (max_chunks <= B3_PLAN_MAX && g_scan_path == 0) {
+        hipLaunchKernelGGL(plan, dim3(1), dim3(B3_PLAN_T), 0, st, desc, d_total, max_chunks, d_group_base, d_gmap);
+    } else {
+        hipLaunchKernelGGL(count, dim3(cblocks), dim3(256), 0, st, desc, d_total, max_chunks, d_gcount_u32);
+        launch_exclusive_scan_u32(d_gcount_u32, d_group_base, max_chunks, 0, d_scan_tmp, st);
+        hipLaunchKernelGGL(k_b3_map, dim3(cblocks), dim3(256), 0, st, d_group_base, d_total, max_chunks, d_gmap);
+    }
     hipLaunchKernelGGL(groups,
                        dim3((uint32_t)((gbound + B3_WAVES - 1) / B3_WAVES)), dim3(64 * B3_WAVES), 0, st, d_data, d_abs,
                        desc, d_total, max_chunks, d_group_base, d_gmap, d_hash_base, hash_stride, d_gcv, d_lcv);

@@ -34,6 +34,23 @@ struct CdcParams {
 // Kernel launch wrappers (defined next to their kernels).
 namespace cg {
 
+// Block-wide inclusive scan of one u64 per thread (wave64 shuffles + LDS).
+__device__ __forceinline__ uint64_t block_inclusive_scan(uint64_t v, uint64_t *s_wave) {
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint64_t t = __shfl_up(v, d, 64);
+        if (lane >= d) v += t;
+    }
+    if (lane == 63) s_wave[wave] = v;
+    __syncthreads();
+    uint64_t add = 0;
+    for (uint32_t w = 0; w < wave; ++w) add += s_wave[w];
+    __syncthreads();
+    return v + add;
+}
+
+
 void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint64_t mask_s, uint64_t mask_l,
                  uint32_t cap, uint32_t *d_seg_count, uint32_t *d_seg_cand, uint64_t nseg, hipStream_t st);
 
@@ -42,6 +59,7 @@ void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint
 void launch_exclusive_scan_u32(const uint32_t *d_in, uint64_t *d_out, uint64_t n, uint32_t cap, uint64_t *d_tmp,
                                hipStream_t st);
 size_t exclusive_scan_tmp_elems(uint64_t n);
+extern uint32_t g_scan_path;  // test hook cg_test_scan_path (scan.hip)
 
 // Exclusive scan of the per-segment candidate counts into d_eoff fused with the compaction of
 // the candidate slots into the sorted entry list.

@@ -1673,22 +1673,6 @@ void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint
 
 __device__ __forceinline__ uint64_t xform(uint32_t v, uint32_t cap) { return cap ? (v <= cap ? v : 1u) : v; }
 
-// Block-wide inclusive scan of one u64 per thread (wave64 shuffles + LDS).
-__device__ __forceinline__ uint64_t block_inclusive_scan(uint64_t v, uint64_t *s_wave) {
-    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint64_t t = __shfl_up(v, d, 64);
-        if (lane >= d) v += t;
-    }
-    if (lane == 63) s_wave[wave] = v;
-    __syncthreads();
-    uint64_t add = 0;
-    for (uint32_t w = 0; w < wave; ++w) add += s_wave[w];
-    __syncthreads();
-    return v + add;
-}
-
 __global__ __launch_bounds__(SCAN_T) void k_tile_sums(const uint32_t *__restrict__ in, uint64_t n, uint32_t cap,
                                                       uint64_t *__restrict__ tile_sum) {
     __shared__ uint64_t s_wave[SCAN_T / 64];
