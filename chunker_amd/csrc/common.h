@@ -84,9 +84,11 @@ void launch_walk(const uint8_t *d_data, const uint64_t *d_gear, const uint64_t *
                  CdcParams p, uint64_t *d_wchunk, uint32_t *d_nar_nchunks, const WalkPiecesHost &pieces,
                  hipStream_t st);
 
+// exclusive scan of the per-NAR chunk counts into d_nar_first (total at [n_nars]) + the
+// descriptors and absolute chunk offsets of every NAR's chunks
 void launch_assemble(const uint64_t *d_nar_off, const uint64_t *d_cap_base, const uint64_t *d_wchunk,
-                     const uint64_t *d_nar_first, uint64_t n_nars, void *d_out, uint64_t out_cap,
-                     uint64_t *d_chunk_abs, hipStream_t st);
+                     const uint32_t *d_nar_nchunks, uint64_t *d_nar_first, uint64_t n_nars, void *d_out,
+                     uint64_t out_cap, uint64_t *d_chunk_abs, uint64_t *d_scan_tmp, hipStream_t st);
 
 // d_order_tmp (sha256_order_tmp_elems(max_chunks) u32, or nullptr = identity order) holds
 // the longest-first lane order; max_len bounds every chunk length (bucket width);

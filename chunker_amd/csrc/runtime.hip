@@ -373,10 +373,9 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
                     d_nar_off, d_cap_base, n_nars, P, ws->wchunk.as<uint64_t>(),
                     ws->nar_nchunks.as<uint32_t>(), pieces, st);
     if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_WALK], st));
-    cg::launch_exclusive_scan_u32(ws->nar_nchunks.as<uint32_t>(), ws->nar_first.as<uint64_t>(), n_nars, 0,
-                                  ws->scan_tmp.as<uint64_t>(), st);
-    cg::launch_assemble(d_nar_off, d_cap_base, ws->wchunk.as<uint64_t>(),
-                        ws->nar_first.as<uint64_t>(), n_nars, d_out, out_cap, ws->chunk_abs.as<uint64_t>(), st);
+    cg::launch_assemble(d_nar_off, d_cap_base, ws->wchunk.as<uint64_t>(), ws->nar_nchunks.as<uint32_t>(),
+                        ws->nar_first.as<uint64_t>(), n_nars, d_out, out_cap, ws->chunk_abs.as<uint64_t>(),
+                        ws->scan_tmp.as<uint64_t>(), st);
     if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_ASSEMBLE], st));
     const uint64_t *d_total = ws->nar_first.as<uint64_t>() + n_nars;
     uint8_t *d_man = nullptr;

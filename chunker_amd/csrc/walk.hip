@@ -409,9 +409,56 @@ __global__ __launch_bounds__(64) void k_assemble(const uint64_t *__restrict__ na
     }
 }
 
+// k_assemble with the exclusive scan of the per-NAR chunk counts folded in: NAR i's wave
+// sums the counts of NARs 0..i-1 itself (at most ASM_FUSED_MAX - 1 of them, L2-resident)
+// and writes nar_first[i] (the last NAR also the total, nar_first[n_nars]), so batches of
+// up to ASM_FUSED_MAX NARs take one launch instead of the scan's and the assembly's.
+#define ASM_FUSED_MAX 8192u
+__global__ __launch_bounds__(64) void k_assemble_counts(const uint64_t *__restrict__ nar_off,
+                                                        const uint64_t *__restrict__ cap_base,
+                                                        const uint64_t *__restrict__ wchunk,
+                                                        const uint32_t *__restrict__ nar_nchunks,
+                                                        uint64_t *__restrict__ nar_first, uint64_t n_nars,
+                                                        DescRaw *__restrict__ out, uint64_t out_cap,
+                                                        uint64_t *__restrict__ chunk_abs) {
+    const uint64_t i = blockIdx.x;
+    if (i >= n_nars) return;
+    const uint32_t lane = threadIdx.x;
+    uint64_t pre = 0;
+    for (uint64_t j = lane; j < i; j += 64) pre += nar_nchunks[j];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)pre, d, 64);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(pre >> 32), d, 64);
+        pre += ((uint64_t)hi << 32) | lo;
+    }
+    const uint64_t first = pre, cnt = nar_nchunks[i];
+    if (lane == 0) {
+        nar_first[i] = first;
+        if (i == n_nars - 1) nar_first[n_nars] = first + cnt;
+    }
+    const uint64_t *w = wchunk + 2 * cap_base[i];
+    const uint64_t base = nar_off[i];
+    for (uint64_t k = lane; k < cnt; k += 64) {
+        const uint64_t g = first + k;
+        if (g >= out_cap) break;
+        const uint64_t abs = w[2 * k];
+        out[g].offset = abs - base;
+        out[g].length = w[2 * k + 1];
+        chunk_abs[g] = abs;
+    }
+}
+
 void launch_assemble(const uint64_t *d_nar_off, const uint64_t *d_cap_base, const uint64_t *d_wchunk,
-                     const uint64_t *d_nar_first, uint64_t n_nars, void *d_out, uint64_t out_cap,
-                     uint64_t *d_chunk_abs, hipStream_t st) {
+                     const uint32_t *d_nar_nchunks, uint64_t *d_nar_first, uint64_t n_nars, void *d_out,
+                     uint64_t out_cap, uint64_t *d_chunk_abs, uint64_t *d_scan_tmp, hipStream_t st) {
+    // (a forced scan path, cg_test_scan_path, takes the two-kernel form so tests reach it)
+    if (n_nars > 0 && n_nars <= ASM_FUSED_MAX && g_scan_path == 0) {
+        hipLaunchKernelGGL(k_assemble_counts, dim3((uint32_t)n_nars), dim3(64), 0, st, d_nar_off, d_cap_base,
+                           d_wchunk, d_nar_nchunks, d_nar_first, n_nars, (DescRaw *)d_out, out_cap, d_chunk_abs);
+        return;
+    }
+    launch_exclusive_scan_u32(d_nar_nchunks, d_nar_first, n_nars, 0, d_scan_tmp, st);
     if (n_nars == 0) return;
     hipLaunchKernelGGL(k_assemble, dim3((uint32_t)n_nars), dim3(64), 0, st, d_nar_off, d_cap_base, d_wchunk,
                        d_nar_first, n_nars, (DescRaw *)d_out, out_cap, d_chunk_abs);
