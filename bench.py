@@ -70,6 +70,9 @@ def parse_args():
     ap.add_argument("--concurrent-only", action="store_true", help="only the in-flight measurement (profiling)")
     ap.add_argument("--hw-queues", type=int, default=16, choices=range(0, 33), metavar="0..32",
                     help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N > 1: nccl = RCCL over xGMI, one GPU per rank (the product); gloo = host-copy "
+                         "gather, ranks may share a GPU (rehearses the N > 1 path on a one-GPU box)")
     return ap.parse_args()
 
 
@@ -105,14 +108,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    nccl = args.dist_backend == "nccl"
+    if world > 1 and nccl:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    elif world > 1:
+        # gloo rehearsal: ranks beyond the box's GPU count share them (RCCL would refuse
+        # two ranks on one GPU); the gather runs on host copies of the descriptors.
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
 
     import chunker_amd as ca
-    from chunker_amd.dist import gather_batch, shard_nars
+    from chunker_amd.dist import check_gathered_batch, gather_batch, shard_nars
     from chunker_amd.nar import synth_nars_device
 
     n_per, nar_bytes, params, algo, desc = CONFIGS[args.config]
@@ -128,11 +137,14 @@ def main():
     stream = torch.cuda.current_stream()
     sptr = stream.cuda_stream
 
+    gathered = [None]
+
     def step():
         first = ca.chunk_batch_device(d_data.data_ptr(), offs, d_out.data_ptr(), cap, *params, hash=algo,
                                       stream=sptr)
         if world > 1:  # descriptors + NAR index to rank 0 over RCCL (the path's only exchange)
-            gather_batch(d_out, first)
+            mine_d = d_out if nccl else d_out[: int(first[-1]) * 48].cpu()
+            gathered[0] = gather_batch(mine_d, first)
         return first
 
     for _ in range(args.warmup):
@@ -157,19 +169,27 @@ def main():
     elapsed = time.perf_counter() - t0
     ca.lib.cg_set_profiling(0)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if nccl else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     n_chunks = int(first[-1])
     stages_ms = dict(zip(["scan", "compact", "walk", "assemble", "digest"],
                          stage[: max(args.steps, 1)].mean(axis=0).round(4)))
 
-    # parity spot check on the last step: descriptors cover every NAR exactly
+    # parity spot check on the last step: descriptors cover every NAR exactly -- this
+    # rank's own batch, and at N > 1 the whole batch as gathered on rank 0 (global NAR
+    # order, every NAR of every rank tiled contiguously)
     descs = d_out[: n_chunks * 48].cpu().numpy().view(ca.DESC_DTYPE)
-    for i in range(len(mine)):
-        a, b = int(first[i]), int(first[i + 1])
-        assert b > a and descs["offset"][a] == 0
-        assert int(descs["offset"][b - 1] + descs["length"][b - 1]) == nar_bytes
+    check_gathered_batch(descs, first, sizes)
+    gather_check = None
+    if world > 1 and rank == 0:
+        g_desc, g_first = gathered[0]
+        g_np = g_desc.cpu().numpy().view(ca.DESC_DTYPE)
+        check_gathered_batch(g_np, g_first, np.full(n_per * world, nar_bytes, np.uint64))
+        gather_check = {"nars": n_per * world, "chunks": int(g_first[-1]), "backend": args.dist_backend,
+                        "rank0_prefix_equal": bool(np.array_equal(g_np[:n_chunks].view(np.uint8),
+                                                                  descs.view(np.uint8)))}
+        assert gather_check["rank0_prefix_equal"], "rank 0's own descriptors differ inside the gathered batch"
 
     total_all = total_bytes * world
     value = total_all * args.steps / elapsed / GIB
@@ -191,7 +211,7 @@ def main():
                         "traffic": None},
     }
     if algo == 1:
-        roofline["latency_floor"] = sha_chain_floor(descs, len(mine), total_bytes, params, dig_ms)
+        roofline["latency_floor"] = sha_chain_floor(ca, descs, dig_ms)
     dig_kernels = ["k_sha256"] if algo == 1 else ["k_b3_groups", "k_b3_fold", "k_b3_top"]
     traffic, src = pmc_traffic(args.config, dig_kernels)
     if traffic is not None:
@@ -226,7 +246,8 @@ def main():
             "dtype": "u8",
             "data": "synthetic (xorshift64 NAR payloads)" if not args.zeros else "synthetic (all-zero NAR payloads)",
             "config": {"workload": desc, "nars_per_gpu": len(mine), "nar_bytes": nar_bytes,
-                       "params": list(params), "parallelism": f"nar-shard x{world}"},
+                       "params": list(params), "parallelism": f"nar-shard x{world}",
+                       **({"dist_backend": args.dist_backend} if world > 1 else {})},
             "gear_table": gear,
             "chunks": n_chunks,
             "stages_ms": stages_ms,
@@ -234,6 +255,12 @@ def main():
             "cpu_baseline": cpu,
             "concurrent": conc,
         }
+        if gather_check is not None:
+            line["gather_check"] = gather_check
+            if not nccl:
+                line["note"] = (f"gloo rehearsal of the N > 1 path: {world} ranks on "
+                                f"{min(world, torch.cuda.device_count())} GPU(s), host-copy gather; "
+                                "not a scaling measurement")
         print(json.dumps(line))
     if world > 1:
         dist.destroy_process_group()
@@ -289,19 +316,23 @@ def concurrent_rates(ca, torch, args, n_per, nar_bytes, params, algo):
     return res
 
 
-def sha_chain_floor(descs, n_nars, total_bytes, params, dig_ms):
+def sha_chain_floor(ca, descs, dig_ms):
     """The SHA-256 digest stage cannot end before the longest chunk's serial chain of
     64-round compressions has issued: blocks x 64 x (VALU per round x ~4.64 clocks,
-    lone-wave issue cost measured by scripts/diag_sha_split.py: 41.8 quad, 46.5 pair)
-    at 2.4 GHz.  The tier rule mirrors sha256_grid (quads when the expected chunk
-    count leaves <= 256 x 64 chunks for one-lane workgroups)."""
+    lone-wave issue cost measured by scripts/diag_sha_split.py: 41.8 quad, 46.5 pair,
+    59.4 one-lane) at 2.4 GHz.  The tier is the one the library's last digest launch
+    gave the longest chunk (cg_last_sha_tiers: the length order hands the longest
+    chunks to the quad workgroups first, then pairs, then one-lane workgroups)."""
+    tiers = (np.ctypeslib.ctypes.c_uint32 * 4)()
+    ca.lib.cg_last_sha_tiers(tiers)
+    nquad, npair, nlane, pad = (int(t) for t in tiers)
+    tier = "quad" if nquad else "pair" if npair else "one-lane"
+    cyc = {"quad": 41.8, "pair": 46.5, "one-lane": 59.4}[tier]
     longest = int(descs["length"].max()) if len(descs) else 0
     blocks = (longest + 9 + 63) // 64
-    expected = total_bytes // (params[0] + params[1]) + n_nars
-    quad = expected <= 8 * 256 + 32 * 256 + 256 * 64
-    cyc = 41.8 if quad else 46.5
     floor_ms = blocks * 64 * cyc / 2.4e9 * 1e3
-    return {"longest_chunk_bytes": longest, "blocks": blocks, "tier": "quad" if quad else "pair",
+    return {"longest_chunk_bytes": longest, "blocks": blocks, "tier": tier,
+            "workgroups": {"quad": nquad, "pair": npair, "one_lane": nlane, "lds_pad": pad},
             "cycles_per_round": cyc, "clock_GHz": 2.4, "floor_ms": round(floor_ms, 3),
             "frac": round(floor_ms / dig_ms, 4) if dig_ms else None}
 

@@ -843,6 +843,10 @@ uint32_t sha256_grid(uint64_t max_chunks, uint64_t expected, uint32_t *nquad_out
     return (uint32_t)(nq + np + (rest + 63) / 64);
 }
 
+// Shape of this thread's last digest launch (cg_last_sha_tiers): quad, pair and
+// one-lane workgroups, dynamic LDS pad bytes.
+thread_local uint32_t t_sha_tiers[4];
+
 void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
                    uint64_t max_chunks, uint64_t expected, uint64_t max_len, uint32_t *d_order_tmp,
                    uint8_t *d_hash_base, size_t hash_stride, uint32_t *d_err, hipStream_t st) {
@@ -856,6 +860,10 @@ void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
     // a CU's 160 KiB so no two workgroups share a CU, and a consumer wave never shares a
     // SIMD with another workgroup's wave (which costs it 20-90 % per round).
     const size_t pad = nwg <= 256 ? 16384 : 0;
+    t_sha_tiers[0] = nquad;
+    t_sha_tiers[1] = npair;
+    t_sha_tiers[2] = nwg - nquad - npair;
+    t_sha_tiers[3] = (uint32_t)pad;
     hipLaunchKernelGGL(k_sha256, dim3(nwg), dim3(128), pad, st, d_data, d_abs,
                        (const DescRaw *)d_desc, d_total, max_chunks, order, d_hash_base, hash_stride, g_sha_diag,
                        g_sha_mode, nquad, npair, g_sha_spin_limit, d_err);
@@ -944,6 +952,11 @@ extern "C" uint32_t cg_diag_sha_grid(uint64_t max_chunks, uint64_t expected) {
     return cg::sha256_grid(max_chunks, expected, nullptr, nullptr);
 }
 #endif  // CG_DIAG
+
+extern "C" int cg_last_sha_tiers(uint32_t out[4]) {
+    for (int i = 0; i < 4; ++i) out[i] = cg::t_sha_tiers[i];
+    return (cg::t_sha_tiers[0] | cg::t_sha_tiers[1] | cg::t_sha_tiers[2]) ? 1 : 0;
+}
 
 // Test hooks: tier caps of the digest launch (the parity tests force every tier mix)
 // and the spin-guard limit (a test drives the timeout path); each returns the old value.

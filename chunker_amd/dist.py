@@ -77,3 +77,36 @@ def gather_batch(desc: torch.Tensor, nar_first, group=None):
         firsts.append(f[1:] + np.uint64(base))
         base += int(f[-1])
     return torch.cat(parts) if parts else desc[:0], np.concatenate(firsts)
+
+
+def check_gathered_batch(descs: np.ndarray, first, nar_sizes) -> None:
+    """Structural check of a batch gathered on rank 0 (bench.py runs it at N > 1 before
+    printing): `first` (global NAR -> first-descriptor index, n_nars + 1 entries) starts
+    at 0, strictly increases (every non-empty NAR has >= 1 chunk, an empty one none) and
+    ends at the descriptor count; inside every NAR the descriptors tile [0, size) in
+    order with no gap, overlap or empty chunk (src/chunking.rs:567-570).  Raises
+    AssertionError naming the first NAR that fails."""
+    first = np.asarray(first, dtype=np.int64)
+    sizes = np.asarray(nar_sizes, dtype=np.int64)
+    assert len(first) == len(sizes) + 1, f"nar_first has {len(first)} entries for {len(sizes)} NARs"
+    assert first[0] == 0 and first[-1] == len(descs), f"nar_first ends at {first[-1]}, {len(descs)} descriptors"
+    counts = np.diff(first)
+    bad = np.flatnonzero((counts < 0) | ((counts == 0) != (sizes == 0)))
+    assert not len(bad), f"NAR {bad[0]}: {counts[bad[0]]} chunks for {sizes[bad[0]]} bytes"
+    if not len(descs):
+        return
+    off = descs["offset"].astype(np.int64)
+    ln = descs["length"].astype(np.int64)
+    assert (ln > 0).all(), f"empty chunk at descriptor {int(np.flatnonzero(ln <= 0)[0])}"
+    nar_of = np.repeat(np.arange(len(sizes)), counts)
+    start = first[:-1][counts > 0]
+    # within a NAR: the first chunk at 0, each next one where the previous ended
+    expect = np.empty_like(off)
+    expect[1:] = off[:-1] + ln[:-1]
+    expect[start] = 0
+    gap = np.flatnonzero(off != expect)
+    assert not len(gap), f"NAR {nar_of[gap[0]]}: descriptor {gap[0]} at offset {off[gap[0]]}, expected {expect[gap[0]]}"
+    last = first[1:][counts > 0] - 1
+    end = off[last] + ln[last]
+    short = np.flatnonzero(end != sizes[counts > 0])
+    assert not len(short), f"NAR {np.flatnonzero(counts > 0)[short[0]]}: chunks end at {end[short[0]]}"

@@ -211,6 +211,14 @@ int cg_tables_verified(void); /* 1 once the installed set passed cg_selftest */
 void cg_set_profiling(int on);
 size_t cg_last_stage_times(double *ms, size_t n);
 
+/* Shape of the last SHA-256 digest launch on this thread (K3 k_sha256 work units):
+ * out = {quad workgroups (8 chunks, 8 lanes each), pair workgroups (32 chunks, 2 lanes
+ * each), one-lane workgroups (64 chunks), LDS pad bytes (non-zero: one workgroup per
+ * CU)}.  The quad tier holds the longest chunks (length order), so the digest stage's
+ * latency floor is the longest chunk's blocks x 64 rounds at the quad tier's cycles per
+ * round when out[0] > 0.  Returns 1 if this thread has launched a SHA-256 digest. */
+int cg_last_sha_tiers(uint32_t out[4]);
+
 /* Synthetic NAR writer: nix-archive-1 framing around an
  * xorshift64 payload (crates/node/src/lib.rs:192-203) with seed
  * 0x9E3779B97F4A7C15 ^ (first_index + i), or zeros.  NAR i is nar_sizes[i] bytes

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Round 3, first session: the N > 1 path rehearsed on the one-GPU box (2 ranks over
+# gloo, rank-0 check of the gathered batch), the dist GPU tests, config-4 bench with the
+# exported digest tiers, and the host's CPU share.  Every GPU step has its own time limit.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-.}"
+mkdir -p gpurun_out
+{ echo "nproc=$(nproc) affinity=$(python3 -c 'import os; print(len(os.sched_getaffinity(0)))') OMP=$OMP_NUM_THREADS MAX_JOBS=$MAX_JOBS";
+  cat /sys/fs/cgroup/cpu.max 2>/dev/null; grep -m1 "model name" /proc/cpuinfo; } > gpurun_out/cpuinfo.txt
+timeout -k 10 300 python -u -m pytest tests/test_dist.py -x -v -m gpu --timeout 200 --timeout-method thread > gpurun_out/pytest_dist.log 2>&1 \
+ && echo "dist tests ok" \
+ && timeout -k 10 300 python bench.py --gpus 2 --dist-backend gloo --steps 3 --warmup 1 --no-cpu-baseline --no-concurrent > gpurun_out/bench_g2_gloo.json 2> gpurun_out/bench_g2_gloo.err \
+ && cat gpurun_out/bench_g2_gloo.json \
+ && timeout -k 10 300 python bench.py --config c4 --steps 3 --warmup 1 --no-cpu-baseline --no-concurrent > gpurun_out/bench_c4.json 2> gpurun_out/bench_c4.err \
+ && cat gpurun_out/bench_c4.json
+rc=$?
+echo "rc=$rc"
+cat gpurun_out/cpuinfo.txt
+tail -3 gpurun_out/pytest_dist.log
+exit $rc

@@ -173,3 +173,34 @@ def test_gpu_sharded_batch_matches_oracle(n_total):
         first.append(first[-1] + len(dsc))
     assert got_first == first
     assert got_bytes == np.concatenate(want).tobytes()
+
+
+def test_check_gathered_batch():
+    """The rank-0 structural check bench.py runs on the gathered batch accepts a
+    well-formed batch and names the NAR of every kind of defect."""
+    from chunker_amd.dist import check_gathered_batch
+    from oracle import oracle as O
+
+    sizes = np.array([10, 0, 7, 5], np.uint64)
+    d = np.zeros(5, O.DESC_DTYPE)
+    d["offset"] = [0, 4, 0, 0, 3]
+    d["length"] = [4, 6, 7, 3, 2]
+    first = np.array([0, 2, 2, 3, 5], np.uint64)
+    check_gathered_batch(d, first, sizes)
+    check_gathered_batch(np.zeros(0, O.DESC_DTYPE), np.zeros(3, np.uint64), [0, 0])
+    bad = d.copy()
+    bad["offset"][1] = 5  # gap inside NAR 0
+    with pytest.raises(AssertionError, match="NAR 0"):
+        check_gathered_batch(bad, first, sizes)
+    bad = d.copy()
+    bad["length"][4] = 1  # NAR 3 ends short
+    with pytest.raises(AssertionError, match="NAR 3"):
+        check_gathered_batch(bad, first, sizes)
+    with pytest.raises(AssertionError, match="NAR 1"):  # an empty NAR given a chunk
+        check_gathered_batch(d, np.array([0, 1, 2, 3, 5], np.uint64), sizes)
+    with pytest.raises(AssertionError, match="ends at"):
+        check_gathered_batch(d, np.array([0, 2, 2, 3, 4], np.uint64), sizes)
+    bad = d.copy()
+    bad["offset"][2] = 1  # NAR 2 does not start at 0
+    with pytest.raises(AssertionError, match="NAR 2"):
+        check_gathered_batch(bad, first, sizes)
