@@ -68,6 +68,7 @@ def parse_args():
     ap.add_argument("--no-concurrent", action="store_true", help="skip the K-batches-in-flight measurement")
     ap.add_argument("--concurrent", default="8,32", help="K values of the in-flight measurement")
     ap.add_argument("--concurrent-only", action="store_true", help="only the in-flight measurement (profiling)")
+    ap.add_argument("--e2e", default="1,8", help="K values of the host-to-host in-flight measurement ('' = skip)")
     ap.add_argument("--hw-queues", type=int, default=16, choices=range(0, 33), metavar="0..32",
                     help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -227,6 +228,8 @@ def main():
         del d_out, d_data
         torch.cuda.empty_cache()
         conc = concurrent_rates(ca, torch, args, n_per, nar_bytes, params, algo)
+        if args.e2e:
+            conc["e2e"] = e2e_rates(ca, torch, args, n_per, nar_bytes, params, algo, descs)
 
     if rank == 0:
         gear = "placeholder" if ca.lib.cg_gear_is_placeholder() else (
@@ -313,6 +316,64 @@ def concurrent_rates(ca, torch, args, n_per, nar_bytes, params, algo):
             if errs:
                 raise RuntimeError(errs[0])
         res[f"K{K}"] = round(K * reps * batch_bytes / dt / GIB, 3)
+    return res
+
+
+def e2e_rates(ca, torch, args, n_per, nar_bytes, params, algo, want):
+    """NAR bytes start and end in host memory (north_star: a file or socket): K host
+    threads, each with its own pinned host batch and host descriptor array, call the
+    host entry cg_chunk_batch `reps` times -- H2D copy, chunk + digest, descriptors D2H
+    -- so one batch's copies overlap the other batches' kernels.  Aggregate GiB/s =
+    K x reps x batch bytes / wall time, after one untimed round; every call's
+    descriptors must equal the device-resident run's (`want`, same NARs)."""
+    import ctypes
+
+    from chunker_amd.nar import synth_nars
+
+    ks = sorted({int(k) for k in args.e2e.split(",") if k})
+    host0, offs = synth_nars(np.full(n_per, nar_bytes, np.uint64), zeros=args.zeros, first_index=0)
+    nbytes = int(offs[-1])
+    cap = ca.chunking.batch_capacity(offs, params[0])
+    bufs = []
+    for _ in range(max(ks)):
+        t = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+        t.numpy()[:] = host0
+        bufs.append((t, np.zeros(cap, ca.DESC_DTYPE), np.zeros(n_per + 1, np.uint64)))
+    del host0
+    res = {"unit": "GiB/s", "batch": f"{n_per}x{nar_bytes >> 20}MiB", "reps": 2, "host_buffers": "pinned",
+           "entry": "cg_chunk_batch (H2D + chunk + digest + descriptors D2H)"}
+    for K in ks:
+        for timed in (False, True):
+            reps = res["reps"] if timed else 1
+            bar = threading.Barrier(K + 1)
+            errs = []
+
+            def work(k):
+                t, out, first = bufs[k]
+                bar.wait()
+                for _ in range(reps):
+                    st = ca.lib.cg_chunk_batch(ctypes.c_void_p(t.data_ptr()), offs.ctypes.data, n_per, *params,
+                                               algo, out.ctypes.data, cap, first.ctypes.data)
+                    if st:
+                        errs.append(f"status {st}: {ca._lib.last_error()}")
+                        return
+
+            th = [threading.Thread(target=work, args=(k,)) for k in range(K)]
+            for x in th:
+                x.start()
+            bar.wait()
+            t0 = time.perf_counter()
+            for x in th:
+                x.join()
+            dt = time.perf_counter() - t0
+            if errs:
+                raise RuntimeError(errs[0])
+        for k in range(K):
+            _, out, first = bufs[k]
+            n = int(first[-1])
+            assert n == len(want) and np.array_equal(out[:n].view(np.uint8), want.view(np.uint8)), \
+                f"e2e batch {k}: descriptors differ from the device-resident run"
+        res[f"K{K}"] = round(K * reps * nbytes / dt / GIB, 3)
     return res
 
 

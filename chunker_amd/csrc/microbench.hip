@@ -156,8 +156,9 @@ extern uint32_t g_b3_diag;
 // 1 = BLAKE3 leaves compress register words without loading them (digests garbage)
 extern "C" void cg_diag_b3_mode(uint32_t mode) { cg::g_b3_diag = mode; }
 // Enable (n_wg > 0) / read back / disable (n_wg == 0) per-workgroup SHA producer and
-// consumer timing: out[4*wg + {0,1,2,3}] = producer spin, producer total, consumer
-// spin, consumer total (shader clocks).  Diagnostics only.
+// consumer timing: out[8*wg + {0,1,2,3}] = producer spin, producer total, consumer
+// spin, consumer total (shader clocks); + {4,5} consumer start/end (s_memrealtime,
+// 100 MHz), {6,7} consumer/producer wave location (HW_ID | XCC_ID << 32).  Diagnostics only.
 extern "C" int cg_diag_sha_stats(uint32_t n_wg, unsigned long long *out) {
     static unsigned long long *buf = nullptr;
     static uint32_t cap = 0;
@@ -168,15 +169,15 @@ extern "C" int cg_diag_sha_stats(uint32_t n_wg, unsigned long long *out) {
     if (out == nullptr) {  // arm
         if (n_wg > cap) {
             if (buf) (void)hipFree(buf);
-            if (hipMalloc(&buf, (size_t)n_wg * 32) != hipSuccess) return 2;
+            if (hipMalloc(&buf, (size_t)n_wg * 64) != hipSuccess) return 2;
             cap = n_wg;
         }
-        (void)hipMemset(buf, 0, (size_t)n_wg * 32);
+        (void)hipMemset(buf, 0, (size_t)n_wg * 64);
         cg::g_sha_diag = buf;
         return 0;
     }
     (void)hipDeviceSynchronize();
-    return hipMemcpy(out, buf, (size_t)n_wg * 32, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 2;
+    return hipMemcpy(out, buf, (size_t)n_wg * 64, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 2;
 }
 
 // ---------------------------------------------------------------------------

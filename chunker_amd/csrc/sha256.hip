@@ -588,11 +588,31 @@ __device__ void split_consumer(uint32_t (*sW)[64 * PC_ROW], uint32_t row, bool h
     }
 }
 
+// Hardware location of the calling wave (diagnostics): HW_ID | XCC_ID << 32.
+__device__ __forceinline__ unsigned long long wave_location() {
+    uint32_t hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    return ((unsigned long long)xcc << 32) | hw;
+}
+
+__device__ __forceinline__ void sha_diag_consumer(unsigned long long *diag, unsigned long long t_spin,
+                                                  unsigned long long t_start, unsigned long long rt_start) {
+    diag[8 * blockIdx.x + 2] = t_spin;
+    diag[8 * blockIdx.x + 3] = __builtin_amdgcn_s_memtime() - t_start;
+    diag[8 * blockIdx.x + 4] = rt_start;
+    diag[8 * blockIdx.x + 5] = __builtin_amdgcn_s_memrealtime();
+    diag[8 * blockIdx.x + 6] = wave_location();
+}
+
 // Workgroup kinds, longest chunks first (the length order): [0, nquad) take 8 chunks
 // on 8 lanes each, [nquad, nquad + npair) 32 chunks on lane pairs, the rest 64
 // chunks on one lane each.  The quad and pair kinds share the pair producer.
-// diag (optional, nullptr in production): per workgroup {producer spin, producer
-// total, consumer spin, consumer total} in shader clocks (s_memtime).
+// diag (optional, nullptr in production, diagnostics build only): per workgroup
+// {producer spin, producer total, consumer spin, consumer total} in shader clocks
+// (s_memtime), then the consumer's start and end on the 100 MHz global clock
+// (s_memrealtime) and where the consumer and the producer wave ran
+// (HW_ID | XCC_ID << 32: SIMD, CU, shader array, SE, XCD).
 __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data, const uint64_t *__restrict__ abs,
                                                const DescRaw *__restrict__ desc, const uint64_t *__restrict__ total_p,
                                                uint64_t max_chunks, const uint32_t *__restrict__ order,
@@ -601,6 +621,7 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
                                                uint32_t nquad, uint32_t npair, uint32_t spin_limit,
                                                uint32_t *__restrict__ err) {
     unsigned long long t_start = diag ? __builtin_amdgcn_s_memtime() : 0ull, t_spin = 0;
+    const unsigned long long rt_start = diag ? __builtin_amdgcn_s_memrealtime() : 0ull;
     __shared__ __attribute__((aligned(16))) uint32_t sW[PC_RING][64 * PC_ROW];
     // hand-off words (SY_*): blocks filled by the producer / consumed by the consumer,
     // the spin guard's timeout flag and limit
@@ -655,8 +676,9 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
             t_spin = sha_produce(p, len, nbt, NB, sW, row, lane, &s_ready, &s_done, diag != nullptr);
         }
         if (diag && lane == 0) {
-            diag[4 * blockIdx.x + 0] = t_spin;
-            diag[4 * blockIdx.x + 1] = __builtin_amdgcn_s_memtime() - t_start;
+            diag[8 * blockIdx.x + 0] = t_spin;
+            diag[8 * blockIdx.x + 1] = __builtin_amdgcn_s_memtime() - t_start;
+            diag[8 * blockIdx.x + 7] = wave_location();
         }
     } else if (split) {
         uint32_t st[4];
@@ -664,10 +686,7 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
             split_consumer<true>(sW, row, hi, lane, NB, nbt, &s_ready, &s_done, st, &t_spin, diag != nullptr);
         else
             split_consumer<false>(sW, row, hi, lane, NB, nbt, &s_ready, &s_done, st, &t_spin, diag != nullptr);
-        if (diag && lane == 0) {
-            diag[4 * blockIdx.x + 2] = t_spin;
-            diag[4 * blockIdx.x + 3] = __builtin_amdgcn_s_memtime() - t_start;
-        }
+        if (diag && lane == 0) sha_diag_consumer(diag, t_spin, t_start, rt_start);
         if (valid && (!quad || (lane & 3u) == 0)) {  // hi: H0..H3 (bytes 0-15), lo: H4..H7 (bytes 16-31)
             uint4 *o = reinterpret_cast<uint4 *>(hash_base + ci * stride + (hi ? 0 : 16));
             *o = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]), __builtin_bswap32(st[2]),
@@ -694,10 +713,7 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
             __builtin_amdgcn_s_waitcnt(0xc07f);
             if (lane == 0) lds_store_release(&s_done, k + 2);
         }
-        if (diag && lane == 0) {
-            diag[4 * blockIdx.x + 2] = t_spin;
-            diag[4 * blockIdx.x + 3] = __builtin_amdgcn_s_memtime() - t_start;
-        }
+        if (diag && lane == 0) sha_diag_consumer(diag, t_spin, t_start, rt_start);
         if (valid) {
             uint4 *o = reinterpret_cast<uint4 *>(hash_base + ci * stride);
             o[0] = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]), __builtin_bswap32(st[2]),

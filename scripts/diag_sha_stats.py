@@ -38,11 +38,11 @@ for name, n, size, params, mode in runs:
     first = ca.chunk_batch_device(d.data_ptr(), offs, out.data_ptr(), cap, *params)
     st = (ctypes.c_double * 5)()
     ca.lib.cg_last_stage_times(st, 5)
-    buf = np.zeros(4 * nwg, np.uint64)
+    buf = np.zeros(8 * nwg, np.uint64)
     lib.cg_diag_sha_stats(nwg, buf.ctypes.data)
     lib.cg_diag_sha_stats(0, None)
     used = int((int(first[-1]) + 63) // 64)
-    b = buf.reshape(-1, 4)[:used].astype(float)
+    b = buf.reshape(-1, 8)[:used, :4].astype(float)
     worst = int(np.argmax(b[:, 3]))
     lens = np.frombuffer(out.cpu().numpy().tobytes()[:48 * int(first[-1])], dtype=np.uint64).reshape(-1, 6)[:, 1]
     max_blocks = int(lens.max()) // 64 + 1

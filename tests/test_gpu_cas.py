@@ -9,6 +9,8 @@ every ObjectKind, the reference's own CAS and Node tests
 (crates/core/cas/src/lib.rs:254-310, crates/node/src/lib.rs:214-280), empty and
 ragged NAR batches, and enough spans to engage the longest-first order.
 """
+import contextlib
+
 import numpy as np
 import pytest
 
@@ -58,12 +60,18 @@ def test_shake_kat_and_reference_cas_cases(cas, O):
     assert a == b and a != c and len(a.to_hex()) == 64
 
 
+@contextlib.contextmanager
 def _pair_max(v):
-    """Cap the CAS pair tier (test hook cg_test_cas_pair_max): -1 = wave budget only, 0 =
-    one lane per span everywhere, k = the k longest spans on lane pairs; returns the old cap."""
+    """Cap the CAS pair tier (test hook cg_test_cas_pair_max) for the block: -1 = wave
+    budget only, 0 = one lane per span everywhere, k = the k longest spans on lane pairs.
+    The old cap comes back even when the block fails, so no tier leaks into later tests."""
     from chunker_amd import lib
 
-    return lib.cg_test_cas_pair_max(v)
+    old = lib.cg_test_cas_pair_max(v)
+    try:
+        yield
+    finally:
+        lib.cg_test_cas_pair_max(old)
 
 
 TIERS = pytest.mark.parametrize("pair_max", [-1, 0, 37], ids=["pairs", "single", "mixed"])
@@ -72,8 +80,6 @@ TIERS = pytest.mark.parametrize("pair_max", [-1, 0, 37], ids=["pairs", "single",
 @TIERS
 def test_cas_ids_all_lengths_and_alignments(cas, O, pair_max):
     import torch
-
-    old = _pair_max(pair_max)
 
     rng = np.random.default_rng(17)
     data = rng.integers(0, 256, 4 << 20, dtype=np.uint8)
@@ -85,11 +91,11 @@ def test_cas_ids_all_lengths_and_alignments(cas, O, pair_max):
     ln = torch.tensor(lens, dtype=torch.int64).cuda()
     for kind in (cas.ObjectKind.Chunk, cas.ObjectKind.Commit):
         ids = torch.zeros(len(lens) * 32, dtype=torch.uint8, device="cuda")
-        cas.content_ids_device(d.data_ptr(), o.data_ptr(), ln.data_ptr(), len(lens), kind, ids.data_ptr())
+        with _pair_max(pair_max):
+            cas.content_ids_device(d.data_ptr(), o.data_ptr(), ln.data_ptr(), len(lens), kind, ids.data_ptr())
         ids = ids.cpu().numpy().reshape(-1, 32)
         for k, (a, n) in enumerate(zip(offs, lens)):
             assert bytes(ids[k]) == O.content_id(int(kind), data[a:a + n]), (int(kind), n, a)
-    _pair_max(old)
 
 
 def test_node_put_matches_oracle(cas, O):
@@ -154,8 +160,6 @@ def test_cas_many_spans_ordered(cas, O, pair_max):
     """> 64 spans of mixed lengths: the longest-first order path."""
     import torch
 
-    old = _pair_max(pair_max)
-
     rng = np.random.default_rng(23)
     data = rng.integers(0, 256, 8 << 20, dtype=np.uint8)
     lens = rng.integers(0, 200_000, 700).tolist() + [2 << 20, 1 << 20]
@@ -164,11 +168,12 @@ def test_cas_many_spans_ordered(cas, O, pair_max):
     o = torch.tensor(offs, dtype=torch.int64).cuda()
     ln = torch.tensor(lens, dtype=torch.int64).cuda()
     ids = torch.zeros(len(lens) * 32, dtype=torch.uint8, device="cuda")
-    cas.content_ids_device(d.data_ptr(), o.data_ptr(), ln.data_ptr(), len(lens), cas.ObjectKind.Chunk, ids.data_ptr())
+    with _pair_max(pair_max):
+        cas.content_ids_device(d.data_ptr(), o.data_ptr(), ln.data_ptr(), len(lens), cas.ObjectKind.Chunk,
+                               ids.data_ptr())
     ids = ids.cpu().numpy().reshape(-1, 32)
     want = O.content_ids(data, np.array(list(zip(offs, lens)), dtype=[("offset", "<u8"), ("length", "<u8")]),
                          O.KIND_CHUNK, nthreads=8)
-    _pair_max(old)
     assert [bytes(x) for x in ids] == want
 
 

@@ -100,3 +100,24 @@ def test_config5_shard_16x1gib(ca, O):
     assert 16 * 600 < n < 16 * 1100  # ~820 chunks per GiB at D on random data
     for i in (0, 7, 15):
         oracle_check(O, d, offs, first, descs, i, D, 1)
+
+
+def test_config4_full_16x1gib(ca, O):
+    """BASELINE config 4 at full size (16 x 1 GiB at S, SHA-256, the bench's NARs): the
+    only shape whose expected chunk count (~54 K) fills the GPU, so the digest runs the
+    GPU-filling tier mix (a few quad workgroups for the longest chunks, then pairs, then
+    one-lane workgroups, cg_last_sha_tiers).  Every NAR covered contiguously; NARs 0, 7
+    and 15 oracle-checked chunk by chunk."""
+    import ctypes
+
+    sizes = [GIB] * 16
+    d, offs, first, descs = run_device_batch(ca, sizes, S, 1, 0)
+    tiers = (ctypes.c_uint32 * 4)()
+    assert ca.lib.cg_last_sha_tiers(tiers) == 1
+    nquad, npair, nlane, _ = (int(t) for t in tiers)
+    assert 0 < nquad < 256 and npair > 0 and nlane > 0, list(tiers)
+    check_cover(descs, first, offs, S)
+    n = int(first[-1])
+    assert 16 * 2600 < n < 16 * 4000  # ~3.3 K chunks per GiB at S on random data (SURVEY.md App. B)
+    for i in (0, 7, 15):
+        oracle_check(O, d, offs, first, descs, i, S, 1)
