@@ -16,7 +16,12 @@ chunk_descriptors[_with_hash]          :299-374
 ChunkStream                            :382-740 (read-slice sizing :713-716, env cap :427-433),
                                        pipelined on the GPU (cg_stream_*)
 PushChunker                            :742-829
+ChunkStreamAsync (asyncio)             :835-1017 (feature async-stream), same handle
+chunk_data_async / chunk_stream_async  :1049-1130 (buffer limit :420-445)
+BlockingAsyncReadAdapter,              :1019-1047, :1090-1113
+  chunk_stream_blocking_adapter
 chunk_stream / chunk_stream_with_hash  :1132-1166
+metrics (StreamMetrics)                :398-416 (recorded by the streaming paths only)
 =====================================  ======================================================
 
 Plus batch entry points the reference has no equivalent for (many NARs per call,
@@ -48,6 +53,10 @@ MAXIMUM_MIN, MAXIMUM_MAX = 1024, 16_777_216
 DEFAULT_READ_SLICE_CAP = 8 * 1024 * 1024
 MAX_READ_SLICE_CAP = 256 * 1024 * 1024
 MIN_READ_SLICE_CAP = 4096
+# ChunkStreamAsync collection cap (src/chunking.rs:420-425)
+DEFAULT_ASYNC_BUFFER_LIMIT = 2 * 1024 * 1024 * 1024
+MAX_ASYNC_BUFFER_LIMIT = 3 * 1024 * 1024 * 1024
+MIN_ASYNC_BUFFER_LIMIT = 64 * 1024 * 1024
 
 
 # ---------------------------------------------------------------------------
@@ -377,6 +386,8 @@ class PushChunker:
     def _collect(self, arr: np.ndarray) -> list[ChunkMetadata]:
         out = [ChunkMetadata(bytes(d["hash"]), int(d["offset"]), int(d["length"]),
                              self._payload(int(d["offset"]), int(d["length"]))) for d in arr]
+        for c in out:  # drain_finalized_chunks records per emitted chunk (:613-616, :655-658)
+            metrics.record(c.length)
         if len(arr):
             end = int(arr[-1]["offset"] + arr[-1]["length"])
             self._segs = [(st, mv) for st, mv in self._segs if st + len(mv) > end]
@@ -448,14 +459,150 @@ def stream_inflight_bytes() -> int:
     return DEFAULT_STREAM_INFLIGHT
 
 
-class ChunkStream:
+class StreamMetrics:
+    """The reference's streaming metrics (src/chunking.rs:398-416): counters
+    `chunker.chunks_emitted` and `chunker.bytes_processed` and histogram
+    `chunker.chunk_size`, recorded per chunk handed out by the streaming paths --
+    PushChunker / ChunkStream (:613-616, :655-658) and ChunkStreamAsync (:926-929,
+    :962-965) -- and not by chunk_data, as in the reference.  The histogram keeps count,
+    sum, min and max.  `snapshot()` returns them by the reference's metric names."""
+
+    def __init__(self):
+        import threading
+
+        self._mu = threading.Lock()
+        self.reset()
+
+    def reset(self) -> None:
+        self.chunks_emitted = 0
+        self.bytes_processed = 0
+        self._hist = [0, 0, None, None]  # count, sum, min, max
+
+    def record(self, length: int) -> None:
+        with self._mu:
+            self.chunks_emitted += 1
+            self.bytes_processed += length
+            h = self._hist
+            h[0] += 1
+            h[1] += length
+            h[2] = length if h[2] is None else min(h[2], length)
+            h[3] = length if h[3] is None else max(h[3], length)
+
+    def snapshot(self) -> dict:
+        with self._mu:
+            c, sm, lo, hi = self._hist
+            return {"chunker.chunks_emitted": self.chunks_emitted, "chunker.bytes_processed": self.bytes_processed,
+                    "chunker.chunk_size": {"count": c, "sum": sm, "min": lo, "max": hi}}
+
+
+metrics = StreamMetrics()
+
+
+class _StreamCore:
+    """What ChunkStream and ChunkStreamAsync share: the engine's pipelined stream handle
+    (cg_stream_*), the read slices kept for payloads, and the failure rule -- the first
+    engine error poisons the handle (the C side repeats it on every later call) and the
+    stream ends, so no chunk after a lost slice is ever handed out.
+
+    Payloads are read-only memoryviews (the reference's `Bytes`): a view into the slice
+    the chunk was read in, or, for a chunk spanning slices, into one joined copy.  A view
+    keeps its slice alive (at most one read size); bytes(payload) makes an owned copy."""
+
+    def _open(self, read_size: int) -> None:
+        st = ctypes.c_int(0)
+        o = self.options
+        self._h = lib.cg_stream_new(o.min_size, o.avg_size, o.max_size, int(self.hash), read_size,
+                                    stream_inflight_bytes(), ctypes.byref(st))
+        if not self._h:
+            _raise(st.value)
+        self._segs: deque = deque()  # (stream offset, read-only memoryview) not yet fully emitted
+        self._pushed = 0
+        self._pending: deque = deque()
+        self._eof = False
+        self._done = False
+        self._out = np.zeros(4096, DESC_DTYPE)
+
+    def _engine(self, status: int) -> None:
+        """_check for engine calls: on failure the stream is over (handle freed)."""
+        if status != _lib.CG_OK:
+            try:
+                _raise(status)
+            finally:
+                self._done = True
+                self._release()
+
+    def _take(self, wait: bool) -> int:
+        n = ctypes.c_size_t(0)
+        self._engine(lib.cg_stream_take(self._h, self._out.ctypes.data, len(self._out), ctypes.byref(n), int(wait)))
+        for d in self._out[: n.value]:
+            off, ln = int(d["offset"]), int(d["length"])
+            self._pending.append(ChunkMetadata(bytes(d["hash"]), off, ln, self._payload(off, ln)))
+        if n.value:  # drop slices wholly before the last emitted byte
+            end = self._pending[-1].offset + self._pending[-1].length
+            while self._segs and self._segs[0][0] + len(self._segs[0][1]) <= end:
+                self._segs.popleft()
+        return n.value
+
+    def _push(self, buf) -> None:
+        a = _as_u8(buf)
+        self._engine(lib.cg_stream_push(self._h, _ptr(a), len(a)))
+        # payloads are views of what was read: keep immutable buffers as they are
+        # (bytes, read-only views), copy anything the reader might reuse
+        keep = buf if isinstance(buf, bytes) or (isinstance(buf, memoryview) and buf.readonly) else a.tobytes()
+        mv = memoryview(keep).cast("B")
+        self._segs.append((self._pushed, mv.toreadonly()))
+        self._pushed += len(mv)
+
+    def _finish(self) -> None:
+        self._engine(lib.cg_stream_finish(self._h))
+        self._eof = True
+
+    def _drained(self) -> bool:
+        """At EOF: nothing left in the engine -> the stream is done (handle freed now,
+        not at garbage collection)."""
+        if lib.cg_stream_pending(self._h) == 0:
+            self._done = True
+            self._release()
+            return True
+        return False
+
+    def _payload(self, off: int, ln: int) -> memoryview:
+        parts = []
+        for start, mv in self._segs:
+            if start >= off + ln:
+                break
+            lo, hi = max(off, start), min(off + ln, start + len(mv))
+            if lo < hi:
+                parts.append(mv[lo - start:hi - start])
+        # one slice: a zero-copy view of the bytes read (the reference's Bytes::split_to,
+        # src/chunking.rs:592); a chunk spanning slices is joined once
+        return parts[0] if len(parts) == 1 else memoryview(b"".join(parts))
+
+    def _emit(self) -> ChunkMetadata:
+        c = self._pending.popleft()
+        metrics.record(c.length)
+        return c
+
+    def bytes_consumed(self) -> int:
+        return self._pushed
+
+    def _release(self) -> None:
+        h = getattr(self, "_h", None)
+        if h:
+            lib.cg_stream_free(h)
+            self._h = None
+
+
+class ChunkStream(_StreamCore):
     """ChunkStream (src/chunking.rs:382-740): pull chunks from a binary reader.
 
     Reads slices of the reference's size (stream_read_size) and pushes them into the
     engine's pipelined stream handle (cg_stream_*): cut points are found per slice, the
     digests of many slices run concurrently on the GPU, and chunks come back strictly in
     stream order with the reference's (offset, length, hash).  One slice is read ahead
-    on a helper thread while the engine works (the ctypes calls release the GIL)."""
+    on a helper thread while the engine works (the ctypes calls release the GIL).  A
+    reader error raises IoError and the next call reads again (as the reference's
+    ChunkStream::next does); an engine error ends the stream."""
 
     def __init__(self, reader: BinaryIO, min_size=None, avg_size=None, max_size=None,
                  hash: HashAlgorithm = HashAlgorithm.Sha256):
@@ -463,20 +610,9 @@ class ChunkStream:
         self.options = ChunkingOptions.resolve(min_size, avg_size, max_size)
         self.hash = HashAlgorithm(hash)
         self._slice = stream_read_size(self.options.max_size)
-        st = ctypes.c_int(0)
-        o = self.options
-        self._h = lib.cg_stream_new(o.min_size, o.avg_size, o.max_size, int(self.hash), self._slice,
-                                    stream_inflight_bytes(), ctypes.byref(st))
-        if not self._h:
-            _raise(st.value)
-        self._segs: deque = deque()  # (stream offset, bytes) not yet fully emitted
-        self._pushed = 0
-        self._pending: deque = deque()
-        self._eof = False
-        self._done = False
-        self._out = np.zeros(4096, DESC_DTYPE)
         self._pool = None
         self._next = None
+        self._open(self._slice)
 
     @classmethod
     def new_with_hash(cls, reader, min_size, avg_size, max_size, hash):
@@ -494,29 +630,12 @@ class ChunkStream:
             self._pool.shutdown(wait=True)
             self._pool = None
 
-    def _take(self, wait: bool) -> int:
-        n = ctypes.c_size_t(0)
-        _check(lib.cg_stream_take(self._h, self._out.ctypes.data, len(self._out), ctypes.byref(n), int(wait)))
-        for d in self._out[: n.value]:
-            off, ln = int(d["offset"]), int(d["length"])
-            self._pending.append(ChunkMetadata(bytes(d["hash"]), off, ln, self._payload(off, ln)))
-        if n.value:  # drop slices wholly before the last emitted byte
-            end = self._pending[-1].offset + self._pending[-1].length
-            while self._segs and self._segs[0][0] + len(self._segs[0][1]) <= end:
-                self._segs.popleft()
-        return n.value
-
-    def _payload(self, off: int, ln: int) -> bytes:
-        parts = []
-        for start, mv in self._segs:
-            if start >= off + ln:
-                break
-            lo, hi = max(off, start), min(off + ln, start + len(mv))
-            if lo < hi:
-                parts.append(mv[lo - start:hi - start])
-        # one slice: a zero-copy view of the bytes read (the reference's Bytes::split_to,
-        # src/chunking.rs:592); a chunk spanning slices is joined once
-        return parts[0] if len(parts) == 1 else b"".join(parts)
+    def _release(self) -> None:
+        super()._release()
+        pool = getattr(self, "_pool", None)
+        if pool is not None:
+            pool.shutdown(wait=False)
+            self._pool = None
 
     def __iter__(self) -> Iterator[ChunkMetadata]:
         return self
@@ -524,12 +643,12 @@ class ChunkStream:
     def __next__(self) -> ChunkMetadata:
         while True:
             if self._pending:
-                return self._pending.popleft()
+                return self._emit()
             if self._done:
                 raise StopIteration
             if self._eof:
-                if self._take(True) == 0 and lib.cg_stream_pending(self._h) == 0:
-                    self._done = True
+                if self._take(True) == 0:
+                    self._drained()
                 continue
             if self._take(False):
                 continue
@@ -545,29 +664,143 @@ class ChunkStream:
             if not buf:
                 self._next = None
                 self._close_pool()
-                _check(lib.cg_stream_finish(self._h))
-                self._eof = True
+                self._finish()
                 continue
             self._read_async()
-            a = _as_u8(buf)
-            _check(lib.cg_stream_push(self._h, _ptr(a), len(a)))
-            # payloads are views of what was read: keep immutable buffers as they are
-            # (bytes, read-only views), copy anything the reader might reuse
-            keep = buf if isinstance(buf, bytes) or (isinstance(buf, memoryview) and buf.readonly) else a.tobytes()
-            self._segs.append((self._pushed, memoryview(keep)))
-            self._pushed += len(keep)
-
-    def bytes_consumed(self) -> int:
-        return int(lib.cg_stream_bytes_consumed(self._h))
+            self._push(buf)
 
     def __del__(self):
-        pool = getattr(self, "_pool", None)
-        if pool is not None:
-            pool.shutdown(wait=False)
-        h = getattr(self, "_h", None)
-        if h:
-            lib.cg_stream_free(h)
-            self._h = None
+        self._release()
+
+
+def effective_async_buffer_limit() -> int:
+    """src/chunking.rs:435-445: CHUNKER_ASYNC_BUFFER_LIMIT_BYTES (default 2 GiB), clamped
+    to 64 MiB..3 GiB."""
+    v = DEFAULT_ASYNC_BUFFER_LIMIT
+    try:
+        v = int(os.environ.get("CHUNKER_ASYNC_BUFFER_LIMIT_BYTES", ""))
+    except ValueError:
+        pass
+    return min(max(v, MIN_ASYNC_BUFFER_LIMIT), MAX_ASYNC_BUFFER_LIMIT)
+
+
+class ChunkStreamAsync(_StreamCore):
+    """ChunkStreamAsync (src/chunking.rs:835-1017, feature `async-stream`) for asyncio:
+
+        async for chunk in ChunkStreamAsync(reader, min_size, avg_size, max_size): ...
+
+    `reader` is any object with a coroutine `read(n)` (asyncio.StreamReader, an async
+    file).  It reads max(min(max_size, CHUNKER_READ_SLICE_CAP_BYTES), 4096) bytes per
+    refill (:981-986) and yields the chunks the reference's try_stream! yields -- its
+    rule of emitting the buffer's first FastCDC chunk when `len != buffer.len() || eof ||
+    len >= max_size` (:923) gives exactly the eager chunk sequence, which is what the
+    engine's stream handle produces (retain rule :579-584 + EOF remainder).  The
+    reference digests each chunk inline (:931); here the slices' digests run on the GPU
+    while the event loop keeps reading: engine calls (which wait for the device) run on
+    one helper thread per stream, in call order, off the loop.  Metrics are recorded per
+    chunk as at :926-929 / :962-965.  As in try_stream!, the first error (reader or
+    engine) is raised once and ends the stream."""
+
+    def __init__(self, reader, min_size=None, avg_size=None, max_size=None,
+                 hash: HashAlgorithm = HashAlgorithm.Sha256):
+        self._reader = reader
+        self.options = ChunkingOptions.resolve(min_size, avg_size, max_size)
+        self.hash = HashAlgorithm(hash)
+        self._read_size = max(min(self.options.max_size, effective_read_slice_cap()), MIN_READ_SLICE_CAP)
+        self._exec = None
+        self._open(self._read_size)
+
+    @classmethod
+    def new_with_hash(cls, reader, min_size, avg_size, max_size, hash):
+        return cls(reader, min_size, avg_size, max_size, hash)
+
+    async def _call(self, fn, *args):
+        import asyncio
+        from concurrent.futures import ThreadPoolExecutor
+
+        if self._exec is None:
+            self._exec = ThreadPoolExecutor(1, thread_name_prefix="chunk-stream-async")
+        return await asyncio.get_running_loop().run_in_executor(self._exec, fn, *args)
+
+    def _release(self) -> None:
+        super()._release()
+        ex = getattr(self, "_exec", None)
+        if ex is not None:
+            ex.shutdown(wait=False)
+            self._exec = None
+
+    def __aiter__(self):
+        return self
+
+    async def __anext__(self) -> ChunkMetadata:
+        while True:
+            if self._pending:
+                return self._emit()
+            if self._done:
+                raise StopAsyncIteration
+            if self._eof:
+                if await self._call(self._take, True) == 0:
+                    self._drained()
+                continue
+            if await self._call(self._take, False):
+                continue
+            try:
+                buf = await self._reader.read(self._read_size)
+            except OSError as e:
+                self._done = True
+                self._release()
+                raise IoError(str(e)) from e
+            if not buf:
+                await self._call(self._finish)
+                continue
+            await self._call(self._push, buf)
+
+    def __del__(self):
+        self._release()
+
+
+async def chunk_data_async(reader, min_size=None, avg_size=None, max_size=None) -> list[ChunkMetadata]:
+    """chunk_data_async (src/chunking.rs:1061-1088): collect a ChunkStreamAsync's chunks,
+    raising BufferLimitExceededError once their total length passes
+    effective_async_buffer_limit()."""
+    limit = effective_async_buffer_limit()
+    chunks, total = [], 0
+    async for c in ChunkStreamAsync(reader, min_size, avg_size, max_size):
+        total += c.length
+        if total > limit:
+            raise BufferLimitExceededError(total, limit)
+        chunks.append(c)
+    return chunks
+
+
+async def chunk_stream_async(reader, min_size=None, avg_size=None, max_size=None) -> list[ChunkMetadata]:
+    """chunk_stream_async (src/chunking.rs:1122-1130) = chunk_data_async."""
+    return await chunk_data_async(reader, min_size, avg_size, max_size)
+
+
+class BlockingAsyncReadAdapter:
+    """BlockingAsyncReadAdapter (src/chunking.rs:1028-1047): a blocking `read(n)` over an
+    async reader -- on `loop` from another thread (run_coroutine_threadsafe), or on a
+    private event loop when none is given.  Blocks the calling thread, as the
+    reference warns."""
+
+    def __init__(self, inner, loop=None):
+        self._inner, self._loop, self._own = inner, loop, None
+
+    def read(self, n: int = -1) -> bytes:
+        import asyncio
+
+        if self._loop is not None:
+            return asyncio.run_coroutine_threadsafe(self._inner.read(n), self._loop).result()
+        if self._own is None:
+            self._own = asyncio.new_event_loop()
+        return self._own.run_until_complete(self._inner.read(n))
+
+
+def chunk_stream_blocking_adapter(reader, min_size=None, avg_size=None, max_size=None,
+                                  loop=None) -> list[ChunkMetadata]:
+    """chunk_stream_blocking_adapter (src/chunking.rs:1104-1113)."""
+    return chunk_stream(BlockingAsyncReadAdapter(reader, loop), min_size, avg_size, max_size)
 
 
 def chunk_stream_with_hash(reader, min_size=None, avg_size=None, max_size=None,

@@ -27,6 +27,7 @@ int fail(int code, const std::string &msg);
 void clear_error();
 int fail_bounds(uint64_t data_len, uint64_t offset, uint64_t length, const std::string &what);
 int fail_limit(uint64_t attempted, const std::string &what);
+int fail_detail(int code, const std::string &msg, const uint64_t detail[3]);  // a failure with given fields
 int hip_fail(hipError_t e, const char *what, uint64_t attempted = 0);
 
 #define HIP_TRY(expr)                                   \

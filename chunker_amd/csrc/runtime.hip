@@ -63,6 +63,12 @@ int fail_limit(uint64_t attempted, const std::string &what) {
     return CG_E_BUFFER_LIMIT;
 }
 
+int fail_detail(int code, const std::string &msg, const uint64_t detail[3]) {
+    fail(code, msg);
+    for (int i = 0; i < 3; ++i) t_detail[i] = detail[i];
+    return code;
+}
+
 static std::atomic<uint32_t> g_fail_alloc{0};  // countdown: the allocation that takes it to 0 fails
 
 bool test_alloc_fault() {

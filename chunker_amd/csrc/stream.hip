@@ -15,6 +15,14 @@
 // (offset, length, hash) the reference's ChunkStream / PushChunker yields.  Memory is
 // bounded by the arena (slots are reused only after every group reading them has
 // completed); when no slot is free a push waits for the oldest group.
+//
+// Device resources are taken as the stream needs them: the arena starts at two slots at
+// the first push and doubles (up to the in-flight budget) only when the pipeline runs
+// out of free slots; digest lanes (stream + event + scratch) are created one at a time
+// when every existing lane is busy.  A short stream therefore holds two slots and one
+// lane, not the whole budget.  The first failure of push / finish / take poisons the
+// handle: every later call returns the same status (a failed push may have left part of
+// its slice inside the engine, so nothing after it could be trusted).
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -50,8 +58,30 @@ struct Lane {
 struct Group {
     std::vector<cg_desc> desc;  // offsets are stream offsets (ChunkMetadata::offset)
     std::vector<uint64_t> abs;  // arena offsets of the same chunks
+    const uint8_t *base = nullptr;  // the arena those offsets are into (it may have been retired since)
     uint64_t slot_lo = 0, slot_hi = 0, bytes = 0;
     int lane = -1;
+};
+
+// The arena: nslots slots of slot_bytes, allocated exactly (no DevBuf slack).
+struct Arena {
+    uint8_t *p = nullptr;
+    uint64_t nslots = 0;
+    int alloc(uint64_t n, uint64_t slot_bytes) {
+        const uint64_t bytes = n * slot_bytes;
+        hipError_t e = test_alloc_fault() ? hipErrorOutOfMemory : hipMalloc(reinterpret_cast<void **>(&p), bytes);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return hip_fail(e, "stream arena", bytes);
+        }
+        nslots = n;
+        return CG_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);  // hipFree waits for the device: no copy or kernel still reads it
+        p = nullptr;
+        nslots = 0;
+    }
 };
 
 }  // namespace cgrt
@@ -63,8 +93,13 @@ struct cg_stream {
     int algo = CG_SHA256;
     int device = -1;
     Workspace *ws = nullptr;  // boundary pipeline, held for the handle's lifetime
-    DevBuf arena;
-    uint64_t slot_bytes = 0, nslots = 0, group_bytes = 0;
+    Arena arena;
+    std::vector<Arena> retired;  // earlier, smaller arenas still read by launched groups
+    uint64_t slot_bytes = 0, max_slots = 0, group_bytes = 0;
+    size_t max_lanes = 0;
+    int poisoned = CG_OK;  // first failure of push / finish / take, returned by every later call
+    std::string poison_msg;
+    uint64_t poison_detail[3] = {0, 0, 0};
     uint64_t cur = 0;       // sequence number of the slot holding the retained tail
     uint64_t tail = 0;      // retained bytes at the start of slot `cur`
     uint64_t position = 0;  // stream offset of slot `cur`'s first byte
@@ -73,7 +108,7 @@ struct cg_stream {
     Group open;
     std::deque<Group> inflight;
     std::deque<cg_desc> ready;
-    std::vector<Lane> lanes;
+    std::vector<Lane> lanes;  // reserved to max_lanes up front: references stay valid as it grows
     std::vector<cg_desc> scratch;  // boundary descriptors of the current slot
     hipEvent_t ev_bytes = nullptr;  // boundary stream position a digest launch must wait for
     ~cg_stream() {
@@ -88,14 +123,29 @@ struct cg_stream {
         }
         if (ev_bytes) (void)hipEventDestroy(ev_bytes);
         arena.release();
+        for (Arena &a : retired) a.release();
         (void)hipSetDevice(prev);
     }
 };
 
 namespace cgrt {
 
-uint8_t *slot_ptr(cg_stream *h, uint64_t seq) { return h->arena.as<uint8_t>() + (seq % h->nslots) * h->slot_bytes; }
-uint64_t slot_off(const cg_stream *h, uint64_t seq) { return (seq % h->nslots) * h->slot_bytes; }
+uint8_t *slot_ptr(cg_stream *h, uint64_t seq) { return h->arena.p + (seq % h->arena.nslots) * h->slot_bytes; }
+uint64_t slot_off(const cg_stream *h, uint64_t seq) { return (seq % h->arena.nslots) * h->slot_bytes; }
+
+// Retired arenas no launched group reads any more are freed.
+void release_retired(cg_stream *h) {
+    for (size_t i = 0; i < h->retired.size();) {
+        bool used = false;
+        for (const Group &g : h->inflight) used = used || g.base == h->retired[i].p;
+        if (used) {
+            ++i;
+        } else {
+            h->retired[i].release();
+            h->retired.erase(h->retired.begin() + i);
+        }
+    }
+}
 
 // Wait for the oldest launched group, check it, and move its chunks (now with digests)
 // to the ready queue.
@@ -116,6 +166,7 @@ int complete_oldest(cg_stream *h) {
         h->ready.push_back(d);
     }
     h->inflight.pop_front();
+    if (!h->retired.empty()) release_retired(h);
     return CG_OK;
 }
 
@@ -128,6 +179,19 @@ int launch_open(cg_stream *h) {
         for (size_t i = 0; i < h->lanes.size(); ++i)
             if (!h->lanes[i].busy) li = (int)i;
         if (li >= 0) break;
+        if (h->lanes.size() < h->max_lanes) {  // every lane busy: open one more
+            h->lanes.emplace_back();
+            if ((rc = h->lanes.back().init())) {
+                h->lanes.back().destroy();
+                h->lanes.pop_back();
+                if (h->lanes.empty()) return rc;
+                h->max_lanes = h->lanes.size();  // the runtime will not give more: wait instead
+                clear_error();
+                continue;
+            }
+            li = (int)h->lanes.size() - 1;
+            break;
+        }
         if ((rc = complete_oldest(h))) return rc;
     }
     Lane &l = h->lanes[li];
@@ -153,7 +217,7 @@ int launch_open(cg_stream *h) {
     HIP_TRY(hipMemcpyAsync(l.total.p, stg + nd + n * 8, 8, hipMemcpyHostToDevice, l.st));
     HIP_TRY(hipMemsetAsync(l.err.p, 0, 4, l.st));
     uint8_t *hb = l.desc.as<uint8_t>() + offsetof(cg_desc, hash);
-    const uint8_t *base = h->arena.as<uint8_t>();
+    const uint8_t *base = g.base;
     const uint64_t *d_total = l.total.as<uint64_t>();
     if (h->algo == CG_SHA256) {
         if ((rc = l.order.ensure(cg::sha256_order_tmp_elems(n) * 4, "order"))) return rc;
@@ -180,15 +244,39 @@ int launch_open(cg_stream *h) {
     return CG_OK;
 }
 
-// Make slot `seq` writable: every group reading its previous tenant (seq - nslots) done.
+// Double the arena (up to the budget) instead of waiting for a slot.  A group never
+// spans two arenas, so the open one is launched on the current arena first; the old
+// arena is kept until the groups reading it (and the pending tail move) are done.  When
+// the device has no memory for the larger arena the budget shrinks to the current size.
+int grow_arena(cg_stream *h) {
+    int rc;
+    if ((rc = launch_open(h))) return rc;
+    Arena nb;
+    if (nb.alloc(std::min(h->arena.nslots * 2, h->max_slots), h->slot_bytes)) {
+        clear_error();
+        h->max_slots = h->arena.nslots;
+        return CG_OK;
+    }
+    h->retired.push_back(h->arena);
+    h->arena = nb;
+    return CG_OK;
+}
+
+// Make slot `seq` writable: every group reading its previous tenant (seq - nslots) in the
+// current arena done (groups launched on a retired arena do not count).
 int free_slot(cg_stream *h, uint64_t seq) {
     int rc;
     for (;;) {
-        const uint64_t oldest = !h->inflight.empty() ? h->inflight.front().slot_lo
-                                : !h->open.desc.empty() ? h->open.slot_lo
-                                                        : h->cur;
-        if (seq < oldest + h->nslots) return CG_OK;
-        if (h->inflight.empty()) {
+        uint64_t oldest = !h->open.desc.empty() ? h->open.slot_lo : h->cur;
+        for (const Group &g : h->inflight)
+            if (g.base == h->arena.p) {
+                oldest = g.slot_lo;
+                break;
+            }
+        if (seq < oldest + h->arena.nslots) return CG_OK;
+        if (h->arena.nslots < h->max_slots) {
+            if ((rc = grow_arena(h))) return rc;
+        } else if (h->inflight.empty()) {
             if ((rc = launch_open(h))) return rc;
         } else if ((rc = complete_oldest(h))) {
             return rc;
@@ -224,7 +312,10 @@ int stream_drain(cg_stream *h, uint64_t len, bool eof) {
         const cg_desc &d = h->scratch[k];
         if (d.length == 0) return fail(CG_E_ZERO_LENGTH_CHUNK, "FastCDC returned a chunk with length 0");
         if (d.offset + d.length == buf && !eof && d.length < h->o.max) break;  // retained tail (:579-584)
-        if (h->open.desc.empty()) h->open.slot_lo = h->cur;
+        if (h->open.desc.empty()) {
+            h->open.slot_lo = h->cur;
+            h->open.base = h->arena.p;
+        }
         h->open.slot_hi = h->cur;
         cg_desc c{};
         c.offset = h->position + d.offset;
@@ -237,10 +328,10 @@ int stream_drain(cg_stream *h, uint64_t len, bool eof) {
     if (eof && consumed < buf) return fail(CG_E_IO, "stream: chunks do not cover the buffer at finish");
     const uint64_t rest = buf - consumed;
     if (consumed) {  // the chunks emitted from this slot stay put; the next slice goes to the next slot
+        const uint8_t *src = slot_ptr(h, h->cur) + consumed;  // (free_slot may move on to a larger arena)
         if ((rc = free_slot(h, h->cur + 1))) return rc;
         if (rest)  // the retained tail moves to the front of that slot
-            HIP_TRY(hipMemcpyAsync(slot_ptr(h, h->cur + 1), slot_ptr(h, h->cur) + consumed, rest,
-                                   hipMemcpyDeviceToDevice, ws->stream));
+            HIP_TRY(hipMemcpyAsync(slot_ptr(h, h->cur + 1), src, rest, hipMemcpyDeviceToDevice, ws->stream));
         h->cur += 1;
     }
     h->position += consumed;
@@ -270,24 +361,24 @@ cg_stream *cg_stream_new(uint64_t min_size, uint64_t avg_size, uint64_t max_size
     h->o = o;
     h->algo = algo;
     h->device = dev;
-    // slot = the largest retained tail (< max) + one slice.  Digest lanes: one per
+    // slot = the largest retained tail (< max) + one slice.  Digest lanes: up to one per
     // hardware queue left beside the workspace stream's (GPU_MAX_HW_QUEUES, HIP's
     // default 4; streams sharing a queue serialise), 3..8; groups of ~1/(lanes + 1) of
-    // the arena, so every lane can hold one while the next fills.
+    // the full arena, so every lane can hold one while the next fills.  The arena and
+    // the lanes themselves are allocated as the stream needs them (see the file header).
     const uint64_t slice = std::max<uint64_t>(slice_bytes ? slice_bytes : 8ull << 20, 4096);
     h->slot_bytes = (o.max + slice + 256 + 255) & ~255ull;
     const uint64_t budget = inflight_bytes ? inflight_bytes : 512ull << 20;
-    h->nslots = std::max<uint64_t>(budget / h->slot_bytes, 4);
+    h->max_slots = std::max<uint64_t>(budget / h->slot_bytes, 4);
     int queues = 4;
     if (const char *q = std::getenv("GPU_MAX_HW_QUEUES")) queues = std::atoi(q) > 0 ? std::atoi(q) : 4;
-    const int nlanes = std::min(std::max(queues - 1, 3), 8);
-    h->group_bytes = std::max<uint64_t>(h->nslots * h->slot_bytes / (uint64_t)(nlanes + 1), slice);
-    if (!(rc = acquire(&h->ws)) && !(rc = h->arena.ensure(h->nslots * h->slot_bytes, "stream arena"))) {
+    h->max_lanes = (size_t)std::min(std::max(queues - 1, 3), 8);
+    h->lanes.reserve(h->max_lanes);
+    h->group_bytes = std::max<uint64_t>(h->max_slots * h->slot_bytes / (uint64_t)(h->max_lanes + 1), slice);
+    if (!(rc = acquire(&h->ws))) {
         const hipError_t e = hipEventCreateWithFlags(&h->ev_bytes, hipEventDisableTiming);
         if (e != hipSuccess) rc = hip_fail(e, "hipEventCreate");
     }
-    h->lanes.resize(nlanes);
-    for (int i = 0; !rc && i < nlanes; ++i) rc = h->lanes[i].init();
     if (rc) {
         delete h;
         if (status) *status = rc;
@@ -297,12 +388,26 @@ cg_stream *cg_stream_new(uint64_t min_size, uint64_t avg_size, uint64_t max_size
     return h;
 }
 
-int cg_stream_push(cg_stream *h, const uint8_t *data, uint64_t len) {
-    clear_error();
-    if (!h) return fail(CG_E_IO, "null stream handle");
-    if (h->finished) return fail(CG_E_INVALID_OPTIONS, "push called after finish");
-    int rc = check_tables();
-    if (rc) return rc;
+namespace {
+
+// The first failure poisons the handle; later calls repeat it (status, message, fields).
+int poison(cg_stream *h, int rc) {
+    if (rc && !h->poisoned) {
+        h->poisoned = rc;
+        h->poison_msg = cg_last_error_message();
+        cg_last_error_detail(h->poison_detail);
+    }
+    return rc;
+}
+
+int check_poisoned(const cg_stream *h) {
+    if (!h->poisoned) return CG_OK;
+    return fail_detail(h->poisoned, "stream failed earlier and cannot continue: " + h->poison_msg, h->poison_detail);
+}
+
+int stream_push(cg_stream *h, const uint8_t *data, uint64_t len) {
+    int rc;
+    if (len && !h->arena.p && (rc = h->arena.alloc(std::min<uint64_t>(2, h->max_slots), h->slot_bytes))) return rc;
     while (len) {  // a slice larger than a slot goes in slot-sized pieces (chunks do not depend on slicing)
         const uint64_t room = h->slot_bytes - 256 - h->tail;
         const uint64_t take = std::min(len, room);
@@ -312,24 +417,19 @@ int cg_stream_push(cg_stream *h, const uint8_t *data, uint64_t len) {
         data += take;
         len -= take;
     }
+    // the caller may reuse `data` as soon as push returns: its copy has completed
+    HIP_TRY(hipStreamSynchronize(h->ws->stream));
     return CG_OK;
 }
 
-int cg_stream_finish(cg_stream *h) {
-    clear_error();
-    if (!h) return fail(CG_E_IO, "null stream handle");
-    if (h->finished) return CG_OK;
-    int rc = check_tables();
-    if (rc) return rc;
+int stream_finish(cg_stream *h) {
     h->finished = true;
-    if ((rc = stream_drain(h, 0, true))) return rc;
+    int rc = stream_drain(h, 0, true);
+    if (rc) return rc;
     return launch_open(h);
 }
 
-int cg_stream_take(cg_stream *h, cg_desc *out, size_t out_cap, size_t *n_out, int wait) {
-    clear_error();
-    if (n_out) *n_out = 0;
-    if (!h) return fail(CG_E_IO, "null stream handle");
+int stream_take(cg_stream *h, cg_desc *out, size_t out_cap, size_t *n_out, int wait) {
     int rc;
     while (h->ready.empty()) {
         if (!h->inflight.empty()) {
@@ -349,6 +449,37 @@ int cg_stream_take(cg_stream *h, cg_desc *out, size_t out_cap, size_t *n_out, in
     }
     if (n_out) *n_out = n;
     return CG_OK;
+}
+
+}  // namespace
+
+int cg_stream_push(cg_stream *h, const uint8_t *data, uint64_t len) {
+    clear_error();
+    if (!h) return fail(CG_E_IO, "null stream handle");
+    int rc = check_poisoned(h);
+    if (rc) return rc;
+    if (h->finished) return fail(CG_E_INVALID_OPTIONS, "push called after finish");
+    if ((rc = check_tables())) return rc;
+    return poison(h, stream_push(h, data, len));
+}
+
+int cg_stream_finish(cg_stream *h) {
+    clear_error();
+    if (!h) return fail(CG_E_IO, "null stream handle");
+    int rc = check_poisoned(h);
+    if (rc) return rc;
+    if (h->finished) return CG_OK;
+    if ((rc = check_tables())) return rc;
+    return poison(h, stream_finish(h));
+}
+
+int cg_stream_take(cg_stream *h, cg_desc *out, size_t out_cap, size_t *n_out, int wait) {
+    clear_error();
+    if (n_out) *n_out = 0;
+    if (!h) return fail(CG_E_IO, "null stream handle");
+    int rc = check_poisoned(h);
+    if (rc) return rc;
+    return poison(h, stream_take(h, out, out_cap, n_out, wait));
 }
 
 uint64_t cg_stream_pending(const cg_stream *h) {

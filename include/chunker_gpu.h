@@ -108,19 +108,26 @@ uint64_t cg_push_bytes_consumed(const cg_push *h); /* PushChunker::bytes_consume
 size_t cg_push_out_capacity(const cg_push *h, uint64_t next_len);
 void cg_push_free(cg_push *h);
 
-/* Pipelined stream: ChunkStream::next (src/chunking.rs:675-740) over
- * drain_finalized_chunks (:541-673) with many read slices in flight.  Each push finds
- * the slice's cut points at once (the reference's retain rule, :579-584), but the
- * chunks' digests run asynchronously, grouped over several slices; cg_stream_take
- * returns finished chunks strictly in stream order (offsets are stream offsets), with
- * exactly the (offset, length, hash) ChunkStream / PushChunker yields.  Device memory
- * is bounded by `inflight_bytes` (0 = 512 MiB): an arena of slots of max_size +
- * slice_bytes (0 = 8 MiB, the reference's read size, :713-716) bytes, each reused only
- * after the digests reading it completed -- a push waits for them when none is free.
- * Digests run on one HIP stream per hardware queue beside the call's own
- * (GPU_MAX_HW_QUEUES - 1, 3..8, read at cg_stream_new).  take with wait = 0 returns what has completed; wait != 0 blocks until at least one
- * chunk is ready or nothing is pending.  push after finish -> CG_E_INVALID_OPTIONS.
- * Single owner, like cg_push. */
+/* Pipelined stream: ChunkStream::next (src/chunking.rs:675-740) and ChunkStreamAsync
+ * (:835-1017) over drain_finalized_chunks (:541-673) with many read slices in flight.
+ * Each push finds the slice's cut points at once (the reference's retain rule,
+ * :579-584), but the chunks' digests run asynchronously, grouped over several slices;
+ * cg_stream_take returns finished chunks strictly in stream order (offsets are stream
+ * offsets), with exactly the (offset, length, hash) ChunkStream / PushChunker /
+ * ChunkStreamAsync yields.  Device memory is bounded by `inflight_bytes` (0 = 512 MiB):
+ * an arena of slots of max_size + slice_bytes (0 = 8 MiB, the reference's read size,
+ * :713-716) bytes, each reused only after the digests reading it completed.  The arena
+ * starts at two slots at the first push and doubles up to that budget only when no slot
+ * is free (a short stream holds two slots); at the budget a push waits for the oldest
+ * digests.  Digests run on up to one HIP stream per hardware queue beside the call's
+ * own (GPU_MAX_HW_QUEUES - 1, 3..8, read at cg_stream_new), created as they are needed.
+ * push returns once its bytes are copied: the caller may reuse `data` right away.  take
+ * with wait = 0 returns what has completed; wait != 0 blocks until at least one chunk is
+ * ready or nothing is pending.  push after finish -> CG_E_INVALID_OPTIONS.  The first
+ * failure of push / finish / take poisons the handle: every later push / finish / take
+ * returns that status again (message prefixed "stream failed earlier", the failure's
+ * cg_last_error_detail fields), since a failed push may have left part of its slice in
+ * the engine.  Single owner, like cg_push. */
 typedef struct cg_stream cg_stream;
 cg_stream *cg_stream_new(uint64_t min_size, uint64_t avg_size, uint64_t max_size, int algo, uint64_t slice_bytes,
                          uint64_t inflight_bytes, int *status);

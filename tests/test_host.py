@@ -1,0 +1,72 @@
+"""Host-side mirror logic that needs no GPU: the async-stream configuration
+(src/chunking.rs:417-445), the streaming metrics (:398-416), and the async adapters'
+plumbing (errors surface before any engine call)."""
+import asyncio
+
+import pytest
+
+import chunker_amd as ca
+from chunker_amd import chunking
+
+
+def test_async_buffer_limit_clamp(monkeypatch):
+    """effective_async_buffer_limit (src/chunking.rs:435-445): default 2 GiB, clamped to
+    64 MiB..3 GiB, unparsable -> default."""
+    monkeypatch.delenv("CHUNKER_ASYNC_BUFFER_LIMIT_BYTES", raising=False)
+    assert chunking.effective_async_buffer_limit() == 2 << 30
+    for v, want in (("1", 64 << 20), (str(100 << 20), 100 << 20), (str(1 << 40), 3 << 30), ("x", 2 << 30)):
+        monkeypatch.setenv("CHUNKER_ASYNC_BUFFER_LIMIT_BYTES", v)
+        assert chunking.effective_async_buffer_limit() == want, v
+
+
+def test_read_sizes(monkeypatch):
+    """ChunkStream reads max(min(max(max*8, 4 MiB), cap), 4096) (:713-716);
+    ChunkStreamAsync max(min(max, cap), 4096) (:982-983); cap from
+    CHUNKER_READ_SLICE_CAP_BYTES in 4 KiB..256 MiB, else 8 MiB (:427-433)."""
+    monkeypatch.delenv("CHUNKER_READ_SLICE_CAP_BYTES", raising=False)
+    assert chunking.stream_read_size(4 << 20) == 8 << 20
+    assert chunking.stream_read_size(1024) == 4 << 20
+    monkeypatch.setenv("CHUNKER_READ_SLICE_CAP_BYTES", "65536")
+    assert chunking.stream_read_size(4 << 20) == 65536
+    monkeypatch.setenv("CHUNKER_READ_SLICE_CAP_BYTES", "100")  # out of range -> default
+    assert chunking.effective_read_slice_cap() == 8 << 20
+
+
+def test_stream_metrics_counters():
+    m = chunking.StreamMetrics()
+    assert m.snapshot()["chunker.chunk_size"]["count"] == 0
+    for n in (5, 1, 9):
+        m.record(n)
+    s = m.snapshot()
+    assert s["chunker.chunks_emitted"] == 3 and s["chunker.bytes_processed"] == 15
+    assert s["chunker.chunk_size"] == {"count": 3, "sum": 15, "min": 1, "max": 9}
+    m.reset()
+    assert m.snapshot()["chunker.chunks_emitted"] == 0
+
+
+def test_async_invalid_options_raise_before_the_engine():
+    """ChunkStreamAsync::new_with_hash resolves the options first (:880): bad sizes raise
+    InvalidOptions with the reference's message, no device needed."""
+    class R:
+        async def read(self, n):
+            return b""
+
+    with pytest.raises(ca.InvalidOptionsError, match="min_size must be in 64..=1048576, got 32"):
+        ca.ChunkStreamAsync(R(), 32, 256, 1024)
+    with pytest.raises(ca.InvalidOptionsError):
+        asyncio.run(ca.chunk_data_async(R(), 1024, 512, 4096))
+
+
+def test_blocking_adapter_reads_through_private_loop():
+    class R:
+        def __init__(self):
+            self.n = 0
+
+        async def read(self, n):
+            await asyncio.sleep(0)
+            self.n += 1
+            return b"ab"[: n]
+
+    r = R()
+    a = chunking.BlockingAsyncReadAdapter(r)
+    assert a.read(1) == b"a" and a.read(5) == b"ab" and r.n == 2
