@@ -68,7 +68,7 @@ def parse_args():
     ap.add_argument("--no-concurrent", action="store_true", help="skip the K-batches-in-flight measurement")
     ap.add_argument("--concurrent", default="8,32", help="K values of the in-flight measurement")
     ap.add_argument("--concurrent-only", action="store_true", help="only the in-flight measurement (profiling)")
-    ap.add_argument("--e2e", default="1,8", help="K values of the host-to-host in-flight measurement ('' = skip)")
+    ap.add_argument("--e2e", default="1,8,16", help="K values of the host-to-host in-flight measurement ('' = skip)")
     ap.add_argument("--hw-queues", type=int, default=16, choices=range(0, 33), metavar="0..32",
                     help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -342,6 +342,16 @@ def e2e_rates(ca, torch, args, n_per, nar_bytes, params, algo, want):
     del host0
     res = {"unit": "GiB/s", "batch": f"{n_per}x{nar_bytes >> 20}MiB", "reps": 2, "host_buffers": "pinned",
            "entry": "cg_chunk_batch (H2D + chunk + digest + descriptors D2H)"}
+    # the host link alone: one pinned batch copied to HBM (the ceiling of every e2e rate)
+    dev = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    dev.copy_(bufs[0][0], non_blocking=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        dev.copy_(bufs[0][0], non_blocking=True)
+    torch.cuda.synchronize()
+    res["h2d_only"] = round(3 * nbytes / (time.perf_counter() - t0) / GIB, 3)
+    del dev
     for K in ks:
         for timed in (False, True):
             reps = res["reps"] if timed else 1
@@ -446,13 +456,13 @@ def cpu_baseline(args, n_per, nar_bytes, params, algo):
     from chunker_amd.nar import synth_nars
     from oracle import oracle as O
 
-    nt = min(os.cpu_count() or 1, 16)
+    nt, affinity, quota = host_cpus()
     O.lib()
     k = args.cpu_sample_nars or (n_per if nar_bytes <= (64 << 20) else 1)
     host, offs = synth_nars(np.full(k, nar_bytes, np.uint64), zeros=args.zeros, first_index=0)
     nars = [host[int(offs[i]):int(offs[i + 1])] for i in range(k)]
     O.chunk_descriptors(nars[0][: 8 << 20], *params, algo=algo, nthreads=nt)  # warm
-    reps = 3  # median of three passes over the sample (~1-3 s of CPU work in all)
+    reps = 5  # median of five passes over the sample (~2-5 s of CPU work in all)
     dts = []
     for _ in range(reps):
         t0 = time.perf_counter()
@@ -485,13 +495,32 @@ def cpu_baseline(args, n_per, nar_bytes, params, algo):
             ts.append(time.perf_counter() - t)
         c1[name] = round(ten / float(np.median(ts)) / GIB, 3)
     c1["published_zeros"] = PUBLISHED_CHUNK_DATA_ZEROS
-    return {"value": round(nbytes / dt / GIB, 4), "unit": "GiB/s", "cores": nt, "kind": "port",
+    return {"value": round(nbytes / dt / GIB, 4), "unit": "GiB/s", "cores": nt,
+            "cores_note": f"threads = the CPUs this process may use: affinity {affinity}, cgroup cpu.max quota "
+                          f"{quota if quota else 'none'} (rayon's hardware_concurrency() inside the same cgroup)",
+            "kind": "port",
             "sample": f"{k} NAR(s) ({nbytes / GIB:.3f} GiB) of the same workload, one chunk_descriptors call "
                       f"per NAR, median of {reps} passes, SHA-NI={'yes' if O.lib().or_sha256_uses_shani() else 'no'}",
             "seconds": round(dt, 3),
             "nar_parallel": round(nbytes / dt_par / GIB, 4),
             "config1_chunk_data_10MiB_D_sha256": c1,
             "cpu_model": cpu_model()}
+
+
+def host_cpus():
+    """(usable, affinity, quota): the CPUs this process may use -- its affinity set,
+    capped by the cgroup v2 CPU quota (/sys/fs/cgroup/cpu.max) when one is set.  On the
+    GPU box a one-GPU job sees the host's 256 hardware threads in its affinity mask but
+    a 16-CPU quota; more threads than the quota only time-slice the same 16 CPUs."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = max(1, int(q) // int(period))
+    except (OSError, ValueError):
+        pass
+    return (min(aff, quota) if quota else aff), aff, quota
 
 
 def cpu_model() -> str:

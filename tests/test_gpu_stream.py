@@ -131,7 +131,7 @@ def test_stream_metrics_recorded_by_streaming_paths_only(ca):
 def test_stream_payloads_are_readonly_views(ca):
     """ChunkStream payloads have one type: a read-only memoryview, whether
     the chunk lies in one read slice or spans two."""
-    data = rand_bytes(3_000_000, 12)
+    data = rand_bytes(9_000_000, 12)  # three read slices of stream_read_size(256 KiB) = 4 MiB
     got = list(ca.ChunkStream(io.BytesIO(data), *P))
     slice_size = ca.chunking.stream_read_size(P[2])
     spans = [c for c in got if c.offset // slice_size != (c.offset + c.length - 1) // slice_size]
