@@ -206,7 +206,14 @@ void cg_get_gear_table(uint64_t gear[256]);
 int cg_gear_is_placeholder(void);
 /* Run the reference fixture through the GPU pipeline (scan, walk, assembly) with the
  * installed tables: CG_OK if it gives fastcdc's 10 boundaries (the set is then marked
- * verified), CG_E_TABLES with the boundaries found otherwise.  Needs a device. */
+ * verified), CG_E_TABLES with the boundaries found otherwise.  Needs a device.
+ * COVERAGE: the fixture is the reference's only FastCDC vector.  Its bytes take the
+ * values 0..250 and its avg 6000 gives bits = 13, so it exercises GEAR[0..250], MASKS[12]
+ * and MASKS[14] only.  A table set that is wrong at GEAR[251..255] or at any other
+ * MASKS entry passes this selftest, and then cuts other boundaries than fastcdc for
+ * inputs holding those bytes or for other averages.  Install the crate's arrays
+ * verbatim (scripts/install_fastcdc_tables.py, or the shim's build.rs reading them
+ * from the cargo registry), never a transcription. */
 int cg_selftest(void);
 int cg_tables_verified(void); /* 1 once the installed set passed cg_selftest */
 
