@@ -340,7 +340,7 @@ def e2e_rates(ca, torch, args, n_per, nar_bytes, params, algo, want):
         t.numpy()[:] = host0
         bufs.append((t, np.zeros(cap, ca.DESC_DTYPE), np.zeros(n_per + 1, np.uint64)))
     del host0
-    res = {"unit": "GiB/s", "batch": f"{n_per}x{nar_bytes >> 20}MiB", "reps": 2, "host_buffers": "pinned",
+    res = {"unit": "GiB/s", "batch": f"{n_per}x{nar_bytes >> 20}MiB", "reps": 4, "host_buffers": "pinned",
            "entry": "cg_chunk_batch (H2D + chunk + digest + descriptors D2H)"}
     # the host link alone: one pinned batch copied to HBM (the ceiling of every e2e rate)
     dev = torch.empty(nbytes, dtype=torch.uint8, device="cuda")

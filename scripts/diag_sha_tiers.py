@@ -20,8 +20,10 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--fill", default="0,8,16,32,64")
 ap.add_argument("--pairs", default="256")
 ap.add_argument("--nars", type=int, default=16)
+ap.add_argument("--quad-max", default="256", help="cg_test_sha_quad_max values (quads outside fill mode)")
+ap.add_argument("--params", default="65536,262144,1048576", help="config 4 (default); config 5: 262144,1048576,4194304")
 args = ap.parse_args()
-params = (64 << 10, 256 << 10, 1 << 20)
+params = tuple(int(x) for x in args.params.split(","))
 d, offs = synth_nars_device(np.full(args.nars, 1 << 30, np.uint64))
 cap = ca.chunking.batch_capacity(offs, params[0])
 out = torch.empty(cap * 48, dtype=torch.uint8, device="cuda")
@@ -29,10 +31,13 @@ sp = torch.cuda.current_stream().cuda_stream
 buf = (ctypes.c_double * 5)()
 ref = None
 res = {}
-for pairs in [int(x) for x in args.pairs.split(",")]:
-    for fill in [int(x) for x in args.fill.split(",")]:
+for qmax, pairs, fill in [(q, p, f) for q in [int(x) for x in args.quad_max.split(",")]
+                          for p in [int(x) for x in args.pairs.split(",")]
+                          for f in [int(x) for x in args.fill.split(",")]]:
+    if True:
         old_f = ca.lib.cg_test_sha_quad_fill(fill)
         old_p = ca.lib.cg_test_sha_split_max(pairs)
+        old_q = ca.lib.cg_test_sha_quad_max(qmax)
         ms = []
         for it in range(4):
             ca.lib.cg_set_profiling(1)
@@ -42,9 +47,10 @@ for pairs in [int(x) for x in args.pairs.split(",")]:
                 ms.append(buf[4])
         ca.lib.cg_test_sha_quad_fill(old_f)
         ca.lib.cg_test_sha_split_max(old_p)
+        ca.lib.cg_test_sha_quad_max(old_q)
         got = out[: int(first[-1]) * 48].cpu().numpy()
         if ref is None:
             ref = got
         assert np.array_equal(got, ref), "digests differ between tier layouts"
-        res[f"pairs{pairs}_quadfill{fill}"] = round(float(np.median(ms)), 3)
+        res[f"quadmax{qmax}_pairs{pairs}_quadfill{fill}"] = round(float(np.median(ms)), 3)
 print(json.dumps({"digest_ms": res, "chunks": int(first[-1])}))
