@@ -265,21 +265,18 @@ __device__ __forceinline__ void b3_wave_fold(uint32_t cv[8], uint32_t count, boo
 
 #define B3_WAVES 4u
 
-// group -> chunk map: thread c writes c into its chunk's group slots, and zeroes the
-// chunk's group-completion counter (k_b3_fold; the group counts in it are dead after the scan)
+// group -> chunk map: thread c writes c into its chunk's group slots
 __global__ __launch_bounds__(256) void k_b3_map(const uint64_t *__restrict__ group_base,
                                                 const uint64_t *__restrict__ total_p, uint64_t max_chunks,
-                                                uint32_t *__restrict__ gmap, uint32_t *__restrict__ done) {
+                                                uint32_t *__restrict__ gmap) {
     uint64_t total = *total_p;
     if (total > max_chunks) total = max_chunks;
     const uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x;
     if (c >= total) return;
     for (uint64_t g = group_base[c]; g < group_base[c + 1]; ++g) gmap[g] = (uint32_t)c;
-    done[c] = 0;
 }
 
-// k_b3_count + the exclusive scan + k_b3_map (and the zeroed completion counters) in one
-// single-block launch, for batches of
+// k_b3_count + the exclusive scan + k_b3_map in one single-block launch, for batches of
 // up to B3_PLAN_MAX chunk slots (config 3: ~4,400): 1024 threads, 8 consecutive chunks
 // each per pass, group counts scanned with a carry between passes, each thread then
 // writes its chunks' group -> chunk entries.  group_base[max_chunks] = the group total,
@@ -292,8 +289,7 @@ __global__ __launch_bounds__(256) void k_b3_map(const uint64_t *__restrict__ gro
 template <uint32_t LPL>
 __global__ __launch_bounds__(B3_PLAN_T) void k_b3_plan(const DescRaw *__restrict__ desc,
                                                        const uint64_t *__restrict__ total_p, uint64_t max_chunks,
-                                                       uint64_t *__restrict__ group_base, uint32_t *__restrict__ gmap,
-                                                       uint32_t *__restrict__ done) {
+                                                       uint64_t *__restrict__ group_base, uint32_t *__restrict__ gmap) {
     __shared__ uint64_t s_wave[B3_PLAN_T / 64];
     __shared__ uint64_t s_carry;
     uint64_t total = *total_p;
@@ -312,10 +308,7 @@ __global__ __launch_bounds__(B3_PLAN_T) void k_b3_plan(const DescRaw *__restrict
         uint64_t run = carry + inc - s;
 #pragma unroll
         for (uint32_t k = 0; k < B3_PLAN_ITEMS; ++k) {
-            if (c0 + k < max_chunks) {
-                group_base[c0 + k] = run;
-                done[c0 + k] = 0;  // k_b3_fold's group-completion counter
-            }
+            if (c0 + k < max_chunks) group_base[c0 + k] = run;
             for (uint32_t g = 0; g < cnt[k]; ++g) gmap[run + g] = (uint32_t)(c0 + k);
             run += cnt[k];
         }
@@ -425,76 +418,6 @@ __global__ __launch_bounds__(64 * B3_WAVES) void k_b3_groups(const uint8_t *__re
     }
 }
 
-// One wave folds chunk c's `count` group chaining values (gcv[g0 .. g0 + count), the
-// subtree values of its 64 KiB groups; <= 256 of them, chunks are <= 16 MiB) into its
-// digest: levels wider than 64 nodes through `scratch` (LDS, >= 256 x 9 words, this wave's
-// alone), the last six as register shuffles (b3_wave_fold).  The pairing is BLAKE3's
-// left-complete tree; ROOT on the last parent.
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // this wave's LDS writes done before its reads
-    __builtin_amdgcn_wave_barrier();
-}
-
-// COHERENT: gcv was written by other blocks of the running kernel (k_b3_fold), so it is
-// read with device-coherent loads (agent-scope atomics: past the XCDs' own L2s).
-template <bool COHERENT>
-__device__ __forceinline__ uint32_t gcv_load(const uint32_t *p) {
-    if constexpr (COHERENT)
-        return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-        return *p;
-}
-
-template <bool COHERENT>
-__device__ void b3_top_fold(const uint32_t *__restrict__ gcv, uint64_t g0, uint32_t count, uint32_t lane,
-                            uint32_t (*scratch)[9], uint8_t *dst) {
-    if (count <= 64) {
-        uint32_t cv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (lane < count)
-#pragma unroll
-            for (int i = 0; i < 8; ++i) cv[i] = gcv_load<COHERENT>(gcv + (g0 + lane) * 8 + i);
-        b3_wave_fold(cv, count, true, lane);
-        if (lane == 0) store_digest(dst, cv);
-        return;
-    }
-    for (uint32_t k = lane; k < count; k += 64)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) scratch[k][i] = gcv_load<COHERENT>(gcv + (g0 + k) * 8 + i);
-    wave_lds_sync();
-    while (count > 64) {
-        const uint32_t half = count >> 1;
-        uint32_t t[2][8];
-        bool wr[2];
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const uint32_t j = lane + 64u * s;
-            wr[s] = false;
-            if (j < half) {
-                b3_parent(scratch[2 * j], scratch[2 * j + 1], false, t[s]);
-                wr[s] = true;
-            } else if ((count & 1u) && j == half) {
-#pragma unroll
-                for (int i = 0; i < 8; ++i) t[s][i] = scratch[count - 1][i];
-                wr[s] = true;
-            }
-        }
-        wave_lds_sync();
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-            if (wr[s])
-#pragma unroll
-                for (int i = 0; i < 8; ++i) scratch[lane + 64u * s][i] = t[s][i];
-        wave_lds_sync();
-        count = (count + 1) >> 1;
-    }
-    uint32_t cv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (lane < count)
-#pragma unroll
-        for (int i = 0; i < 8; ++i) cv[i] = scratch[lane][i];
-    b3_wave_fold(cv, count, true, lane);
-    if (lane == 0) store_digest(dst, cv);
-}
-
 // Fold the leaf chaining values of B3_FOLD_G consecutive 64-leaf groups per wave, level
 // by level in LDS: at each level every (group, parent) slot is a lane, so a level of the
 // 16 groups costs (16 x parents) / 64 wave-wide compressions instead of one per group
@@ -503,34 +426,24 @@ __device__ void b3_top_fold(const uint32_t *__restrict__ gcv, uint64_t g0, uint3
 // the group's value goes to the digest (single-group chunks) or gcv (k_b3_top).
 #define B3_FOLD_G 16u
 #define B3_FOLD_T 256u  // 4 waves: level-1 loads all in flight at once, level slots over 4 waves
-//
-// The top of the tree (k_b3_top's job when it ran as a kernel of its own): every group
-// value written to gcv bumps its chunk's completion counter (done[c], acquire-release at
-// device scope), and the block that writes a chunk's last group folds the chunk's group
-// values into its digest right away (b3_top_fold) -- one launch less per batch, and the
-// top folds overlap the other blocks' group folds instead of following them all.
 __global__ __launch_bounds__(B3_FOLD_T) void k_b3_fold(const DescRaw *__restrict__ desc,
                                                        const uint64_t *__restrict__ total_p, uint64_t max_chunks,
                                                        const uint64_t *__restrict__ group_base,
                                                        const uint32_t *__restrict__ gmap,
                                                        const uint32_t *__restrict__ lcv, uint8_t *__restrict__ hash_base,
-                                                       size_t stride, uint32_t *__restrict__ gcv,
-                                                       uint32_t *__restrict__ done) {
+                                                       size_t stride, uint32_t *__restrict__ gcv) {
     // level-1 results only (32 per group): level 1 reads its children straight from lcv,
     // so the block needs 18 KiB of LDS and a CU holds six blocks (one dispatch round at
     // 1 GiB; the 64-node layout took 37 KiB and two rounds)
     __shared__ uint32_t s_node[B3_FOLD_G][32][9];  // 9: a CV's 8 words + 1 (bank spread)
     __shared__ uint32_t s_cnt[B3_FOLD_G];          // nodes at the current level (0: skip)
     __shared__ uint32_t s_whole[B3_FOLD_G];
-    __shared__ uint32_t s_top[B3_FOLD_G];          // chunks whose last group this block wrote
-    __shared__ uint32_t s_ntop;
     uint64_t total = *total_p;
     if (total > max_chunks) total = max_chunks;
     const uint64_t ng = group_base[total];
     const uint64_t g0 = (uint64_t)blockIdx.x * B3_FOLD_G;
     if (g0 >= ng) return;  // uniform over the block
     const uint32_t t = threadIdx.x;
-    if (t == 0) s_ntop = 0;
     if (t < B3_FOLD_G) {
         const uint64_t g = g0 + t;
         uint32_t cnt = 0, whole = 0;
@@ -627,44 +540,19 @@ __global__ __launch_bounds__(B3_FOLD_T) void k_b3_fold(const DescRaw *__restrict
         if (g < ng && s_cnt[t]) {  // 1 node left
             const uint32_t *w = s_node[t][0];
             const uint32_t cv[8] = {w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7]};
-            const uint32_t c = gmap[g];
             if (s_whole[t]) {
-                store_digest(hash_base + (uint64_t)c * stride, cv);
+                store_digest(hash_base + (uint64_t)gmap[g] * stride, cv);
             } else {
-                // The group value goes out with device-coherent stores (agent-scope atomic
-                // stores, written through past this XCD's L2), all of them complete (vmcnt)
-                // before the count that may complete chunk c; the top fold reads the values
-                // back with device-coherent loads.  (Acquire / release at agent scope would
-                // write back and invalidate the whole L2 of the XCD on every count.)
 #pragma unroll
-                for (int i = 0; i < 8; ++i)
-                    __hip_atomic_store(gcv + g * 8 + i, cv[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                const uint32_t n = (uint32_t)(group_base[c + 1] - group_base[c]);
-                const uint32_t prev = __hip_atomic_fetch_add(done + c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (prev + 1 == n) s_top[atomicAdd(&s_ntop, 1u)] = c;
+                for (int i = 0; i < 8; ++i) gcv[g * 8 + i] = cv[i];
             }
         }
     }
-    __syncthreads();
-    const uint32_t ntop = s_ntop;  // uniform
-    if (ntop == 0) return;
-    // chunks of <= 64 groups round-robin over the waves (registers only); larger ones
-    // (max_size > 4 MiB) on wave 0, with the block's level storage (dead by now) as scratch
-    const uint32_t wv = t >> 6, lane = t & 63u;
-    uint32_t(*scratch)[9] = reinterpret_cast<uint32_t(*)[9]>(&s_node[0][0][0]);
-    static_assert(sizeof(s_node) >= 256 * 9 * sizeof(uint32_t), "scratch for a 256-group top fold");
-    for (uint32_t k = 0; k < ntop; ++k) {
-        const uint32_t c = s_top[k];
-        const uint64_t gb = group_base[c];
-        const uint32_t count = (uint32_t)(group_base[c + 1] - gb);
-        if (count > 64 ? wv == 0 : k % (B3_FOLD_T / 64) == wv)
-            b3_top_fold<true>(gcv, gb, count, lane, scratch, hash_base + (uint64_t)c * stride);
-    }
 }
 
-// One wave per chunk with more than one group (the in-wave-fold path, hash_spans and the
-// diagnostics' fold modes; the product's deferred path folds the top inside k_b3_fold).
+// One wave per chunk with more than one group: fold the subtree chaining values
+// (<= 256 of them: chunks are <= 16 MiB).  Levels wider than 64 nodes go through
+// LDS; the last six levels are register shuffles (b3_wave_fold).
 __global__ __launch_bounds__(64) void k_b3_top(const DescRaw *__restrict__ desc, const uint64_t *__restrict__ total_p,
                                                uint64_t max_chunks, const uint64_t *__restrict__ group_base,
                                                const uint32_t *__restrict__ gcv, uint8_t *__restrict__ hash_base,
@@ -675,9 +563,54 @@ __global__ __launch_bounds__(64) void k_b3_top(const DescRaw *__restrict__ desc,
     const uint64_t c = blockIdx.x;
     if (c >= total) return;
     const uint64_t g0 = group_base[c];
-    const uint32_t count = (uint32_t)(group_base[c + 1] - g0);
+    uint32_t count = (uint32_t)(group_base[c + 1] - g0);
     if (count <= 1) return;
-    b3_top_fold<false>(gcv, g0, count, threadIdx.x, s_cv, hash_base + c * stride);
+    const uint32_t lane = threadIdx.x;
+    if (count <= 64) {
+        uint32_t cv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (lane < count)
+#pragma unroll
+            for (int i = 0; i < 8; ++i) cv[i] = gcv[(g0 + lane) * 8 + i];
+        b3_wave_fold(cv, count, true, lane);
+        if (lane == 0) store_digest(hash_base + c * stride, cv);
+        return;
+    }
+    for (uint32_t k = lane; k < count; k += 64)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s_cv[k][i] = gcv[(g0 + k) * 8 + i];
+    __syncthreads();
+    while (count > 64) {
+        const uint32_t half = count >> 1;
+        uint32_t t[2][8];
+        bool wr[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const uint32_t j = lane + 64u * s;
+            wr[s] = false;
+            if (j < half) {
+                b3_parent(s_cv[2 * j], s_cv[2 * j + 1], false, t[s]);
+                wr[s] = true;
+            } else if ((count & 1u) && j == half) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) t[s][i] = s_cv[count - 1][i];
+                wr[s] = true;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+            if (wr[s])
+#pragma unroll
+                for (int i = 0; i < 8; ++i) s_cv[lane + 64u * s][i] = t[s][i];
+        __syncthreads();
+        count = (count + 1) >> 1;
+    }
+    uint32_t cv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (lane < count)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) cv[i] = s_cv[lane][i];
+    b3_wave_fold(cv, count, true, lane);
+    if (lane == 0) store_digest(hash_base + c * stride, cv);
 }
 
 #ifdef CG_DIAG
@@ -814,27 +747,21 @@ void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
     }
 #endif
     // (a forced scan path, cg_test_scan_path, takes the three-kernel form so tests reach it)
-    // d_gcount_u32 doubles as k_b3_fold's per-chunk completion counters (zeroed by the plan or
-    // by k_b3_map, after the scan has consumed the counts)
     if (max_chunks <= B3_PLAN_MAX && g_scan_path == 0) {
-        hipLaunchKernelGGL(plan, dim3(1), dim3(B3_PLAN_T), 0, st, desc, d_total, max_chunks, d_group_base, d_gmap,
-                           d_gcount_u32);
+        hipLaunchKernelGGL(plan, dim3(1), dim3(B3_PLAN_T), 0, st, desc, d_total, max_chunks, d_group_base, d_gmap);
     } else {
         hipLaunchKernelGGL(count, dim3(cblocks), dim3(256), 0, st, desc, d_total, max_chunks, d_gcount_u32);
         launch_exclusive_scan_u32(d_gcount_u32, d_group_base, max_chunks, 0, d_scan_tmp, st);
-        hipLaunchKernelGGL(k_b3_map, dim3(cblocks), dim3(256), 0, st, d_group_base, d_total, max_chunks, d_gmap,
-                           d_gcount_u32);
+        hipLaunchKernelGGL(k_b3_map, dim3(cblocks), dim3(256), 0, st, d_group_base, d_total, max_chunks, d_gmap);
     }
     hipLaunchKernelGGL(groups,
                        dim3((uint32_t)((gbound + B3_WAVES - 1) / B3_WAVES)), dim3(64 * B3_WAVES), 0, st, d_data, d_abs,
                        desc, d_total, max_chunks, d_group_base, d_gmap, d_hash_base, hash_stride, d_gcv, d_lcv);
-    if (defer)  // group folds, and each multi-group chunk's top fold by the block finishing it
+    if (defer)
         hipLaunchKernelGGL(k_b3_fold, dim3((uint32_t)((gbound + B3_FOLD_G - 1) / B3_FOLD_G)), dim3(B3_FOLD_T), 0, st, desc,
-                           d_total, max_chunks, d_group_base, d_gmap, d_lcv, d_hash_base, hash_stride, d_gcv,
-                           d_gcount_u32);
-    else
-        hipLaunchKernelGGL(k_b3_top, dim3((uint32_t)max_chunks), dim3(64), 0, st, desc, d_total, max_chunks,
-                           d_group_base, d_gcv, d_hash_base, hash_stride);
+                           d_total, max_chunks, d_group_base, d_gmap, d_lcv, d_hash_base, hash_stride, d_gcv);
+    hipLaunchKernelGGL(k_b3_top, dim3((uint32_t)max_chunks), dim3(64), 0, st, desc, d_total, max_chunks,
+                       d_group_base, d_gcv, d_hash_base, hash_stride);
 }
 
 }  // namespace cg

@@ -183,6 +183,7 @@ int ensure_gear(Workspace *ws, const Tables &t) {
 // the link, finishing together, and every batch's work starting only then (bench.py
 // `e2e`).  Small copies are not held behind a large one.
 constexpr size_t H2D_CHAIN_MIN = 64ull << 20;
+std::atomic<uint32_t> g_h2d_chain{1};  // test hook cg_test_h2d_chain (0: every copy unchained)
 struct H2DChain {
     std::mutex mu;
     hipEvent_t last = nullptr;  // the event recorded after the newest chained copy
@@ -190,7 +191,7 @@ struct H2DChain {
 H2DChain g_h2d[MAX_DEV];
 
 int h2d_input(Workspace *ws, void *dst, const void *src, size_t bytes) {
-    if (bytes < H2D_CHAIN_MIN) {
+    if (bytes < H2D_CHAIN_MIN || !g_h2d_chain.load(std::memory_order_relaxed)) {
         HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ws->stream));
         return CG_OK;
     }
@@ -814,6 +815,10 @@ uint32_t cg_abi_version(void) { return CG_ABI_VERSION; }
 // Test hook: make the n-th device-buffer growth from now fail as out of memory (0 = off);
 // returns the previous countdown.
 uint32_t cg_test_fail_alloc(uint32_t n) { return cgrt::g_fail_alloc.exchange(n); }
+
+// Test hook: chain large host-entry input copies device-wide (1, the default) or not (0);
+// returns the previous setting.
+uint32_t cg_test_h2d_chain(uint32_t on) { return cgrt::g_h2d_chain.exchange(on ? 1u : 0u); }
 
 const char *cg_last_error_message(void) { return t_err.c_str(); }
 

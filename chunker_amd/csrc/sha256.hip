@@ -829,10 +829,14 @@ constexpr uint32_t g_sha_mode = 0;
 uint32_t g_sha_split_max = 256;
 // Quad workgroups per launch (8 longest chunks each).  Test hook cg_test_sha_quad_max.
 uint32_t g_sha_quad_max = 256;
-// Quad workgroups when the batch fills the GPU: a few, for the longest chunks only
-// (config 4: 32 -> digest 23.7 -> 21.7 ms; all 256 would hold back the one-lane
-// workgroups queued behind them, 26 ms).  Test hook cg_test_sha_quad_fill.
-uint32_t g_sha_quad_fill = 32;
+// Quad and pair workgroups when the batch fills the GPU: enough quads for the longest
+// chunks (all 256 would hold back the one-lane workgroups queued behind them) and half
+// the pair workgroups of a latency-bound batch -- a pair spends 1.4x the SIMD time of one
+// lane per chunk, and in a GPU-filling batch the three tiers end together (DESIGN.md §4,
+// config 4: 32 quads / 256 pairs 21.7 ms, 64 / 128 19.9-20.3 ms in the same sweep,
+// profiles/r03_v2_diag_sha_tiers_c4.json, r03_v3_...).  Test hook cg_test_sha_quad_fill.
+uint32_t g_sha_quad_fill = 64;
+uint32_t g_sha_pair_fill = 128;
 // Spin-guard limit (sleeps per wait) of the producer/consumer hand-off: test hook
 // cg_test_sha_spin_limit.
 uint32_t g_sha_spin_limit = 1u << 26;
@@ -843,16 +847,18 @@ uint32_t g_sha_spin_limit = 1u << 26;
 // behind them fits in one round of workgroups (<= 256 x 64 chunks); on a batch that
 // fills the GPU (config 4) only g_sha_quad_fill of them, for the longest chunks.
 uint32_t sha256_grid(uint64_t max_chunks, uint64_t expected, uint32_t *nquad_out, uint32_t *npair_out) {
-    auto tiers = [&](uint64_t qmax, uint64_t &nq, uint64_t &np) {
+    auto tiers = [&](uint64_t qmax, uint64_t pmax, uint64_t &nq, uint64_t &np) {
         nq = (max_chunks + 7) / 8;
         if (nq > qmax) nq = qmax;
         const uint64_t rest = max_chunks > 8 * nq ? max_chunks - 8 * nq : 0;
         np = (rest + 31) / 32;
-        if (np > g_sha_split_max) np = g_sha_split_max;
+        if (np > pmax) np = pmax;
     };
     uint64_t nq, np;
-    tiers(g_sha_quad_max, nq, np);
-    if (expected > 8 * nq + 32 * np + 256 * 64) tiers(std::min<uint64_t>(g_sha_quad_max, g_sha_quad_fill), nq, np);
+    tiers(g_sha_quad_max, g_sha_split_max, nq, np);
+    if (expected > 8 * nq + 32 * np + 256 * 64)
+        tiers(std::min<uint64_t>(g_sha_quad_max, g_sha_quad_fill), std::min<uint64_t>(g_sha_split_max, g_sha_pair_fill),
+              nq, np);
     const uint64_t rest = max_chunks > 8 * nq + 32 * np ? max_chunks - 8 * nq - 32 * np : 0;
     if (nquad_out) *nquad_out = (uint32_t)nq;
     if (npair_out) *npair_out = (uint32_t)np;
@@ -991,6 +997,12 @@ extern "C" uint32_t cg_test_sha_spin_limit(uint32_t v) {
 extern "C" uint32_t cg_test_sha_quad_fill(uint32_t v) {
     const uint32_t old = cg::g_sha_quad_fill;
     cg::g_sha_quad_fill = v;
+    return old;
+}
+
+extern "C" uint32_t cg_test_sha_pair_fill(uint32_t v) {
+    const uint32_t old = cg::g_sha_pair_fill;
+    cg::g_sha_pair_fill = v;
     return old;
 }
 

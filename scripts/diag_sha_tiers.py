@@ -38,6 +38,7 @@ for qmax, pairs, fill in [(q, p, f) for q in [int(x) for x in args.quad_max.spli
         old_f = ca.lib.cg_test_sha_quad_fill(fill)
         old_p = ca.lib.cg_test_sha_split_max(pairs)
         old_q = ca.lib.cg_test_sha_quad_max(qmax)
+        old_pf = ca.lib.cg_test_sha_pair_fill(pairs)  # --pairs also sets the GPU-filling pair count
         ms = []
         for it in range(4):
             ca.lib.cg_set_profiling(1)
@@ -48,6 +49,7 @@ for qmax, pairs, fill in [(q, p, f) for q in [int(x) for x in args.quad_max.spli
         ca.lib.cg_test_sha_quad_fill(old_f)
         ca.lib.cg_test_sha_split_max(old_p)
         ca.lib.cg_test_sha_quad_max(old_q)
+        ca.lib.cg_test_sha_pair_fill(old_pf)
         got = out[: int(first[-1]) * 48].cpu().numpy()
         if ref is None:
             ref = got
