@@ -47,8 +47,7 @@ EXPORTS = (
 )
 # test hooks the product library exports beyond the header (tier caps, spin-guard limit)
 TEST_HOOKS = ("cg_test_sha_quad_max", "cg_test_sha_split_max", "cg_test_sha_spin_limit", "cg_test_cas_pair_max",
-              "cg_test_fail_alloc", "cg_test_sha_quad_fill", "cg_test_sha_pair_fill", "cg_test_scan_path",
-              "cg_test_h2d_chain")
+              "cg_test_fail_alloc", "cg_test_sha_quad_fill", "cg_test_sha_pair_fill", "cg_test_scan_path")
 
 
 def _hw_queues_default() -> None:
@@ -144,7 +143,7 @@ def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
     L.cg_tables_verified.restype = i
     u32 = ctypes.c_uint32
     for name in ("cg_test_sha_quad_max", "cg_test_sha_split_max", "cg_test_sha_spin_limit", "cg_test_sha_quad_fill",
-                 "cg_test_sha_pair_fill", "cg_test_scan_path", "cg_test_h2d_chain"):
+                 "cg_test_sha_pair_fill", "cg_test_scan_path"):
         getattr(L, name).argtypes = [u32]
         getattr(L, name).restype = u32
     L.cg_test_cas_pair_max.argtypes = [ctypes.c_int64]

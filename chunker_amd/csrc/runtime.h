@@ -113,7 +113,6 @@ struct Workspace {
     // their longest chunk's serial chain, not by the chip, so they overlap for free.
     hipStream_t side_stream = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_cas = nullptr;
-    hipEvent_t ev_h2d = nullptr;  // after this workspace's last chained input copy (runtime.hip h2d_input)
     // Streams map onto the process's few hardware queues (GPU_MAX_HW_QUEUES, 4 by default)
     // and two streams on one queue serialise: the side stream exists only where used.
     int ensure_side_stream() {

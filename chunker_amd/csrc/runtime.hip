@@ -176,35 +176,6 @@ int ensure_gear(Workspace *ws, const Tables &t) {
     return CG_OK;
 }
 
-// Host-entry input copies of at least H2D_CHAIN_MIN bytes are chained device-wide in
-// issue order: each waits (on the GPU) for the previous one to land.  K concurrent
-// callers' batches then cross the host link one after another at its full rate, and each
-// batch's kernels start as soon as its own bytes are in -- rather than K copies sharing
-// the link, finishing together, and every batch's work starting only then (bench.py
-// `e2e`).  Small copies are not held behind a large one.
-constexpr size_t H2D_CHAIN_MIN = 64ull << 20;
-std::atomic<uint32_t> g_h2d_chain{1};  // test hook cg_test_h2d_chain (0: every copy unchained)
-struct H2DChain {
-    std::mutex mu;
-    hipEvent_t last = nullptr;  // the event recorded after the newest chained copy
-};
-H2DChain g_h2d[MAX_DEV];
-
-int h2d_input(Workspace *ws, void *dst, const void *src, size_t bytes) {
-    if (bytes < H2D_CHAIN_MIN || !g_h2d_chain.load(std::memory_order_relaxed)) {
-        HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ws->stream));
-        return CG_OK;
-    }
-    if (!ws->ev_h2d) HIP_TRY(hipEventCreateWithFlags(&ws->ev_h2d, hipEventDisableTiming));
-    H2DChain &c = g_h2d[ws->device];
-    std::lock_guard<std::mutex> g(c.mu);
-    if (c.last) HIP_TRY(hipStreamWaitEvent(ws->stream, c.last, 0));
-    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ws->stream));
-    HIP_TRY(hipEventRecord(ws->ev_h2d, ws->stream));
-    c.last = ws->ev_h2d;  // (workspaces live for the process: the event outlives the chain)
-    return CG_OK;
-}
-
 // The SHA-256 kernel's spin-guard word (launch_sha256 d_err): zeroed before a digest
 // launch, copied back with the call's other results, checked after the stream sync.
 int sha_err_arm(Workspace *ws, hipStream_t st) {
@@ -575,7 +546,7 @@ int batch_host(const uint8_t *data, const uint64_t *nar_offsets, size_t n_nars, 
     for (size_t i = 0; i < n_nars; ++i) total_cap += capacity_of(off[i + 1] - off[i], o.min);
     if ((rc = ws->in.ensure(bytes + 256, "input"))) return rc;
     if ((rc = ws->out.ensure((total_cap + 1) * sizeof(cg_desc), "descriptors"))) return rc;
-    if (bytes && (rc = h2d_input(ws, ws->in.p, data + lo, bytes))) return rc;
+    if (bytes) HIP_TRY(hipMemcpyAsync(ws->in.p, data + lo, bytes, hipMemcpyHostToDevice, ws->stream));
     std::vector<uint64_t> first(n_nars + 1);
     rc = run_batch(ws, ws->in.as<uint8_t>(), off.data(), n_nars, o, algo, ws->out.as<cg_desc>(), total_cap,
                    first.data(), ws->stream);
@@ -816,10 +787,6 @@ uint32_t cg_abi_version(void) { return CG_ABI_VERSION; }
 // returns the previous countdown.
 uint32_t cg_test_fail_alloc(uint32_t n) { return cgrt::g_fail_alloc.exchange(n); }
 
-// Test hook: chain large host-entry input copies device-wide (1, the default) or not (0);
-// returns the previous setting.
-uint32_t cg_test_h2d_chain(uint32_t on) { return cgrt::g_h2d_chain.exchange(on ? 1u : 0u); }
-
 const char *cg_last_error_message(void) { return t_err.c_str(); }
 
 int cg_validate(uint64_t min_size, uint64_t avg_size, uint64_t max_size, char *msg, size_t msg_cap) {
@@ -944,7 +911,7 @@ int cg_node_put(const uint8_t *data, uint64_t len, uint64_t min_size, uint64_t a
     if ((rc = ws->in.ensure(len + 256, "input"))) return rc;
     if ((rc = ws->out.ensure((cap + 1) * sizeof(cg_desc), "descriptors"))) return rc;
     if ((rc = ws->span_len.ensure((cap + 1) * 32, "chunk ids"))) return rc;
-    if (len && (rc = h2d_input(ws, ws->in.p, data, len))) return rc;
+    if (len) HIP_TRY(hipMemcpyAsync(ws->in.p, data, len, hipMemcpyHostToDevice, ws->stream));
     uint64_t offs[2] = {0, len}, first[2] = {0, 0};
     uint8_t man[32];
     rc = run_batch(ws, ws->in.as<uint8_t>(), offs, 1, o, CG_SHA256, ws->out.as<cg_desc>(), cap, first, ws->stream,

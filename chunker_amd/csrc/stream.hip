@@ -17,10 +17,11 @@
 // completed); when no slot is free a push waits for the oldest group.
 //
 // Device resources are taken as the stream needs them: the arena starts at two slots at
-// the first push and doubles (up to the in-flight budget) only when the pipeline runs
-// out of free slots; digest lanes (stream + event + scratch) are created one at a time
-// when every existing lane is busy.  A short stream therefore holds two slots and one
-// lane, not the whole budget.  The first failure of push / finish / take poisons the
+// the first push and grows to the full in-flight budget only when the pipeline runs out
+// of free slots; digest lanes (stream + event + scratch) are created one at a time when
+// every existing lane is busy.  A short stream therefore holds two slots and one lane,
+// not the whole budget.  (The two-slot arena is kept until the handle is freed: freeing
+// device memory waits for the whole device, which would drain the digest pipeline.)  The first failure of push / finish / take poisons the
 // handle: every later call returns the same status (a failed push may have left part of
 // its slice inside the engine, so nothing after it could be trusted).
 #include <algorithm>
@@ -94,7 +95,7 @@ struct cg_stream {
     int device = -1;
     Workspace *ws = nullptr;  // boundary pipeline, held for the handle's lifetime
     Arena arena;
-    std::vector<Arena> retired;  // earlier, smaller arenas still read by launched groups
+    std::vector<Arena> retired;  // the first, two-slot arena once grown (freed with the handle)
     uint64_t slot_bytes = 0, max_slots = 0, group_bytes = 0;
     size_t max_lanes = 0;
     int poisoned = CG_OK;  // first failure of push / finish / take, returned by every later call
@@ -133,20 +134,6 @@ namespace cgrt {
 uint8_t *slot_ptr(cg_stream *h, uint64_t seq) { return h->arena.p + (seq % h->arena.nslots) * h->slot_bytes; }
 uint64_t slot_off(const cg_stream *h, uint64_t seq) { return (seq % h->arena.nslots) * h->slot_bytes; }
 
-// Retired arenas no launched group reads any more are freed.
-void release_retired(cg_stream *h) {
-    for (size_t i = 0; i < h->retired.size();) {
-        bool used = false;
-        for (const Group &g : h->inflight) used = used || g.base == h->retired[i].p;
-        if (used) {
-            ++i;
-        } else {
-            h->retired[i].release();
-            h->retired.erase(h->retired.begin() + i);
-        }
-    }
-}
-
 // Wait for the oldest launched group, check it, and move its chunks (now with digests)
 // to the ready queue.
 int complete_oldest(cg_stream *h) {
@@ -166,7 +153,6 @@ int complete_oldest(cg_stream *h) {
         h->ready.push_back(d);
     }
     h->inflight.pop_front();
-    if (!h->retired.empty()) release_retired(h);
     return CG_OK;
 }
 
@@ -244,15 +230,16 @@ int launch_open(cg_stream *h) {
     return CG_OK;
 }
 
-// Double the arena (up to the budget) instead of waiting for a slot.  A group never
-// spans two arenas, so the open one is launched on the current arena first; the old
-// arena is kept until the groups reading it (and the pending tail move) are done.  When
-// the device has no memory for the larger arena the budget shrinks to the current size.
+// Grow the arena to the full budget instead of waiting for a slot.  A group never spans
+// two arenas, so the open one is launched on the current arena first; the old arena stays
+// allocated (launched groups and the pending tail move still read it) until the handle
+// is freed.  When the device has no memory for the larger arena the budget shrinks to
+// the current size.
 int grow_arena(cg_stream *h) {
     int rc;
     if ((rc = launch_open(h))) return rc;
     Arena nb;
-    if (nb.alloc(std::min(h->arena.nslots * 2, h->max_slots), h->slot_bytes)) {
+    if (nb.alloc(h->max_slots, h->slot_bytes)) {
         clear_error();
         h->max_slots = h->arena.nslots;
         return CG_OK;

@@ -117,8 +117,8 @@ void cg_push_free(cg_push *h);
  * ChunkStreamAsync yields.  Device memory is bounded by `inflight_bytes` (0 = 512 MiB):
  * an arena of slots of max_size + slice_bytes (0 = 8 MiB, the reference's read size,
  * :713-716) bytes, each reused only after the digests reading it completed.  The arena
- * starts at two slots at the first push and doubles up to that budget only when no slot
- * is free (a short stream holds two slots); at the budget a push waits for the oldest
+ * starts at two slots at the first push and grows to that budget only when no slot is
+ * free (a short stream holds two slots); at the budget a push waits for the oldest
  * digests.  Digests run on up to one HIP stream per hardware queue beside the call's
  * own (GPU_MAX_HW_QUEUES - 1, 3..8, read at cg_stream_new), created as they are needed.
  * push returns once its bytes are copied: the caller may reuse `data` right away.  take

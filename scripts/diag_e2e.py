@@ -5,9 +5,10 @@ memory; K threads; per mode the aggregate GiB/s and each call's latency (ms):
   h2d      K threads, each copying its batch to HBM on its own stream (the link alone);
   h2d_busy the same while K device-resident batches digest on other streams (the link
            under compute load);
-  e2e      K threads calling cg_chunk_batch (H2D + chunk + digest + D2H), large input
-           copies chained device-wide (the product);
-  e2e_nochain  the same with every copy unchained (cg_test_h2d_chain(0)).
+  e2e      K threads calling cg_chunk_batch (H2D + chunk + digest + D2H).
+(Round 3 also tried chaining the callers' input copies device-wide in issue order, so
+they would cross the link one at a time: K8 28.2 / K16 24.4 GiB/s against 36.7 / 45.4
+unchained, profiles/r03_v4_diag_e2e.json; removed.)
 Prints one JSON object."""
 import os
 os.environ.setdefault("CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR", "1")
@@ -29,7 +30,7 @@ from chunker_amd.nar import synth_nars  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--k", default="4,8,16")
 ap.add_argument("--reps", type=int, default=4)
-ap.add_argument("--modes", default="h2d,h2d_busy,e2e,e2e_nochain")
+ap.add_argument("--modes", default="h2d,h2d_busy,e2e")
 args = ap.parse_args()
 GIB = 1 << 30
 params = (256 << 10, 1 << 20, 4 << 20)
@@ -127,13 +128,6 @@ for K in ks:
     if "e2e" in modes:
         run(K, e2e, 1)
         r["e2e"] = run(K, e2e, args.reps)
-    if "e2e_nochain" in modes:
-        old = ca.lib.cg_test_h2d_chain(0)
-        try:
-            run(K, e2e, 1)
-            r["e2e_nochain"] = run(K, e2e, args.reps)
-        finally:
-            ca.lib.cg_test_h2d_chain(old)
     res[f"K{K}"] = r
     print(json.dumps({f"K{K}": r}), file=sys.stderr, flush=True)
 print(json.dumps(res))
