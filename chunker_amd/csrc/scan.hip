@@ -220,22 +220,32 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
     __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * GEAR_COPIES];
     __shared__ uint32_t s_slots[SCAN2_T / 64][64];  // the open segment's candidate slots, per wave
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t seg0 = ((uint64_t)blockIdx.x * (SCAN2_T / 64) + (threadIdx.x >> 6)) * spw;
+    // the wave index through readfirstlane: the run's base, bounds and buffer resource
+    // are then scalar (SGPRs), not per-lane copies
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t seg0 = ((uint64_t)blockIdx.x * (SCAN2_T / 64) + wv) * spw;
     const bool active = seg0 < nseg;  // whole wave (uniform)
     const uint64_t r0 = seg0 * CG_SEG;
     const uint64_t nrow = (uint64_t)spw * F32_RPS;  // a multiple of RING (spw a multiple of 4)
     static_assert(RING % F32_RPS == 0 && 8 % RING == 0, "ring trips end on segment boundaries");
-    const uint64_t last_abs = (n - 1) & ~(uint64_t)15;
+    // The run's rows are read through a buffer resource based at the run (wave-uniform, in
+    // SGPRs) whose size ends at the batch end: a row's address is an SGPR offset plus the
+    // lane's constant 32 L, and a load past the batch end returns zeros instead of
+    // faulting, so no per-lane address arithmetic or clamp is left in the row loop (the
+    // bytes past the end only feed candidates the tail rows mask off).
     typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-    auto ld = [&](uint64_t a) {
-        const u32x4_t *q = reinterpret_cast<const u32x4_t *>(data + (a < last_abs ? a : last_abs));
-        const u32x4_t x = NT ? __builtin_nontemporal_load(q) : *q;
-        return uint4{x.x, x.y, x.z, x.w};
-    };
+    const uint64_t run_bytes = nrow * F32_ROW;  // <= spw x 4 KiB: 32-bit offsets
+    const uint64_t avail = active ? n - r0 : 0;
+    const __amdgpu_buffer_rsrc_t run_rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(data + (active ? r0 : 0)), (short)0, (int)(avail < run_bytes ? avail : run_bytes),
+        0x00027000);
+    const uint32_t lane_off = 32u * lane;
     auto blk = [&](uint64_t row, uint4 (&v)[2]) {
-        const uint64_t a = r0 + row * F32_ROW + 32u * lane;
-        v[0] = ld(a);
-        v[1] = ld(a + 16);
+        const uint32_t so = (uint32_t)(row * F32_ROW);
+        const u32x4_t x0 = __builtin_amdgcn_raw_buffer_load_b128(run_rs, lane_off, so, NT ? 2 : 0);  // aux 2: nt
+        const u32x4_t x1 = __builtin_amdgcn_raw_buffer_load_b128(run_rs, lane_off + 16u, so, NT ? 2 : 0);
+        v[0] = uint4{x0.x, x0.y, x0.z, x0.w};
+        v[1] = uint4{x1.x, x1.y, x1.z, x1.w};
     };
     static_assert(SCAN2_T == 2 * 256 && GEAR_COPIES == 32, "two threads per Gear entry, 16 copies each");
     const uint32_t ge = threadIdx.x >> 1;
@@ -256,7 +266,7 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
     __syncthreads();
     if (!active) return;
     const char *gbase = reinterpret_cast<const char *>(s_gear);
-    uint32_t *slots = s_slots[threadIdx.x >> 6];
+    uint32_t *slots = s_slots[wv];
     const uint32_t lo8 = (threadIdx.x & 31u) * 8u;
     uint32_t ad[2][4];
 #pragma unroll
