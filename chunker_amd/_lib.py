@@ -47,7 +47,8 @@ EXPORTS = (
 )
 # test hooks the product library exports beyond the header (tier caps, spin-guard limit)
 TEST_HOOKS = ("cg_test_sha_quad_max", "cg_test_sha_split_max", "cg_test_sha_spin_limit", "cg_test_cas_pair_max",
-              "cg_test_fail_alloc", "cg_test_sha_quad_fill", "cg_test_sha_pair_fill", "cg_test_scan_path")
+              "cg_test_fail_alloc", "cg_test_sha_quad_fill", "cg_test_sha_pair_fill", "cg_test_scan_path",
+              "cg_test_stream_group_cap", "cg_test_stream_max_lanes", "cg_test_stream_eager")
 
 
 def _hw_queues_default() -> None:
@@ -148,6 +149,12 @@ def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
         getattr(L, name).restype = u32
     L.cg_test_cas_pair_max.argtypes = [ctypes.c_int64]
     L.cg_test_cas_pair_max.restype = ctypes.c_int64
+    if hasattr(L, "cg_test_stream_group_cap"):  # (absent from builds before round 3: A/B runs)
+        L.cg_test_stream_group_cap.argtypes = [u64]
+        L.cg_test_stream_group_cap.restype = u64
+        for name in ("cg_test_stream_eager", "cg_test_stream_max_lanes"):
+            getattr(L, name).argtypes = [u32]
+            getattr(L, name).restype = u32
     L.cg_test_fail_alloc.argtypes = [ctypes.c_uint32]
     L.cg_test_fail_alloc.restype = ctypes.c_uint32
     L.cg_set_profiling.argtypes = [i]

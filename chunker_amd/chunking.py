@@ -443,13 +443,14 @@ def stream_read_size(max_size: int) -> int:
     return max(min(target, effective_read_slice_cap()), MIN_READ_SLICE_CAP)
 
 
-DEFAULT_STREAM_INFLIGHT = 512 * 1024 * 1024
+DEFAULT_STREAM_INFLIGHT = 2048 * 1024 * 1024
 
 
 def stream_inflight_bytes() -> int:
     """HBM the engine may hold for one ChunkStream's slices in flight (cg_stream_new):
-    CHUNKER_AMD_STREAM_INFLIGHT_BYTES, default 512 MiB.  The host keeps the same
-    slices alive until their chunks are emitted (payloads are slices of them)."""
+    CHUNKER_AMD_STREAM_INFLIGHT_BYTES, default 2 GiB (the engine's own default).  The
+    host keeps the same slices alive until their chunks are emitted (payloads are
+    slices of them)."""
     try:
         v = int(os.environ.get("CHUNKER_AMD_STREAM_INFLIGHT_BYTES", ""))
         if v > 0:

@@ -34,22 +34,50 @@
 namespace cgrt {
 
 // One digest launch in flight: device scratch, pinned staging and its own stream.
+// Scratch grows without freeing: hipFree / hipHostFree wait for the whole device, i.e.
+// for every digest in flight (a 50-75 ms stall per growth), so a lane keeps the buffers
+// it outgrew (at most as much again, growth is by doubling) until it is destroyed.
 struct Lane {
     hipStream_t st = nullptr;
     hipEvent_t done = nullptr;
     DevBuf desc, abs, total, order, err, b3_gcount, b3_gbase, b3_gcv, b3_gmap, scan_tmp;
     PinBuf stage;  // [descs | abs | total | err]
+    std::vector<void *> old_dev, old_pin;
     bool busy = false;
     int init() {
         HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
         HIP_TRY(hipEventCreateWithFlags(&done, hipEventDisableTiming));
         return CG_OK;
     }
+    int ensure(DevBuf &b, size_t bytes, const char *name) {
+        if (bytes <= b.cap) return CG_OK;
+        const size_t want = std::max(bytes + 256, 2 * b.cap);
+        void *p = nullptr;
+        const hipError_t e = test_alloc_fault() ? hipErrorOutOfMemory : hipMalloc(&p, want);
+        if (e != hipSuccess) return hip_fail(e, name, want);
+        if (b.p) old_dev.push_back(b.p);
+        b.p = p;
+        b.cap = want;
+        return CG_OK;
+    }
+    int ensure_stage(size_t bytes) {
+        if (bytes <= stage.cap) return CG_OK;
+        const size_t want = std::max(bytes + 256, 2 * stage.cap);
+        void *p = nullptr;
+        const hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e != hipSuccess) return hip_fail(e, "hipHostMalloc", want);
+        if (stage.p) old_pin.push_back(stage.p);
+        stage.p = p;
+        stage.cap = want;
+        return CG_OK;
+    }
     void destroy() {
         if (st) (void)hipStreamSynchronize(st);
         for (DevBuf *b : {&desc, &abs, &total, &order, &err, &b3_gcount, &b3_gbase, &b3_gcv, &b3_gmap, &scan_tmp})
             b->release();
+        for (void *p : old_dev) (void)hipFree(p);
         if (stage.p) (void)hipHostFree(stage.p);
+        for (void *p : old_pin) (void)hipHostFree(p);
         if (done) (void)hipEventDestroy(done);
         if (st) (void)hipStreamDestroy(st);
     }
@@ -84,6 +112,12 @@ struct Arena {
         nslots = 0;
     }
 };
+
+// Stream shape knobs (test hooks cg_test_stream_group_cap / cg_test_stream_max_lanes):
+// 0 = the built-in rule of cg_stream_new.
+uint64_t g_stream_group_cap = 0;
+uint32_t g_stream_max_lanes = 0;
+uint32_t g_stream_eager = 0;  // cg_test_stream_eager: launch a group whenever a lane is idle
 
 }  // namespace cgrt
 
@@ -185,16 +219,16 @@ int launch_open(cg_stream *h) {
     h->open = Group();
     const size_t n = g.desc.size();
     const size_t nd = n * sizeof(cg_desc);
-    if ((rc = l.stage.ensure(nd + n * 8 + 16))) return rc;
+    if ((rc = l.ensure_stage(nd + n * 8 + 16))) return rc;
     uint8_t *stg = l.stage.as<uint8_t>();
     memcpy(stg, g.desc.data(), nd);  // the kernels read lengths here and chunk bytes at arena + abs
     memcpy(stg + nd, g.abs.data(), n * 8);
     *reinterpret_cast<uint64_t *>(stg + nd + n * 8) = n;
     *reinterpret_cast<uint32_t *>(stg + nd + n * 8 + 8) = 0;
-    if ((rc = l.desc.ensure(nd + 64, "stream descriptors"))) return rc;
-    if ((rc = l.abs.ensure(n * 8 + 64, "stream offsets"))) return rc;
-    if ((rc = l.total.ensure(64, "stream total"))) return rc;
-    if ((rc = l.err.ensure(64, "stream err"))) return rc;
+    if ((rc = l.ensure(l.desc, nd + 64, "stream descriptors"))) return rc;
+    if ((rc = l.ensure(l.abs, n * 8 + 64, "stream offsets"))) return rc;
+    if ((rc = l.ensure(l.total, 64, "stream total"))) return rc;
+    if ((rc = l.ensure(l.err, 64, "stream err"))) return rc;
     // the chunk bytes were written (H2D, tail moves) on the boundary stream
     HIP_TRY(hipEventRecord(h->ev_bytes, h->ws->stream));
     HIP_TRY(hipStreamWaitEvent(l.st, h->ev_bytes, 0));
@@ -206,16 +240,16 @@ int launch_open(cg_stream *h) {
     const uint8_t *base = g.base;
     const uint64_t *d_total = l.total.as<uint64_t>();
     if (h->algo == CG_SHA256) {
-        if ((rc = l.order.ensure(cg::sha256_order_tmp_elems(n) * 4, "order"))) return rc;
+        if ((rc = l.ensure(l.order, cg::sha256_order_tmp_elems(n) * 4, "order"))) return rc;
         cg::launch_sha256(base, l.abs.as<uint64_t>(), l.desc.p, d_total, n, n, h->o.max, l.order.as<uint32_t>(), hb,
                           sizeof(cg_desc), l.err.as<uint32_t>(), l.st);
     } else {
         const uint64_t gb = cg::blake3_group_bound(g.bytes, n);
-        if ((rc = l.b3_gcount.ensure((n + 1) * 4, "b3_gcount"))) return rc;
-        if ((rc = l.b3_gbase.ensure((n + 1) * 8, "b3_gbase"))) return rc;
-        if ((rc = l.b3_gcv.ensure(cg::blake3_cv_bytes(g.bytes, n, true), "b3_gcv"))) return rc;
-        if ((rc = l.b3_gmap.ensure((gb + 1) * 4, "b3_gmap"))) return rc;
-        if ((rc = l.scan_tmp.ensure(cg::exclusive_scan_tmp_elems(n) * 8 + 64, "scan_tmp"))) return rc;
+        if ((rc = l.ensure(l.b3_gcount, (n + 1) * 4, "b3_gcount"))) return rc;
+        if ((rc = l.ensure(l.b3_gbase, (n + 1) * 8, "b3_gbase"))) return rc;
+        if ((rc = l.ensure(l.b3_gcv, cg::blake3_cv_bytes(g.bytes, n, true), "b3_gcv"))) return rc;
+        if ((rc = l.ensure(l.b3_gmap, (gb + 1) * 4, "b3_gmap"))) return rc;
+        if ((rc = l.ensure(l.scan_tmp, cg::exclusive_scan_tmp_elems(n) * 8 + 64, "scan_tmp"))) return rc;
         cg::launch_blake3(base, l.abs.as<uint64_t>(), l.desc.p, d_total, n, g.bytes, hb, sizeof(cg_desc),
                           l.b3_gmap.as<uint32_t>(), l.b3_gbase.as<uint64_t>(), l.b3_gcount.as<uint32_t>(),
                           l.scan_tmp.as<uint64_t>(), l.b3_gcv.as<uint32_t>(), true, l.st);
@@ -324,6 +358,15 @@ int stream_drain(cg_stream *h, uint64_t len, bool eof) {
     h->position += consumed;
     h->tail = rest;
     if (h->open.bytes >= h->group_bytes) return launch_open(h);
+    if (g_stream_eager && !h->open.desc.empty()) {  // launch now if a lane is idle
+        bool idle = h->lanes.size() < h->max_lanes;
+        for (const Lane &l : h->lanes) idle = idle || !l.busy;
+        if (!idle && !h->inflight.empty() && hipEventQuery(h->lanes[h->inflight.front().lane].done) == hipSuccess) {
+            if ((rc = complete_oldest(h))) return rc;
+            idle = true;
+        }
+        if (idle) return launch_open(h);
+    }
     return CG_OK;
 }
 
@@ -348,20 +391,31 @@ cg_stream *cg_stream_new(uint64_t min_size, uint64_t avg_size, uint64_t max_size
     h->o = o;
     h->algo = algo;
     h->device = dev;
-    // slot = the largest retained tail (< max) + one slice.  Digest lanes: up to one per
-    // hardware queue left beside the workspace stream's (GPU_MAX_HW_QUEUES, HIP's
-    // default 4; streams sharing a queue serialise), 3..8; groups of ~1/(lanes + 1) of
-    // the full arena, so every lane can hold one while the next fills.  The arena and
-    // the lanes themselves are allocated as the stream needs them (see the file header).
+    // slot = the largest retained tail (< max) + one slice.  Digest lanes: one per
+    // hardware queue left beside the workspace stream's and the null stream's
+    // (GPU_MAX_HW_QUEUES, HIP's default 4; streams sharing a queue serialise, and a lane
+    // on the workspace stream's queue would hold every boundary pass behind a 70 ms
+    // chain), 2..8; groups of ~1/(lanes + 1) of the full arena, so every lane can hold
+    // one while the next fills.  The arena and the lanes themselves are allocated as the
+    // stream needs them (see the file header).
     const uint64_t slice = std::max<uint64_t>(slice_bytes ? slice_bytes : 8ull << 20, 4096);
     h->slot_bytes = (o.max + slice + 256 + 255) & ~255ull;
-    const uint64_t budget = inflight_bytes ? inflight_bytes : 512ull << 20;
+    const uint64_t budget = inflight_bytes ? inflight_bytes : 2048ull << 20;
     h->max_slots = std::max<uint64_t>(budget / h->slot_bytes, 4);
     int queues = 4;
     if (const char *q = std::getenv("GPU_MAX_HW_QUEUES")) queues = std::atoi(q) > 0 ? std::atoi(q) : 4;
-    h->max_lanes = (size_t)std::min(std::max(queues - 1, 3), 8);
+    h->max_lanes = (size_t)std::min(std::max(queues - 2, 2), 8);
+    if (g_stream_max_lanes) h->max_lanes = g_stream_max_lanes;
     h->lanes.reserve(h->max_lanes);
-    h->group_bytes = std::max<uint64_t>(h->max_slots * h->slot_bytes / (uint64_t)(h->max_lanes + 1), slice);
+    // A group's SHA-256 launch takes one CU per 8 chunks (quad workgroups, padded to a CU
+    // each while the grid fits the chip), so the groups of all lanes together stay within
+    // the 256 CUs: at most 2048 / lanes chunks of the expected min + avg bytes.  Larger
+    // groups queue workgroups behind other lanes' 70 ms chains (8 lanes,
+    // 455 MiB groups: 4.3 GiB/s; 256 MiB: 9+).
+    const uint64_t group_cap = g_stream_group_cap ? g_stream_group_cap
+                                                  : (2048 / (uint64_t)h->max_lanes) * (o.min + o.avg);
+    h->group_bytes = std::max<uint64_t>(
+        std::min<uint64_t>(h->max_slots * h->slot_bytes / (uint64_t)(h->max_lanes + 1), group_cap), slice);
     if (!(rc = acquire(&h->ws))) {
         const hipError_t e = hipEventCreateWithFlags(&h->ev_bytes, hipEventDisableTiming);
         if (e != hipSuccess) rc = hip_fail(e, "hipEventCreate");
@@ -392,9 +446,27 @@ int check_poisoned(const cg_stream *h) {
     return fail_detail(h->poisoned, "stream failed earlier and cannot continue: " + h->poison_msg, h->poison_detail);
 }
 
+// Size the workspace for the largest boundary pass (a full slot) before any digest is in
+// flight: a workspace buffer that grew later would hipFree, which waits for the whole
+// device.  The pass reads the fresh arena's (uninitialised) first slot; its cuts are
+// discarded.
+int prime_workspace(cg_stream *h) {
+    int rc;
+    Workspace *ws = h->ws;
+    const uint64_t len = h->slot_bytes - 256;
+    const uint64_t cap = capacity_of(len, h->o.min);
+    if ((rc = ws->out.ensure((cap + 1) * sizeof(cg_desc), "descriptors"))) return rc;
+    uint64_t offs[2] = {0, len}, first[2] = {0, 0};
+    return run_batch(ws, h->arena.p, offs, 1, h->o, h->algo, ws->out.as<cg_desc>(), cap, first, ws->stream, nullptr,
+                     nullptr, /*digest=*/false);
+}
+
 int stream_push(cg_stream *h, const uint8_t *data, uint64_t len) {
     int rc;
-    if (len && !h->arena.p && (rc = h->arena.alloc(std::min<uint64_t>(2, h->max_slots), h->slot_bytes))) return rc;
+    if (len && !h->arena.p) {
+        if ((rc = h->arena.alloc(std::min<uint64_t>(2, h->max_slots), h->slot_bytes))) return rc;
+        if ((rc = prime_workspace(h))) return rc;
+    }
     while (len) {  // a slice larger than a slot goes in slot-sized pieces (chunks do not depend on slicing)
         const uint64_t room = h->slot_bytes - 256 - h->tail;
         const uint64_t take = std::min(len, room);
@@ -479,5 +551,22 @@ uint64_t cg_stream_pending(const cg_stream *h) {
 uint64_t cg_stream_bytes_consumed(const cg_stream *h) { return h ? h->pushed : 0; }
 
 void cg_stream_free(cg_stream *h) { delete h; }
+
+// test hooks: stream shape for streams created afterwards; return the previous value
+uint64_t cg_test_stream_group_cap(uint64_t v) {
+    const uint64_t old = g_stream_group_cap;
+    g_stream_group_cap = v;
+    return old;
+}
+uint32_t cg_test_stream_eager(uint32_t v) {
+    const uint32_t old = g_stream_eager;
+    g_stream_eager = v;
+    return old;
+}
+uint32_t cg_test_stream_max_lanes(uint32_t v) {
+    const uint32_t old = g_stream_max_lanes;
+    g_stream_max_lanes = v;
+    return old;
+}
 
 }  // extern "C"

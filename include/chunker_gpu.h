@@ -114,13 +114,15 @@ void cg_push_free(cg_push *h);
  * :579-584), but the chunks' digests run asynchronously, grouped over several slices;
  * cg_stream_take returns finished chunks strictly in stream order (offsets are stream
  * offsets), with exactly the (offset, length, hash) ChunkStream / PushChunker /
- * ChunkStreamAsync yields.  Device memory is bounded by `inflight_bytes` (0 = 512 MiB):
+ * ChunkStreamAsync yields.  Device memory is bounded by `inflight_bytes` (0 = 2 GiB):
  * an arena of slots of max_size + slice_bytes (0 = 8 MiB, the reference's read size,
  * :713-716) bytes, each reused only after the digests reading it completed.  The arena
  * starts at two slots at the first push and grows to that budget only when no slot is
  * free (a short stream holds two slots); at the budget a push waits for the oldest
  * digests.  Digests run on up to one HIP stream per hardware queue beside the call's
- * own (GPU_MAX_HW_QUEUES - 1, 3..8, read at cg_stream_new), created as they are needed.
+ * own and the null stream's (GPU_MAX_HW_QUEUES - 2, 2..8, read at cg_stream_new),
+ * created as they are needed, each on groups of at most 2048 / lanes chunks' expected
+ * bytes (so all lanes' SHA-256 workgroups fit the chip at once).
  * push returns once its bytes are copied: the caller may reuse `data` right away.  take
  * with wait = 0 returns what has completed; wait != 0 blocks until at least one chunk is
  * ready or nothing is pending.  push after finish -> CG_E_INVALID_OPTIONS.  The first

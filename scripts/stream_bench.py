@@ -14,11 +14,13 @@ Every GPU variant is checked chunk for chunk against the eager result."""
 import os
 os.environ.setdefault("CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR", "1")  # placeholder GEAR: see tables/README.md
 os.environ.pop("CHUNKER_READ_SLICE_CAP_BYTES", None)  # the reference's default sizing
-os.environ["GPU_MAX_HW_QUEUES"] = "16"  # as bench.py; before HIP initialises
+import sys  # noqa: E402
+
+# 16 hardware queues as bench.py, or --hw-queues N; before HIP initialises
+os.environ["GPU_MAX_HW_QUEUES"] = sys.argv[sys.argv.index("--hw-queues") + 1] if "--hw-queues" in sys.argv else "16"
 import ctypes  # noqa: E402
 import io  # noqa: E402
 import json  # noqa: E402
-import sys  # noqa: E402
 import time  # noqa: E402
 
 import numpy as np  # noqa: E402
@@ -43,7 +45,7 @@ def key(chunks):
     return [(c.offset, c.length, c.hash) for c in chunks]
 
 
-for inflight in (256 << 20, 512 << 20, 1 << 30):
+for inflight in (512 << 20, 1 << 30, 2 << 30):
     os.environ["CHUNKER_AMD_STREAM_INFLIGHT_BYTES"] = str(inflight)
     list(ca.ChunkStream(io.BytesIO(raw[: 64 << 20])))  # warm (allocations)
     t0 = time.perf_counter()
@@ -53,7 +55,7 @@ for inflight in (256 << 20, 512 << 20, 1 << 30):
     res[f"ChunkStream_inflight_{inflight >> 20}MiB"] = {"GiB_per_s": round(N / dt / 2**30, 3), "s": round(dt, 3)}
     del chunks
 
-for inflight in (256 << 20, 512 << 20, 1 << 30):
+for inflight in (512 << 20, 1 << 30, 2 << 30):
     st = ctypes.c_int(0)
     h = lib.cg_stream_new(256 << 10, 1 << 20, 4 << 20, 1, SL, inflight, ctypes.byref(st))
     out = np.zeros(8192, DESC_DTYPE)

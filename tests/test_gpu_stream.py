@@ -203,7 +203,7 @@ def test_stream_failed_arena_allocation_poisons_handle(ca):
 
 
 def test_short_stream_takes_little_device_memory(ca, O):
-    """a 1 KB stream no longer reserves the whole in-flight budget (512 MiB by
+    """a 1 KB stream no longer reserves the whole in-flight budget (2 GiB by
     default) -- its arena is two slots -- and a long stream still grows to the budget
     and stays exact."""
     import torch
@@ -219,3 +219,25 @@ def test_short_stream_takes_little_device_memory(ca, O):
     data = rand_bytes(40_000_000, 9)
     got = list(ca.ChunkStream(io.BytesIO(data), *P))
     assert triples(got) == oracle_triples(O, data, P, SHA)
+
+
+@pytest.mark.parametrize("algo", [SHA, B3], ids=["sha256", "blake3"])
+@pytest.mark.parametrize("shape", [(0, 1, 0), (1, 2, 0), (1, 0, 1), (0, 0, 0)],
+                         ids=["one-lane", "two-lanes-small-groups", "eager", "built-in"])
+def test_stream_shapes_match_eager(ca, O, monkeypatch, algo, shape):
+    """The stream handle's pipeline shape (group size cap, digest lanes, launching a group
+    whenever a lane is idle; test hooks) changes only timing: with a 24 MiB budget the
+    arena grows, slots are reused and lanes wait for each other, and the chunks stay the
+    eager sequence."""
+    small_groups, lanes, eager = shape
+    monkeypatch.setenv("CHUNKER_AMD_STREAM_INFLIGHT_BYTES", str(24 << 20))
+    data = rand_bytes(40_000_003, 17 + algo)
+    old = (ca.lib.cg_test_stream_group_cap(1 if small_groups else 0), ca.lib.cg_test_stream_max_lanes(lanes),
+           ca.lib.cg_test_stream_eager(eager))
+    try:
+        got = list(ca.ChunkStream(io.BytesIO(data), *P, hash=algo))
+    finally:
+        ca.lib.cg_test_stream_group_cap(old[0])
+        ca.lib.cg_test_stream_max_lanes(old[1])
+        ca.lib.cg_test_stream_eager(old[2])
+    assert triples(got) == oracle_triples(O, data, P, algo)
