@@ -511,19 +511,22 @@ __global__ __launch_bounds__(B3_FOLD_T) void k_b3_fold(const DescRaw *__restrict
         s_cnt[t] = c0 > 1 ? (c0 + 1) >> 1 : c0;
     }
     __syncthreads();
-    // levels 2..6 in LDS: (32 >> (L - 1)) parent slots per group
+    // levels 2..6 in LDS: (32 >> (L - 1)) parent slots per group.  (Rotating which of the 4
+    // waves are live at levels 3-6 by the block index, so that the blocks sharing a CU would
+    // use different SIMDs, measured 48.3 against 47.0 us per config-3 batch: not the limit.)
+    const uint32_t tr = t;
 #pragma unroll 1
     for (uint32_t lvl = 2; lvl <= 6; ++lvl) {
         const uint32_t per = 64u >> lvl;
         const uint32_t slots = B3_FOLD_G * per;
 #pragma unroll 1
         for (uint32_t base = 0; base < slots; base += B3_FOLD_T) {
-            const uint32_t sl = base + t, gl = (sl / per) % B3_FOLD_G, j = sl % per;
+            const uint32_t sl = base + tr, gl = (sl / per) % B3_FOLD_G, j = sl % per;
             const uint32_t cnt = sl < slots ? s_cnt[gl] : 0u;
             const bool pair = j < cnt / 2, carry = (cnt & 1u) && j == cnt / 2 && cnt > 1;
             uint32_t l[8], p[8];
             // waves wholly past the level's slots skip the compression (uniform per wave)
-            const bool wave_live = base + (t & ~63u) < slots;
+            const bool wave_live = base + (tr & ~63u) < slots;
             if (wave_live) {
                 uint32_t r[8];
 #pragma unroll
@@ -579,7 +582,7 @@ __global__ __launch_bounds__(64) void k_b3_top(const DescRaw *__restrict__ desc,
         if (lane < count)
 #pragma unroll
             for (int i = 0; i < 8; ++i) cv[i] = gcv[(g0 + lane) * 8 + i];
-        b3_wave_fold(cv, count, true, lane);
+        b3_wave_fold<true>(cv, count, true, lane);  // full exec mask: the wave is alone on its SIMD
         if (lane == 0) store_digest(hash_base + c * stride, cv);
         return;
     }
@@ -617,7 +620,7 @@ __global__ __launch_bounds__(64) void k_b3_top(const DescRaw *__restrict__ desc,
     if (lane < count)
 #pragma unroll
         for (int i = 0; i < 8; ++i) cv[i] = s_cv[lane][i];
-    b3_wave_fold(cv, count, true, lane);
+    b3_wave_fold<true>(cv, count, true, lane);
     if (lane == 0) store_digest(hash_base + c * stride, cv);
 }
 
