@@ -42,8 +42,9 @@ class parts_policy:
 
 # ragged NARs: most lengths multiples of 16 (aligned cut points), some not (skipped
 # cut points), empties, NARs below min and one spanning several max-size chunks
-LENS = [0, 160, 1_048_576, 7, 1_000_000, 2_000_016, 0, 333_333, 65_536, 4_194_320, 5, 1_500_000, 96, 3_000_000,
-        1_048_577, 2_097_152]
+# (odd lengths come in pairs that restore the alignment)
+LENS = [0, 160, 1_048_576, 7, 9, 1_000_000, 2_000_016, 0, 333_333, 333_339, 65_536, 4_194_320, 5, 11, 1_500_000, 96,
+        3_000_000, 1_048_577, 15, 2_097_152]
 
 
 @pytest.mark.parametrize("algo", [SHA, B3], ids=["sha256", "blake3"])
@@ -119,7 +120,8 @@ def test_parts_by_size_device_blake3(ca, O):
 
     sizes = np.full(80, 4 << 20, np.uint64)
     sizes[5] += 16
-    sizes[40] -= 8  # cut points near the targets move to the next aligned NAR start
+    sizes[39] -= 8  # NAR 40 starts unaligned: the middle cut point moves to NAR 41
+    sizes[40] += 8
     d, offs = synth_nars_device(sizes, first_index=11)
     cap = ca.chunking.batch_capacity(offs, D[0])
     stream = torch.cuda.current_stream().cuda_stream
