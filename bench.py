@@ -78,6 +78,9 @@ def parse_args():
     ap.add_argument("--parts", type=int, default=0, choices=range(0, 9), metavar="0..8",
                     help="batch parts policy for the timed steps (cg_set_batch_parts): 0 = the library's "
                          "default (BLAKE3 batches >= 256 MiB in 4 parts), 1 = never split, k = k parts")
+    ap.add_argument("--dist-force", action="store_true",
+                    help="run the N > 1 code (process group, gather to rank 0, rank-0 check) even at one rank: "
+                         "rehearses the RCCL path on a one-GPU box")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1: nccl = RCCL over xGMI, one GPU per rank (the product); gloo = host-copy "
                          "gather, ranks may share a GPU (rehearses the N > 1 path on a one-GPU box)")
@@ -97,7 +100,7 @@ def launch_ranks(n: int) -> int:
 
 def main():
     args = parse_args()
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+    if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.dist_force):
         sys.exit(launch_ranks(args.gpus))
     # The installed GEAR table is the labelled placeholder (tables/README.md) and the
     # engine refuses to chunk with it unless opted in; the JSON says which table ran.
@@ -117,10 +120,11 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     nccl = args.dist_backend == "nccl"
-    if world > 1 and nccl:
+    multi = world > 1 or args.dist_force
+    if multi and nccl:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    elif world > 1:
+    elif multi:
         # gloo rehearsal: ranks beyond the box's GPU count share them (RCCL would refuse
         # two ranks on one GPU); the gather runs on host copies of the descriptors.
         torch.cuda.set_device(local % torch.cuda.device_count())
@@ -150,7 +154,7 @@ def main():
     def step():
         first = ca.chunk_batch_device(d_data.data_ptr(), offs, d_out.data_ptr(), cap, *params, hash=algo,
                                       stream=sptr)
-        if world > 1:  # descriptors + NAR index to rank 0 over RCCL (the path's only exchange)
+        if multi:  # descriptors + NAR index to rank 0 over RCCL (the path's only exchange)
             mine_d = d_out if nccl else d_out[: int(first[-1]) * 48].cpu()
             gathered[0] = gather_batch(mine_d, first)
         return first
@@ -168,7 +172,7 @@ def main():
     stage = np.zeros((max(args.steps, 1), 5))
     buf = (np.ctypeslib.ctypes.c_double * 5)()
     torch.cuda.synchronize()
-    if world > 1:
+    if multi:
         dist.barrier()
     t0 = time.perf_counter()
     for k in range(args.steps):
@@ -176,7 +180,7 @@ def main():
         ca.lib.cg_last_stage_times(buf, 5)
         stage[k] = list(buf)
     torch.cuda.synchronize()
-    if world > 1:
+    if multi:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     parts = int(ca.lib.cg_last_batch_parts())
@@ -191,7 +195,7 @@ def main():
         prof[k] = list(buf)
     ca.lib.cg_set_profiling(0)
     ca.lib.cg_set_batch_parts(0)
-    if world > 1:
+    if multi:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if nccl else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -205,7 +209,7 @@ def main():
     descs = d_out[: n_chunks * 48].cpu().numpy().view(ca.DESC_DTYPE)
     check_gathered_batch(descs, first, sizes)
     gather_check = None
-    if world > 1 and rank == 0:
+    if multi and rank == 0:
         g_desc, g_first = gathered[0]
         g_np = g_desc.cpu().numpy().view(ca.DESC_DTYPE)
         check_gathered_batch(g_np, g_first, np.full(n_per * world, nar_bytes, np.uint64))
@@ -276,7 +280,7 @@ def main():
             "data": "synthetic (xorshift64 NAR payloads)" if not args.zeros else "synthetic (all-zero NAR payloads)",
             "config": {"workload": desc, "nars_per_gpu": len(mine), "nar_bytes": nar_bytes,
                        "params": list(params), "parallelism": f"nar-shard x{world}",
-                       **({"dist_backend": args.dist_backend} if world > 1 else {})},
+                       **({"dist_backend": args.dist_backend} if multi else {})},
             "gear_table": gear,
             "chunks": n_chunks,
             "batch_parts": parts,
@@ -292,7 +296,7 @@ def main():
                                 f"{min(world, torch.cuda.device_count())} GPU(s), host-copy gather; "
                                 "not a scaling measurement")
         print(json.dumps(line))
-    if world > 1:
+    if multi:
         dist.destroy_process_group()
 
 
