@@ -70,12 +70,12 @@ def test_parts_flat_index_equals_whole_batch(ca, algo):
     offs = np.zeros(len(lens) + 1, np.uint64)
     np.cumsum(lens, out=offs[1:])
     with parts_policy(ca, 1):
-        ref, ref_first = ca.chunk_batch_flat(flat, offs, 1024, 6000, 16384, hash=algo)
+        ref, ref_first = ca.chunking.chunk_batch_flat(flat, offs, 1024, 6000, 16384, hash=algo)
         ref = ref.copy()
         assert ca.lib.cg_last_batch_parts() == 1
     for k in (2, 5, 8):
         with parts_policy(ca, k):
-            got, first = ca.chunk_batch_flat(flat, offs, 1024, 6000, 16384, hash=algo)
+            got, first = ca.chunking.chunk_batch_flat(flat, offs, 1024, 6000, 16384, hash=algo)
             assert ca.lib.cg_last_batch_parts() == k
         assert np.array_equal(first, ref_first), k
         assert np.array_equal(got.view(np.uint8), ref.view(np.uint8)), k
