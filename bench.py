@@ -75,9 +75,6 @@ def parse_args():
     ap.add_argument("--e2e", default="1,8,16", help="K values of the host-to-host in-flight measurement ('' = skip)")
     ap.add_argument("--hw-queues", type=int, default=16, choices=range(0, 33), metavar="0..32",
                     help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's)")
-    ap.add_argument("--parts", type=int, default=0, choices=range(0, 9), metavar="0..8",
-                    help="batch parts policy for the timed steps (cg_set_batch_parts): 0 = the library's "
-                         "default (BLAKE3 batches >= 256 MiB in 4 parts), 1 = never split, k = k parts")
     ap.add_argument("--dist-force", action="store_true",
                     help="run the N > 1 code (process group, gather to rank 0, rank-0 check) even at one rank: "
                          "rehearses the RCCL path on a one-GPU box")
@@ -159,7 +156,6 @@ def main():
             gathered[0] = gather_batch(mine_d, first)
         return first
 
-    ca.lib.cg_set_batch_parts(args.parts)
     for _ in range(args.warmup):
         first = step()
     # Digest-stage device time: the two HIP events the library records around the digest
@@ -183,10 +179,6 @@ def main():
     if multi:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    parts = int(ca.lib.cg_last_batch_parts())
-    # the per-stage breakdown comes from the unsplit pipeline (a split batch's stages
-    # overlap, so only its digest-stream span is timed)
-    ca.lib.cg_set_batch_parts(1)
     ca.lib.cg_set_profiling(1)
     prof = np.zeros((PROFILE_STEPS, 5))
     for k in range(PROFILE_STEPS):
@@ -194,7 +186,6 @@ def main():
         ca.lib.cg_last_stage_times(buf, 5)
         prof[k] = list(buf)
     ca.lib.cg_set_profiling(0)
-    ca.lib.cg_set_batch_parts(0)
     if multi:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if nccl else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -231,11 +222,8 @@ def main():
         "frac": round(total_bytes / (dig_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
         "traffic": None,
         "note": "digest stage: algorithmic bytes = every NAR byte once, / mean digest-stage duration over the "
-                "timed steps (HIP events around the digest only"
-                + (f"; the batch ran as {parts} parts, so the digest stage is the digest stream's span from the end "
-                   "of part 0's boundary stages to the merged batch, overlapping the later parts' scans"
-                   if parts > 1 else "")
-                + f"); scan stage (scan_kernel) from {PROFILE_STEPS} untimed unsplit steps with every stage timed",
+                "timed steps (HIP events around the digest only); scan stage (scan_kernel) from "
+                f"{PROFILE_STEPS} untimed steps with every stage timed",
         "scan_kernel": {"kernel": scan_kernel_name(ca, params[1]),
                         "achieved": round(total_bytes / (scan_ms * 1e-3) / 1e9, 2),
                         "frac": round(total_bytes / (scan_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -283,7 +271,6 @@ def main():
                        **({"dist_backend": args.dist_backend} if multi else {})},
             "gear_table": gear,
             "chunks": n_chunks,
-            "batch_parts": parts,
             "stages_ms": stages_ms,
             "roofline": roofline,
             "cpu_baseline": cpu,

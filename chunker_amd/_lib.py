@@ -43,7 +43,7 @@ EXPORTS = (
     "cg_selftest", "cg_tables_verified", "cg_set_profiling", "cg_last_stage_times", "cg_synth_nars", "cg_hash",
     "cg_cas_ids_device", "cg_cas_id", "cg_node_put_batch_device", "cg_node_put", "cg_stream_new", "cg_stream_push",
     "cg_stream_finish", "cg_stream_take", "cg_stream_pending", "cg_stream_bytes_consumed", "cg_stream_free",
-    "cg_last_sha_tiers", "cg_set_batch_parts", "cg_last_batch_parts",
+    "cg_last_sha_tiers",
 )
 # test hooks the product library exports beyond the header (tier caps, spin-guard limit)
 TEST_HOOKS = ("cg_test_sha_quad_max", "cg_test_sha_split_max", "cg_test_sha_spin_limit", "cg_test_cas_pair_max",
@@ -163,10 +163,6 @@ def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
     L.cg_last_stage_times.restype = sz
     L.cg_last_sha_tiers.argtypes = [p]
     L.cg_last_sha_tiers.restype = i
-    L.cg_set_batch_parts.argtypes = [ctypes.c_uint32]
-    L.cg_set_batch_parts.restype = ctypes.c_uint32
-    L.cg_last_batch_parts.argtypes = []
-    L.cg_last_batch_parts.restype = ctypes.c_uint32
     L.cg_synth_nars.argtypes = [p, p, sz, i, u64]
     L.cg_synth_nars.restype = None
     return L

@@ -726,7 +726,7 @@ size_t blake3_cv_bytes(uint64_t total_bytes, uint64_t max_chunks, bool with_lcv)
 void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
                    uint64_t max_chunks, uint64_t total_bytes, uint8_t *d_hash_base, size_t hash_stride,
                    uint32_t *d_gmap, uint64_t *d_group_base, uint32_t *d_gcount_u32, uint64_t *d_scan_tmp,
-                   uint32_t *d_gcv, bool with_lcv, hipStream_t st, hipStream_t st_leaves, hipEvent_t ev_plan) {
+                   uint32_t *d_gcv, bool with_lcv, hipStream_t st) {
     if (max_chunks == 0) return;
     const DescRaw *desc = (const DescRaw *)d_desc;
     const uint32_t cblocks = (uint32_t)((max_chunks + 255) / 256);
@@ -764,11 +764,6 @@ void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
         hipLaunchKernelGGL(count, dim3(cblocks), dim3(256), 0, st, desc, d_total, max_chunks, d_gcount_u32);
         launch_exclusive_scan_u32(d_gcount_u32, d_group_base, max_chunks, 0, d_scan_tmp, st);
         hipLaunchKernelGGL(k_b3_map, dim3(cblocks), dim3(256), 0, st, d_group_base, d_total, max_chunks, d_gmap);
-    }
-    if (st_leaves) {  // the batch-parts pipeline: the plan stays with the boundary stages, the leaves go on
-        (void)hipEventRecord(ev_plan, st);
-        (void)hipStreamWaitEvent(st_leaves, ev_plan, 0);
-        st = st_leaves;
     }
     hipLaunchKernelGGL(groups,
                        dim3((uint32_t)((gbound + B3_WAVES - 1) / B3_WAVES)), dim3(64 * B3_WAVES), 0, st, d_data, d_abs,

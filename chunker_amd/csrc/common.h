@@ -119,26 +119,9 @@ void launch_manifest_spans(const uint64_t *d_first, uint64_t n_nars, uint64_t *d
 void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
                    uint64_t max_chunks, uint64_t total_bytes, uint8_t *d_hash_base, size_t hash_stride,
                    uint32_t *d_gmap, uint64_t *d_group_base, uint32_t *d_gcount_u32,
-                   uint64_t *d_scan_tmp, uint32_t *d_gcv, bool with_lcv, hipStream_t st,
-                   hipStream_t st_leaves = nullptr, hipEvent_t ev_plan = nullptr);
-// (st_leaves: the group map is built on st, then the leaf / fold kernels run on st_leaves
-// behind ev_plan -- the batch-parts pipeline of runtime.hip)
+                   uint64_t *d_scan_tmp, uint32_t *d_gcv, bool with_lcv, hipStream_t st);
 size_t blake3_group_bound(uint64_t total_bytes, uint64_t max_chunks);
 size_t blake3_cv_bytes(uint64_t total_bytes, uint64_t max_chunks, bool with_lcv);  // launch_blake3's d_gcv
-
-// A batch cut at NAR boundaries into parts, each run as a batch of its own (runtime.hip
-// run_parts); k_merge_parts joins them: descriptors of part p (device, desc[p]) behind the
-// earlier parts' in d_out, and the batch-wide NAR -> first-chunk index (n_nars + 1 entries).
-#define CG_MAX_PARTS 8
-struct PartsView {
-    const DescRaw *desc[CG_MAX_PARTS];
-    const uint64_t *first[CG_MAX_PARTS];  // part-local index, total at [n_nars[p]]
-    uint64_t n_nars[CG_MAX_PARTS];
-    uint64_t nar_base[CG_MAX_PARTS];  // batch index of the part's first NAR
-    uint32_t np;
-};
-void launch_merge_parts(const PartsView &v, uint64_t max_part_chunks, void *d_out, uint64_t out_cap,
-                        uint64_t *d_first, hipStream_t st);
 
 void launch_spans_to_desc(const uint64_t *d_off, const uint64_t *d_len, uint64_t n, uint64_t *d_abs, void *d_desc,
                           uint64_t *d_total, hipStream_t st);

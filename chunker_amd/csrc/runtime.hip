@@ -247,35 +247,25 @@ uint32_t seg_slots(const CdcParams &p) {
     return c;
 }
 
-// Launch side of the device pipeline for one batch (scan -> compact -> walk -> assemble
-// -> digest) on `st`; nothing here waits.  d_out receives descriptors; the digest of
-// descriptor g is written in place at d_out[g].hash.  With st_b set (the batch-parts
-// pipeline, run_parts) the digest kernels go to st_b behind ev_ab -- for BLAKE3 after the
-// group map, which stays on st with the boundary stages -- and no stage events are
-// recorded.
+// The whole device pipeline for one batch.  d_out receives descriptors; the
+// digest of descriptor g is written in place at d_out[g].hash.
 //
 // Node::put mode (crates/node/src/lib.rs:114-132) when d_chunk_ids is set: every
 // chunk's ContentId(Chunk, payload) -> d_chunk_ids[32 g], and NAR i's manifest id
-// ContentId(Level1Manifest, its chunk ids in order) -> the workspace's id buffer
-// (BatchLaunch::d_man).  The CAS stage forks onto ws->side_stream after descriptor
-// assembly; run_batch joins it.
-struct BatchLaunch {
-    uint64_t *s_first = nullptr;  // pinned staging of the NAR -> first-chunk index (n + 1)
-    uint8_t *d_man = nullptr;     // manifest ids (Node::put mode)
-    bool sha_armed = false;
-};
-
-static int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, size_t n_nars,
-                        const Opts &o, int algo, cg_desc *d_out, size_t out_cap, hipStream_t st,
-                        uint8_t *d_chunk_ids, bool digest, int pmode, hipStream_t st_b, hipEvent_t ev_ab,
-                        BatchLaunch *bl) {
+// ContentId(Level1Manifest, its chunk ids in order) -> h_manifest_ids[32 i].  The CAS
+// stage forks onto ws->side_stream after descriptor assembly and joins before return.
+int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, size_t n_nars, const Opts &o,
+              int algo, cg_desc *d_out, size_t out_cap, uint64_t *h_nar_first, hipStream_t st,
+              uint8_t *d_chunk_ids, uint8_t *h_manifest_ids, bool digest) {
     if (algo != CG_BLAKE3 && algo != CG_SHA256) return fail(CG_E_INVALID_OPTIONS, "unknown hash algorithm");
     if (((uintptr_t)d_data & 15u) != 0) return fail(CG_E_IO, "device input must be 16-byte aligned");
     int rc;
+    const uint64_t base0 = n_nars ? h_nar_off[0] : 0;
     const uint64_t total_len = n_nars ? h_nar_off[n_nars] : 0;
     for (size_t i = 0; i < n_nars; ++i)  // NAR i = [off[i], off[i+1]) must lie inside the batch
         if (h_nar_off[i + 1] < h_nar_off[i])
             return fail_bounds(h_nar_off[i + 1], h_nar_off[i], 0, "nar offsets must be non-decreasing");
+    (void)base0;
 
     // one table snapshot for the whole call: GEAR on the device and MASKS in P agree
     const std::shared_ptr<const Tables> tab = tables();
@@ -312,7 +302,6 @@ static int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_
     uint64_t *s_pfirst = s_first + (n_nars + 1);
     uint64_t *s_pbase = s_pfirst + (n_nars + 1);
     uint32_t *s_pnar = reinterpret_cast<uint32_t *>(s_pbase + np);
-    bl->s_first = s_first;
     memcpy(s_off, h_nar_off, (n_nars + 1) * sizeof(uint64_t));
     uint64_t total_cap = 0;
     for (size_t i = 0; i < n_nars; ++i) {
@@ -374,14 +363,13 @@ static int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_
         if ((rc = ws->b3_gbase.ensure((chunk_bound + 1) * 8, "b3_gbase"))) return rc;
         if ((rc = ws->b3_gcv.ensure(cg::blake3_cv_bytes(total_len, chunk_bound, true), "b3_gcv"))) return rc;
         if ((rc = ws->b3_gmap.ensure((cg::blake3_group_bound(total_len, chunk_bound) + 1) * 4, "b3_gmap"))) return rc;
-    } else if (digest) {
-        if ((rc = ws->order.ensure(cg::sha256_order_tmp_elems(chunk_bound) * 4, "order"))) return rc;
     }
 
     // A timing event between two kernels holds the second back by ~6 us (the event's
     // end-of-pipe timestamp), so mode 2 records only the two around the digest stage.
-    const bool prof = pmode != 0 && !st_b;
-    const bool prof_all = pmode == 1 && !st_b;
+    const int pmode = g_profiling.load();
+    const bool prof = pmode != 0;
+    const bool prof_all = pmode == 1;
     HIP_TRY(hipMemcpyAsync(ws->nar_off.p, s_off, 2 * (n_nars + 1) * 8, hipMemcpyHostToDevice, st));
     if (prof_all) HIP_TRY(hipEventRecord(ws->ev[EV_START], st));  // scan stage = the scan kernel alone
 
@@ -400,12 +388,13 @@ static int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_
                         ws->scan_tmp.as<uint64_t>(), st);
     if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_ASSEMBLE], st));
     const uint64_t *d_total = ws->nar_first.as<uint64_t>() + n_nars;
+    uint8_t *d_man = nullptr;
     if (d_chunk_ids) {
         if ((rc = ws->cas_order.ensure(cg::sha256_order_tmp_elems(chunk_bound) * 4, "cas_order"))) return rc;
         if ((rc = ws->ids.ensure((n_nars + 1) * 32, "manifest ids"))) return rc;
         if ((rc = ws->man_abs.ensure((n_nars + 1) * 8, "manifest spans"))) return rc;
         if ((rc = ws->man_desc.ensure((n_nars + 2) * sizeof(cg_desc), "manifest spans"))) return rc;
-        bl->d_man = ws->ids.as<uint8_t>();
+        d_man = ws->ids.as<uint8_t>();
         if ((rc = ws->ensure_side_stream())) return rc;
         hipStream_t side = ws->side_stream;
         HIP_TRY(hipEventRecord(ws->ev_fork, st));
@@ -417,172 +406,37 @@ static int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_
         cg::launch_manifest_spans(ws->nar_first.as<uint64_t>(), n_nars, ws->man_abs.as<uint64_t>(), ws->man_desc.p,
                                   d_man_total, side);
         cg::launch_cas_ids(d_chunk_ids, ws->man_abs.as<uint64_t>(), ws->man_desc.p, d_man_total, n_nars, nullptr,
-                           CG_KIND_LEVEL1_MANIFEST, bl->d_man, 32, side);
+                           CG_KIND_LEVEL1_MANIFEST, d_man, 32, side);
         HIP_TRY(hipEventRecord(ws->ev_cas, side));
         HIP_TRY(hipEventRecord(ws->ev_join, side));
     }
     uint8_t *hash_base = reinterpret_cast<uint8_t *>(d_out) + offsetof(cg_desc, hash);
+    bool sha_armed = false;
     if (!digest) {
         // boundaries only (push_drain digests the chunks that became final afterwards)
     } else if (algo == CG_SHA256) {
+        if ((rc = ws->order.ensure(cg::sha256_order_tmp_elems(chunk_bound) * 4, "order"))) return rc;
         // expected chunk count: FastCDC's mean chunk is about min + avg on random data
         const uint64_t expected = std::min<uint64_t>(chunk_bound, total_len / (o.min + o.avg) + n_nars);
-        hipStream_t sd = st;
-        if (st_b) {
-            HIP_TRY(hipEventRecord(ev_ab, st));
-            HIP_TRY(hipStreamWaitEvent(st_b, ev_ab, 0));
-            sd = st_b;
-        }
-        if ((rc = sha_err_arm(ws, sd))) return rc;
-        bl->sha_armed = true;
+        if ((rc = sha_err_arm(ws, st))) return rc;
+        sha_armed = true;
         cg::launch_sha256(d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, expected, o.max,
-                          ws->order.as<uint32_t>(), hash_base, sizeof(cg_desc), ws->sha_err.as<uint32_t>(), sd);
+                          ws->order.as<uint32_t>(), hash_base, sizeof(cg_desc), ws->sha_err.as<uint32_t>(), st);
     } else {
         cg::launch_blake3(d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, total_len, hash_base,
                           sizeof(cg_desc), ws->b3_gmap.as<uint32_t>(), ws->b3_gbase.as<uint64_t>(),
                           ws->b3_gcount.as<uint32_t>(), ws->scan_tmp.as<uint64_t>(), ws->b3_gcv.as<uint32_t>(), true,
-                          st, st_b, ev_ab);
+                          st);
     }
     if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_DIGEST], st));
-    return CG_OK;
-}
-
-// Batch parts.  A BLAKE3 digest is VALU-bound and the candidate scan HBM-bound, so a
-// batch cut at NAR boundaries into parts runs as a two-stage software pipeline: the
-// boundary stages (scan .. assembly + the BLAKE3 group map) of every part in order on the
-// caller's stream, the digests in order on a second stream, part p's digest overlapping
-// part p + 1's scan.  Each part is a batch of its own on a workspace of its own (its
-// buffers stay live until its digest is done); k_merge_parts places the parts'
-// descriptors and NAR index in the caller's arrays.  SHA-256 batches stay whole: their
-// digest stage is the longest chunk's chain, which no overlap shortens.
-thread_local uint32_t t_last_parts = 1;
-std::atomic<uint32_t> g_parts_override{0};  // cg_set_batch_parts: 0 = by size, 1 = never, k = k parts
-
-// Cut points (NAR indices, increasing, first 0 and last n_nars) for `want` parts of about
-// equal bytes; only NAR starts 16-B aligned in the device buffer qualify (each part's
-// device view must be).  Returns the number of parts (1 = no split).
-static uint32_t plan_parts(const uint64_t *off, size_t n_nars, uint32_t want, size_t *cut) {
-    cut[0] = 0;
-    uint32_t np = 0;
-    const uint64_t total = off[n_nars];
-    size_t i = 1;
-    for (uint32_t k = 1; k < want && i < n_nars; ++k) {
-        const uint64_t target = total / want * k;
-        while (i < n_nars && (off[i] < target || (off[i] & 15u))) ++i;
-        if (i >= n_nars) break;
-        if (off[i] > off[cut[np]]) cut[++np] = i;  // a part holds bytes
-        ++i;
-    }
-    cut[++np] = n_nars;
-    return np;
-}
-
-static uint32_t parts_wanted(int algo, bool digest, bool node_put, size_t n_nars, uint64_t total_len) {
-    const uint32_t ov = g_parts_override.load();
-    if (!digest || node_put || n_nars < 2) return 1;
-    if (ov) return std::min<uint32_t>(ov, CG_MAX_PARTS);
-    if (algo != CG_BLAKE3 || total_len < (256ull << 20)) return 1;
-    return 4;
-}
-
-static int run_parts(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, size_t n_nars,
-                     const Opts &o, int algo, cg_desc *d_out, size_t out_cap, uint64_t *h_nar_first, hipStream_t st,
-                     const size_t *cut, uint32_t np) {
-    int rc;
-    Workspace *w[CG_MAX_PARTS] = {ws};
-    WsGuard guards[CG_MAX_PARTS] = {};
-    for (uint32_t p = 1; p < np; ++p) {
-        if ((rc = acquire(&w[p]))) return rc;
-        guards[p].ws = w[p];
-    }
-    if ((rc = ws->ensure_side_stream())) return rc;
-    hipStream_t sb = ws->side_stream;
-    const int pmode = g_profiling.load();
-    cg::PartsView v{};
-    v.np = np;
-    uint64_t max_part_chunks = 0;
-    BatchLaunch bl[CG_MAX_PARTS];
-    std::vector<uint64_t> offs;
-    for (uint32_t p = 0; p < np; ++p) {
-        const size_t a = cut[p], b = cut[p + 1];
-        const uint64_t base = h_nar_off[a];
-        offs.assign(h_nar_off + a, h_nar_off + b + 1);
-        uint64_t cap = 0;
-        for (auto &x : offs) x -= base;
-        for (size_t i = a; i < b; ++i) cap += capacity_of(h_nar_off[i + 1] - h_nar_off[i], o.min);
-        if ((rc = w[p]->out.ensure((cap + 1) * sizeof(cg_desc), "descriptors"))) return rc;
-        // (every digest waits for its part's boundary stages on st, so for everything the
-        // caller queued on st before this call)
-        if ((rc = launch_batch(w[p], d_data + base, offs.data(), b - a, o, algo, w[p]->out.as<cg_desc>(), cap, st,
-                               nullptr, true, 0, sb, w[p]->ev_fork, &bl[p])))
-            return rc;
-        // digest stage = from the end of part 0's boundary stages (its digest may start) to the
-        // merged batch on the digest stream
-        if (pmode && p == 0) HIP_TRY(hipEventRecord(ws->ev[EV_ASSEMBLE], st));
-        v.desc[p] = reinterpret_cast<const DescRaw *>(w[p]->out.p);
-        v.first[p] = w[p]->nar_first.as<uint64_t>();
-        v.n_nars[p] = b - a;
-        v.nar_base[p] = a;
-        max_part_chunks = std::max<uint64_t>(max_part_chunks, cap);
-    }
-    if ((rc = ws->pfirst.ensure((n_nars + 1) * 8, "nar_first"))) return rc;
-    cg::launch_merge_parts(v, max_part_chunks, d_out, out_cap, ws->pfirst.as<uint64_t>(), sb);
-    if (pmode) HIP_TRY(hipEventRecord(ws->ev[EV_DIGEST], sb));
-    if ((rc = ws->pstage.ensure((n_nars + 1) * 8))) return rc;
-    uint64_t *s_first = ws->pstage.as<uint64_t>();
-    HIP_TRY(hipMemcpyAsync(s_first, ws->pfirst.p, (n_nars + 1) * 8, hipMemcpyDeviceToHost, sb));
-    for (uint32_t p = 0; p < np; ++p)
-        if (bl[p].sha_armed && (rc = sha_err_fetch(w[p], sb))) return rc;
-    HIP_TRY(hipGetLastError());
-    // the caller's stream continues behind the whole batch
-    HIP_TRY(hipEventRecord(ws->ev_cas, sb));
-    HIP_TRY(hipStreamWaitEvent(st, ws->ev_cas, 0));
-    HIP_TRY(hipStreamSynchronize(sb));
-    for (uint32_t p = 0; p < np; ++p)
-        if (bl[p].sha_armed && (rc = sha_err_check(w[p]))) return rc;
-    t_last_parts = np;
-    if (pmode) {
-        t_stage_ms.assign(EV_N - 1, std::nan(""));
-        float ms = 0;
-        HIP_TRY(hipEventElapsedTime(&ms, ws->ev[EV_ASSEMBLE], ws->ev[EV_DIGEST]));
-        t_stage_ms[EV_DIGEST - 1] = ms;
-    }
-    if (h_nar_first) memcpy(h_nar_first, s_first, (n_nars + 1) * 8);
-    if (s_first[n_nars] > out_cap) return fail(CG_E_CAPACITY, "descriptor output array too small");
-    return CG_OK;
-}
-
-// The whole device pipeline for one batch, waited for: launch, then the NAR index (and
-// the Node::put manifest ids) back to the host.
-int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, size_t n_nars, const Opts &o,
-              int algo, cg_desc *d_out, size_t out_cap, uint64_t *h_nar_first, hipStream_t st,
-              uint8_t *d_chunk_ids, uint8_t *h_manifest_ids, bool digest) {
-    int rc;
-    const uint64_t total_len = n_nars ? h_nar_off[n_nars] : 0;
-    const uint32_t want = parts_wanted(algo, digest, d_chunk_ids != nullptr, n_nars, total_len);
-    if (want > 1 && (algo == CG_BLAKE3 || algo == CG_SHA256) && ((uintptr_t)d_data & 15u) == 0) {
-        bool ordered = true;
-        for (size_t i = 0; i < n_nars && ordered; ++i) ordered = h_nar_off[i + 1] >= h_nar_off[i];
-        size_t cut[CG_MAX_PARTS + 1];
-        const uint32_t np = ordered ? plan_parts(h_nar_off, n_nars, want, cut) : 1;
-        if (np > 1) return run_parts(ws, d_data, h_nar_off, n_nars, o, algo, d_out, out_cap, h_nar_first, st, cut, np);
-    }
-    t_last_parts = 1;
-    const int pmode = g_profiling.load();
-    BatchLaunch bl;
-    if ((rc = launch_batch(ws, d_data, h_nar_off, n_nars, o, algo, d_out, out_cap, st, d_chunk_ids, digest, pmode,
-                           nullptr, nullptr, &bl)))
-        return rc;
-    const bool prof = pmode != 0, prof_all = pmode == 1;
-    uint64_t *s_first = bl.s_first;
     if (d_chunk_ids) HIP_TRY(hipStreamWaitEvent(st, ws->ev_join, 0));
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(s_first, ws->nar_first.p, (n_nars + 1) * 8, hipMemcpyDeviceToHost, st));
-    if (bl.d_man && h_manifest_ids)
-        HIP_TRY(hipMemcpyAsync(h_manifest_ids, bl.d_man, n_nars * 32, hipMemcpyDeviceToHost, st));
-    if (bl.sha_armed && (rc = sha_err_fetch(ws, st))) return rc;
+    if (d_man && h_manifest_ids)
+        HIP_TRY(hipMemcpyAsync(h_manifest_ids, d_man, n_nars * 32, hipMemcpyDeviceToHost, st));
+    if (sha_armed && (rc = sha_err_fetch(ws, st))) return rc;
     HIP_TRY(hipStreamSynchronize(st));
-    if (bl.sha_armed && (rc = sha_err_check(ws))) return rc;
+    if (sha_armed && (rc = sha_err_check(ws))) return rc;
     if (prof) {
         t_stage_ms.assign(EV_N - 1 + (d_chunk_ids ? 1 : 0), prof_all ? 0.0 : std::nan(""));
         for (int k = prof_all ? 1 : EV_DIGEST; k < EV_N; ++k) {
@@ -1206,12 +1060,6 @@ int cg_last_error_detail(uint64_t out[3]) {
 }
 
 void cg_set_profiling(int on) { g_profiling.store(on == 2 ? 2 : on ? 1 : 0); }
-
-uint32_t cg_set_batch_parts(uint32_t parts) {
-    return g_parts_override.exchange(std::min<uint32_t>(parts, CG_MAX_PARTS));
-}
-
-uint32_t cg_last_batch_parts(void) { return t_last_parts; }
 
 size_t cg_last_stage_times(double *ms, size_t n) {
     const size_t k = std::min(n, t_stage_ms.size());

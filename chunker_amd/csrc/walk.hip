@@ -464,36 +464,6 @@ void launch_assemble(const uint64_t *d_nar_off, const uint64_t *d_cap_base, cons
                        d_nar_first, n_nars, (DescRaw *)d_out, out_cap, d_chunk_abs);
 }
 
-// Batch parts (runtime.hip run_parts): part p's descriptors and NAR -> first-chunk index
-// were built as a batch of their own; one launch places them in the caller's array behind
-// the parts before it and writes the batch-wide index (first[n_nars] = the total).
-// blockIdx.y = part; each block sums the earlier parts' totals itself (<= CG_MAX_PARTS).
-__global__ __launch_bounds__(256) void k_merge_parts(PartsView v, DescRaw *__restrict__ out, uint64_t out_cap,
-                                                     uint64_t *__restrict__ first) {
-    const uint32_t p = blockIdx.y;
-    uint64_t base = 0;
-    for (uint32_t q = 0; q < p; ++q) base += v.first[q][v.n_nars[q]];
-    const uint64_t *pf = v.first[p];
-    const uint64_t n = v.n_nars[p], cnt = pf[n];
-    const uint64_t t0 = (uint64_t)blockIdx.x * 256 + threadIdx.x, stride = (uint64_t)gridDim.x * 256;
-    const uint4 *src = reinterpret_cast<const uint4 *>(v.desc[p]);
-    uint4 *dst = reinterpret_cast<uint4 *>(out);
-    for (uint64_t k = t0; k < cnt && base + k < out_cap; k += stride) {
-        dst[3 * (base + k)] = src[3 * k];
-        dst[3 * (base + k) + 1] = src[3 * k + 1];
-        dst[3 * (base + k) + 2] = src[3 * k + 2];
-    }
-    for (uint64_t i = t0; i < n; i += stride) first[v.nar_base[p] + i] = base + pf[i];
-    if (p + 1 == gridDim.y && t0 == 0) first[v.nar_base[p] + n] = base + cnt;
-}
-
-void launch_merge_parts(const PartsView &v, uint64_t max_part_chunks, void *d_out, uint64_t out_cap,
-                        uint64_t *d_first, hipStream_t st) {
-    const uint64_t blocks = std::min<uint64_t>((max_part_chunks + 255) / 256 + 1, 256);
-    hipLaunchKernelGGL(k_merge_parts, dim3((uint32_t)blocks, v.np), dim3(256), 0, st, v, (DescRaw *)d_out, out_cap,
-                       d_first);
-}
-
 // Digest-only entry: spans (offset,length) -> desc/abs arrays + total.
 __global__ void k_spans(const uint64_t *__restrict__ off, const uint64_t *__restrict__ len, uint64_t n,
                         uint64_t *__restrict__ abs, DescRaw *__restrict__ desc, uint64_t *__restrict__ total) {

@@ -230,16 +230,6 @@ int cg_tables_verified(void); /* 1 once the installed set passed cg_selftest */
 void cg_set_profiling(int on);
 size_t cg_last_stage_times(double *ms, size_t n);
 
-/* Batch parts (DESIGN.md §4 "Batch parts"): a BLAKE3 batch of >= 256 MiB over two or
- * more NARs runs as up to 4 parts cut at NAR boundaries (16-B aligned in the device
- * buffer), the boundary stages of part p + 1 overlapping the digest of part p on a second
- * stream; results are identical to the whole-batch run.  cg_set_batch_parts(k) sets the
- * process-wide policy -- 0 = by size (default), 1 = never split, k = 2..8 parts for every
- * digesting batch call of two or more NARs, SHA-256 included (tests, profiling) -- and
- * returns the previous one.  cg_last_batch_parts: parts of this thread's last batch call. */
-uint32_t cg_set_batch_parts(uint32_t parts);
-uint32_t cg_last_batch_parts(void);
-
 /* Shape of the last SHA-256 digest launch on this thread (K3 k_sha256 work units):
  * out = {quad workgroups (8 chunks, 8 lanes each), pair workgroups (32 chunks, 2 lanes
  * each), one-lane workgroups (64 chunks), LDS pad bytes (non-zero: one workgroup per

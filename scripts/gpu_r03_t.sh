@@ -1,5 +1,6 @@
 #!/bin/bash
 # Round 3 session T: batch parts (BLAKE3 scan/digest overlap) -- parity tests for the parts
+# (historical: the --parts option and the batch-parts path it measured were reverted after this session)
 # path, then config 3 at parts = 1 / 2 / 4 / 8 and the default, a kernel trace of the default, and
 # the RCCL gather path rehearsed at one rank (bench.py --dist-force).
 set -o pipefail
