@@ -11,7 +11,11 @@ from pathlib import Path
 
 import numpy as np
 
-LIB_PATH = Path(__file__).resolve().parent / "libchunker_amd.so"
+import os as _os
+
+# CHUNKER_AMD_LIB: an alternative build of the same ABI (A/B measurements of compile-time
+# variants, scripts/gpu_ab_*.sh); unset = the product library beside this file
+LIB_PATH = Path(_os.environ.get("CHUNKER_AMD_LIB") or Path(__file__).resolve().parent / "libchunker_amd.so")
 # diagnostics build (make -C chunker_amd/csrc diag): same ABI plus cg_diag_* kernels
 DIAG_LIB_PATH = Path(__file__).resolve().parent / "libchunker_amd_diag.so"
 ABI_VERSION = 2

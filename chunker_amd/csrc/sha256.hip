@@ -152,7 +152,10 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return v;
 }
 
-#define PC_RING 4u  // LDS schedule slots: the producer runs up to 4 blocks ahead
+#ifndef CG_PC_RING
+#define CG_PC_RING 4u
+#endif
+#define PC_RING CG_PC_RING  // LDS schedule slots: the producer runs up to PC_RING blocks ahead
 
 // Spin guard: no legitimate wait for a ring slot lasts more than a few blocks
 // (~10^4 clocks); after `limit` sleeps (2^26 by default, ~2 s) a wait gives up so a
@@ -881,7 +884,8 @@ void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
     // Latency-bound batches (no more workgroups than CUs): pad the LDS request past half
     // a CU's 160 KiB so no two workgroups share a CU, and a consumer wave never shares a
     // SIMD with another workgroup's wave (which costs it 20-90 % per round).
-    const size_t pad = nwg <= 256 ? 16384 : 0;
+    constexpr size_t ring_bytes = PC_RING * 64 * PC_ROW * 4;
+    const size_t pad = nwg <= 256 ? (ring_bytes < 81920 + 4096 ? 81920 + 4096 - ring_bytes : 0) : 0;
     t_sha_tiers[0] = nquad;
     t_sha_tiers[1] = npair;
     t_sha_tiers[2] = nwg - nquad - npair;
