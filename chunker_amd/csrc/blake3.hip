@@ -748,7 +748,7 @@ size_t blake3_cv_bytes(uint64_t total_bytes, uint64_t max_chunks, bool with_lcv)
 void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
                    uint64_t max_chunks, uint64_t total_bytes, uint8_t *d_hash_base, size_t hash_stride,
                    uint32_t *d_gmap, uint64_t *d_group_base, uint32_t *d_gcount_u32, uint64_t *d_scan_tmp,
-                   uint32_t *d_gcv, bool with_lcv, hipStream_t st) {
+                   uint32_t *d_gcv, bool with_lcv, hipStream_t st, bool plan_ready) {
     if (max_chunks == 0) return;
     const DescRaw *desc = (const DescRaw *)d_desc;
     const uint32_t cblocks = (uint32_t)((max_chunks + 255) / 256);
@@ -780,7 +780,9 @@ void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
     }
 #endif
     // (a forced scan path, cg_test_scan_path, takes the three-kernel form so tests reach it)
-    if (max_chunks <= B3_PLAN_MAX && g_scan_path == 0) {
+    if (plan_ready) {
+        // group_base / gmap came with the descriptor assembly (k_assemble_counts)
+    } else if (max_chunks <= B3_PLAN_MAX && g_scan_path == 0) {
         hipLaunchKernelGGL(plan, dim3(1), dim3(B3_PLAN_T), 0, st, desc, d_total, max_chunks, d_group_base, d_gmap);
     } else {
         hipLaunchKernelGGL(count, dim3(cblocks), dim3(256), 0, st, desc, d_total, max_chunks, d_gcount_u32);

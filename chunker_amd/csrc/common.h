@@ -79,16 +79,44 @@ struct WalkPiecesHost {
 // The walk verifies candidate-list walks afterwards (and can use piece lists) when
 // mask_s is sparse enough that a cut inside a chunk's 47-byte warm-up is rare.
 inline bool walk_is_speculative(const CdcParams &p) { return __builtin_popcountll(p.mask_s) >= 14; }
+// d_nar_ngroups (optional, BLAKE3 batches): each NAR's 64-leaf group count, for the
+// group map launch_assemble builds
 void launch_walk(const uint8_t *d_data, const uint64_t *d_gear, const uint64_t *d_entries, const uint64_t *d_eoff,
                  uint64_t nseg, const uint64_t *d_nar_off, const uint64_t *d_cap_base, uint64_t n_nars,
                  CdcParams p, uint64_t *d_wchunk, uint32_t *d_nar_nchunks, const WalkPiecesHost &pieces,
-                 hipStream_t st);
+                 hipStream_t st, uint32_t *d_nar_ngroups = nullptr);
+
+// A chunk's BLAKE3 64-leaf groups (k_b3_groups work units; an empty chunk is one group).
+__device__ __forceinline__ uint32_t b3_groups_of_len(uint64_t len) {
+    const uint64_t leaves = len ? (len + 1023) / 1024 : 1;
+    return (uint32_t)((leaves + 63) / 64);
+}
+__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, d, 64);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), d, 64);
+        v += ((uint64_t)hi << 32) | lo;
+    }
+    return v;
+}
+// The BLAKE3 group map written by the descriptor assembly (launch_blake3 with
+// plan_ready): group_base [bound + 1], gmap (one entry per group), from d_nar_ngroups.
+struct B3PlanOut {
+    const uint32_t *nar_ngroups = nullptr;
+    uint64_t *group_base = nullptr;
+    uint32_t *gmap = nullptr;
+    uint64_t bound = 0;
+};
 
 // exclusive scan of the per-NAR chunk counts into d_nar_first (total at [n_nars]) + the
 // descriptors and absolute chunk offsets of every NAR's chunks
-void launch_assemble(const uint64_t *d_nar_off, const uint64_t *d_cap_base, const uint64_t *d_wchunk,
+// Returns true when it also built the BLAKE3 group map `b3` (the one-launch form, up to
+// 8,192 NARs); otherwise launch_blake3 builds it.
+bool launch_assemble(const uint64_t *d_nar_off, const uint64_t *d_cap_base, const uint64_t *d_wchunk,
                      const uint32_t *d_nar_nchunks, uint64_t *d_nar_first, uint64_t n_nars, void *d_out,
-                     uint64_t out_cap, uint64_t *d_chunk_abs, uint64_t *d_scan_tmp, hipStream_t st);
+                     uint64_t out_cap, uint64_t *d_chunk_abs, uint64_t *d_scan_tmp, hipStream_t st,
+                     const B3PlanOut *b3 = nullptr);
 
 // d_order_tmp (sha256_order_tmp_elems(max_chunks) u32, or nullptr = identity order) holds
 // the longest-first lane order; max_len bounds every chunk length (bucket width);
@@ -119,7 +147,8 @@ void launch_manifest_spans(const uint64_t *d_first, uint64_t n_nars, uint64_t *d
 void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
                    uint64_t max_chunks, uint64_t total_bytes, uint8_t *d_hash_base, size_t hash_stride,
                    uint32_t *d_gmap, uint64_t *d_group_base, uint32_t *d_gcount_u32,
-                   uint64_t *d_scan_tmp, uint32_t *d_gcv, bool with_lcv, hipStream_t st);
+                   uint64_t *d_scan_tmp, uint32_t *d_gcv, bool with_lcv, hipStream_t st,
+                   bool plan_ready = false);  // plan_ready: d_group_base / d_gmap built by launch_assemble
 size_t blake3_group_bound(uint64_t total_bytes, uint64_t max_chunks);
 size_t blake3_cv_bytes(uint64_t total_bytes, uint64_t max_chunks, bool with_lcv);  // launch_blake3's d_gcv
 

@@ -29,6 +29,12 @@ thread_local uint64_t t_detail[3];  // ChunkingError fields of the last failure 
 thread_local int t_status = CG_OK;
 thread_local std::vector<double> t_stage_ms;
 std::atomic<int> g_profiling{0};
+#ifndef CG_B3_FUSED_PLAN
+#define CG_B3_FUSED_PLAN 1
+#endif
+// BLAKE3 group map built by the walk + assembly (1) or by k_b3_plan (0): test hook
+// cg_test_b3_fused_plan
+std::atomic<int> g_b3_fused_plan{CG_B3_FUSED_PLAN};
 
 int fail(int code, const std::string &msg) {
     t_err = msg;
@@ -379,13 +385,25 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
     cg::launch_scan_compact(ws->seg_count.as<uint32_t>(), ws->seg_cand.as<uint32_t>(), ws->eoff.as<uint64_t>(), slots,
                             nseg, ws->entries.as<uint64_t>(), ws->scan_tmp.as<uint64_t>(), st);
     if (prof_all) HIP_TRY(hipEventRecord(ws->ev[EV_COMPACT], st));
+    // BLAKE3: the walk counts each NAR's 64-leaf groups and the assembly builds the group
+    // map from them, so launch_blake3 needs no planning kernel of its own
+    const bool b3_fuse = algo == CG_BLAKE3 && digest && g_b3_fused_plan.load(std::memory_order_relaxed);
+    if (b3_fuse && (rc = ws->nar_ngroups.ensure((n_nars + 1) * 4, "nar_ngroups"))) return rc;
+    cg::B3PlanOut b3plan;
+    if (b3_fuse) {
+        b3plan.nar_ngroups = ws->nar_ngroups.as<uint32_t>();
+        b3plan.group_base = ws->b3_gbase.as<uint64_t>();
+        b3plan.gmap = ws->b3_gmap.as<uint32_t>();
+        b3plan.bound = chunk_bound;
+    }
     cg::launch_walk(d_data, ws->gear.as<uint64_t>(), ws->entries.as<uint64_t>(), ws->eoff.as<uint64_t>(), nseg,
                     d_nar_off, d_cap_base, n_nars, P, ws->wchunk.as<uint64_t>(),
-                    ws->nar_nchunks.as<uint32_t>(), pieces, st);
+                    ws->nar_nchunks.as<uint32_t>(), pieces, st, b3_fuse ? ws->nar_ngroups.as<uint32_t>() : nullptr);
     if (prof_all) HIP_TRY(hipEventRecord(ws->ev[EV_WALK], st));
-    cg::launch_assemble(d_nar_off, d_cap_base, ws->wchunk.as<uint64_t>(), ws->nar_nchunks.as<uint32_t>(),
-                        ws->nar_first.as<uint64_t>(), n_nars, d_out, out_cap, ws->chunk_abs.as<uint64_t>(),
-                        ws->scan_tmp.as<uint64_t>(), st);
+    const bool b3_planned =
+        cg::launch_assemble(d_nar_off, d_cap_base, ws->wchunk.as<uint64_t>(), ws->nar_nchunks.as<uint32_t>(),
+                            ws->nar_first.as<uint64_t>(), n_nars, d_out, out_cap, ws->chunk_abs.as<uint64_t>(),
+                            ws->scan_tmp.as<uint64_t>(), st, b3_fuse ? &b3plan : nullptr);
     if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_ASSEMBLE], st));
     const uint64_t *d_total = ws->nar_first.as<uint64_t>() + n_nars;
     uint8_t *d_man = nullptr;
@@ -426,7 +444,7 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
         cg::launch_blake3(d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, total_len, hash_base,
                           sizeof(cg_desc), ws->b3_gmap.as<uint32_t>(), ws->b3_gbase.as<uint64_t>(),
                           ws->b3_gcount.as<uint32_t>(), ws->scan_tmp.as<uint64_t>(), ws->b3_gcv.as<uint32_t>(), true,
-                          st);
+                          st, b3_planned);
     }
     if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_DIGEST], st));
     if (d_chunk_ids) HIP_TRY(hipStreamWaitEvent(st, ws->ev_join, 0));
@@ -790,6 +808,10 @@ uint32_t cg_abi_version(void) { return CG_ABI_VERSION; }
 // Test hook: make the n-th device-buffer growth from now fail as out of memory (0 = off);
 // returns the previous countdown.
 uint32_t cg_test_fail_alloc(uint32_t n) { return cgrt::g_fail_alloc.exchange(n); }
+
+// Test hook: BLAKE3 group map from the walk + assembly (1) or from k_b3_plan (0); returns
+// the previous setting.
+int cg_test_b3_fused_plan(int on) { return cgrt::g_b3_fused_plan.exchange(on ? 1 : 0); }
 
 const char *cg_last_error_message(void) { return t_err.c_str(); }
 

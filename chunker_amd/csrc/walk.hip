@@ -250,7 +250,7 @@ __global__ __launch_bounds__(64) void k_walk(const uint8_t *__restrict__ data, c
                                              const uint64_t *__restrict__ nar_off,
                                              const uint64_t *__restrict__ cap_base, uint64_t n_nars, CdcParams P,
                                              uint64_t *__restrict__ wchunk, uint32_t *__restrict__ nar_nchunks,
-                                             int spec, WalkPieces wp) {
+                                             int spec, WalkPieces wp, uint32_t *__restrict__ nar_ngroups) {
     __shared__ uint64_t gear[256];
     for (uint32_t i = threadIdx.x; i < 256; i += 64) gear[i] = gear_g[i];
     __syncthreads();
@@ -368,12 +368,20 @@ __global__ __launch_bounds__(64) void k_walk(const uint8_t *__restrict__ data, c
         __syncthreads();
     }
     if (lane == 0) nar_nchunks[nar] = (uint32_t)k;
+    if (nar_ngroups) {  // BLAKE3 batches: the NAR's 64-leaf groups, for the fused group map (k_assemble_counts)
+        __syncthreads();  // out[] lengths written by lane 0 / other lanes are read below
+        uint32_t ng = 0;
+        for (uint64_t j = lane; j < k; j += 64) ng += b3_groups_of_len(ld_l2(out + 2 * j + 1));
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) ng += (uint32_t)__shfl_xor((int)ng, d, 64);
+        if (lane == 0) nar_ngroups[nar] = ng;
+    }
 }
 
 void launch_walk(const uint8_t *d_data, const uint64_t *d_gear, const uint64_t *d_entries, const uint64_t *d_eoff,
                  uint64_t nseg, const uint64_t *d_nar_off, const uint64_t *d_cap_base, uint64_t n_nars,
                  CdcParams p, uint64_t *d_wchunk, uint32_t *d_nar_nchunks, const WalkPiecesHost &pieces,
-                 hipStream_t st) {
+                 hipStream_t st, uint32_t *d_nar_ngroups) {
     if (n_nars == 0) return;
     const int spec = walk_is_speculative(p) ? 1 : 0;
     WalkPieces wp{pieces.first, pieces.nar, pieces.base, pieces.count, pieces.exit, pieces.starts, pieces.pb,
@@ -382,7 +390,7 @@ void launch_walk(const uint8_t *d_data, const uint64_t *d_gear, const uint64_t *
         hipLaunchKernelGGL(k_walk_pieces, dim3((uint32_t)wp.np), dim3(64), 0, st, d_data, d_gear, d_entries, d_eoff,
                            nseg, d_nar_off, p, wp);
     hipLaunchKernelGGL(k_walk, dim3((uint32_t)n_nars), dim3(64), 0, st, d_data, d_gear, d_entries, d_eoff, nseg,
-                       d_nar_off, d_cap_base, n_nars, p, d_wchunk, d_nar_nchunks, spec, wp);
+                       d_nar_off, d_cap_base, n_nars, p, d_wchunk, d_nar_nchunks, spec, wp, d_nar_ngroups);
 }
 
 // One wave per NAR: copy the walker's (abs offset, length) list into the caller's
@@ -420,18 +428,16 @@ __global__ __launch_bounds__(64) void k_assemble_counts(const uint64_t *__restri
                                                         const uint32_t *__restrict__ nar_nchunks,
                                                         uint64_t *__restrict__ nar_first, uint64_t n_nars,
                                                         DescRaw *__restrict__ out, uint64_t out_cap,
-                                                        uint64_t *__restrict__ chunk_abs) {
+                                                        uint64_t *__restrict__ chunk_abs, B3PlanOut b3) {
     const uint64_t i = blockIdx.x;
     if (i >= n_nars) return;
     const uint32_t lane = threadIdx.x;
-    uint64_t pre = 0;
-    for (uint64_t j = lane; j < i; j += 64) pre += nar_nchunks[j];
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) {
-        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)pre, d, 64);
-        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(pre >> 32), d, 64);
-        pre += ((uint64_t)hi << 32) | lo;
+    uint64_t pre = 0, pre_g = 0;
+    for (uint64_t j = lane; j < i; j += 64) {
+        pre += nar_nchunks[j];
+        if (b3.group_base) pre_g += b3.nar_ngroups[j];
     }
+    pre = wave_sum_u64(pre);
     const uint64_t first = pre, cnt = nar_nchunks[i];
     if (lane == 0) {
         nar_first[i] = first;
@@ -447,21 +453,47 @@ __global__ __launch_bounds__(64) void k_assemble_counts(const uint64_t *__restri
         out[g].length = w[2 * k + 1];
         chunk_abs[g] = abs;
     }
+    if (!b3.group_base) return;
+    // BLAKE3 group map (what k_b3_plan builds from the descriptors): group_base[g] = the
+    // 64-leaf groups of chunks 0..g-1 for every chunk index g <= bound, and gmap[q] = g
+    // for each group q of chunk g < bound
+    pre_g = wave_sum_u64(pre_g);
+    uint64_t run = pre_g;
+    for (uint64_t kb = 0; kb < cnt; kb += 64) {
+        const uint64_t k = kb + lane, g = first + k;
+        const uint32_t gc = k < cnt ? b3_groups_of_len(w[2 * k + 1]) : 0u;
+        uint32_t inc = gc;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t t = (uint32_t)__shfl_up((int)inc, d, 64);
+            if (lane >= (uint32_t)d) inc += t;
+        }
+        const uint64_t gb = run + inc - gc;
+        if (k < cnt && g <= b3.bound) b3.group_base[g] = gb;
+        if (k < cnt && g < b3.bound)
+            for (uint32_t q = 0; q < gc; ++q) b3.gmap[gb + q] = (uint32_t)g;
+        run += (uint32_t)__shfl((int)inc, 63, 64);
+    }
+    if (i == n_nars - 1 && lane == 0 && first + cnt <= b3.bound) b3.group_base[first + cnt] = run;
 }
 
-void launch_assemble(const uint64_t *d_nar_off, const uint64_t *d_cap_base, const uint64_t *d_wchunk,
+bool launch_assemble(const uint64_t *d_nar_off, const uint64_t *d_cap_base, const uint64_t *d_wchunk,
                      const uint32_t *d_nar_nchunks, uint64_t *d_nar_first, uint64_t n_nars, void *d_out,
-                     uint64_t out_cap, uint64_t *d_chunk_abs, uint64_t *d_scan_tmp, hipStream_t st) {
+                     uint64_t out_cap, uint64_t *d_chunk_abs, uint64_t *d_scan_tmp, hipStream_t st,
+                     const B3PlanOut *b3) {
     // (a forced scan path, cg_test_scan_path, takes the two-kernel form so tests reach it)
     if (n_nars > 0 && n_nars <= ASM_FUSED_MAX && g_scan_path == 0) {
+        const B3PlanOut none{};
         hipLaunchKernelGGL(k_assemble_counts, dim3((uint32_t)n_nars), dim3(64), 0, st, d_nar_off, d_cap_base,
-                           d_wchunk, d_nar_nchunks, d_nar_first, n_nars, (DescRaw *)d_out, out_cap, d_chunk_abs);
-        return;
+                           d_wchunk, d_nar_nchunks, d_nar_first, n_nars, (DescRaw *)d_out, out_cap, d_chunk_abs,
+                           b3 ? *b3 : none);
+        return b3 != nullptr;
     }
     launch_exclusive_scan_u32(d_nar_nchunks, d_nar_first, n_nars, 0, d_scan_tmp, st);
-    if (n_nars == 0) return;
+    if (n_nars == 0) return false;
     hipLaunchKernelGGL(k_assemble, dim3((uint32_t)n_nars), dim3(64), 0, st, d_nar_off, d_cap_base, d_wchunk,
                        d_nar_first, n_nars, (DescRaw *)d_out, out_cap, d_chunk_abs);
+    return false;
 }
 
 // Digest-only entry: spans (offset,length) -> desc/abs arrays + total.

@@ -624,3 +624,48 @@ def test_scan_paths_agree(ca, O, path):
             assert_same(got, O.chunk_descriptors(dense, *params, algo=algo), f"path={path} dense algo={algo}")
     finally:
         ca.lib.cg_test_scan_path(old)
+
+
+@pytest.mark.parametrize("fused", [1, 0], ids=["assembly_map", "plan_kernel"])
+def test_blake3_group_map_paths(ca, O, fused):
+    """The BLAKE3 group map (group_base / gmap) comes from the walk + descriptor assembly
+    (each NAR's group count, k_assemble_counts) or from k_b3_plan (cg_test_b3_fused_plan):
+    both give the oracle's digests on ragged NARs (empty ones, sub-leaf chunks, chunks of
+    1 .. 256 groups: max 16 MiB on zeros) and many-NAR batches."""
+    rng = np.random.default_rng(57)
+    lens = [0, 1, 1023, 1024, 1025, 65_536, 65_537, 0, 3_000_001, 131_072 * 3 + 5, 7]
+    nars = [rng.integers(0, 256, n, dtype=np.uint8) for n in lens] + [np.zeros(40 << 20, np.uint8)]
+    old = ca.lib.cg_test_b3_fused_plan(fused)
+    try:
+        for params in ((4096, 16384, 65536), (1 << 20, 4 << 20, 16 << 20)):
+            got = ca.chunk_batch(nars, *params, hash=B3)
+            for i, nar in enumerate(nars):
+                assert_same(got[i], O.chunk_descriptors(nar, *params, algo=B3), f"fused={fused} {params} nar{i}")
+        many = [rng.integers(0, 256, int(n), dtype=np.uint8) for n in rng.integers(0, 300_000, 600)]
+        got = ca.chunk_batch(many, 4096, 16384, 65536, hash=B3)
+        for i in (0, 1, 299, 598, 599):
+            assert_same(got[i], O.chunk_descriptors(many[i], 4096, 16384, 65536, algo=B3), f"many nar{i}")
+    finally:
+        ca.lib.cg_test_b3_fused_plan(old)
+
+
+def test_blake3_group_map_capacity_error(ca):
+    """A descriptor array too small for the batch: the fused group map writes only inside
+    its bounds and the call fails as the SHA-256 path does."""
+    import torch
+
+    from chunker_amd.nar import synth_nars
+
+    data, offs = synth_nars([1 << 20] * 8, first_index=5)
+    d = torch.from_numpy(data).cuda()
+    out = torch.zeros(8 * 48, dtype=torch.uint8, device="cuda")
+    for algo in (B3, SHA):
+        with pytest.raises(ca.ChunkingError, match="too small"):
+            ca.chunk_batch_device(d.data_ptr(), offs, out.data_ptr(), 8, 4096, 16384, 65536, hash=algo,
+                                  stream=torch.cuda.current_stream().cuda_stream)
+    # the engine is still usable afterwards
+    cap = ca.chunking.batch_capacity(offs, 4096)
+    out = torch.zeros(cap * 48, dtype=torch.uint8, device="cuda")
+    first = ca.chunk_batch_device(d.data_ptr(), offs, out.data_ptr(), cap, 4096, 16384, 65536, hash=B3,
+                                  stream=torch.cuda.current_stream().cuda_stream)
+    assert int(first[-1]) > 8
