@@ -98,16 +98,15 @@ __device__ __forceinline__ void b3_parent(const uint32_t *l, const uint32_t *r, 
 }
 
 // Leaf of `n` (0..1024) bytes at p with leaf index ctr.  Words are little-endian;
-// p may be unaligned (v_alignbyte realigns dword-aligned loads).  Blocks lying
+// p may be unaligned (v_alignbyte realigns dword-aligned loads: dwordx4 loads from the
+// unaligned address instead, 16 fewer VALU per block, made the digest stage 15 % slower,
+// profiles/r03_v15_ab_c3_b3_plan_unaligned.jsonl).  Blocks lying
 // wholly inside the leaf are fetched as four 16-byte loads (+ the dword after them
 // when p is unaligned), one block ahead of the compression that uses them (the lanes
 // of a wave sit 1 KiB apart, each on its own cache line).  With loads removed
 // altogether (NOLOAD) the kernel is only ~10 % faster: it is bound by the ~700 VALU
 // of each compression (scripts/diag_b3.py).
 typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
-#ifndef CG_B3_UNALIGNED
-#define CG_B3_UNALIGNED 0
-#endif
 // NOLOAD (diagnostics only): compress lane-dependent register words instead of
 // loading the leaf, to time the compression alone.
 template <bool NOLOAD = false>
@@ -132,13 +131,8 @@ __device__ __forceinline__ void b3_leaf(const uint8_t *p, uint32_t n, uint64_t c
         } else {
             const uint32_t dw[17] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
                                      v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w, v16};
-#if CG_B3_UNALIGNED
-#pragma unroll
-            for (int i = 0; i < 16; ++i) m[i] = dw[i];
-#else
 #pragma unroll
             for (int i = 0; i < 16; ++i) m[i] = __builtin_amdgcn_alignbyte(dw[i + 1], dw[i], shift);
-#endif
         }
         b3_compress(cv, m, ctr, 64u, flags_of(j));
     };
@@ -158,20 +152,12 @@ __device__ __forceinline__ void b3_leaf(const uint8_t *p, uint32_t n, uint64_t c
         u32x4_a4 pa[8], pb[8];
         uint32_t pa32 = 0, pb32 = 0;
         auto fetch2 = [&](u32x4_a4 (&v)[8], uint32_t &v32, uint32_t jp) {
-#if CG_B3_UNALIGNED
-            // dwordx4 loads straight from the (byte-aligned) leaf: the memory path realigns
-            const uint8_t *q8 = p + 128 * (jp < npair ? jp : npair - 1);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) v[i] = *reinterpret_cast<const u32x4_a4 *>(q8 + 16 * i);
-            v32 = 0;
-#else
             const uint32_t *q = base + 32 * (jp < npair ? jp : npair - 1);  // past the end: re-read the last pair
 #pragma unroll
             for (int i = 0; i < 8; ++i) v[i] = *reinterpret_cast<const u32x4_a4 *>(q + 4 * i);
             // the dword after the pair starts inside the leaf whenever shift != 0 (ignored by
             // the realignment when shift == 0: the load re-reads the pair's last dword)
             v32 = q[shift ? 32 : 31];
-#endif
         };
         auto pin = [&](u32x4_a4 (&v)[8], uint32_t &v32) {  // the loads stay where they were issued
             asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
@@ -200,16 +186,10 @@ __device__ __forceinline__ void b3_leaf(const uint8_t *p, uint32_t n, uint64_t c
         u32x4_a4 v[4];
         uint32_t v16 = 0;
         if (!NOLOAD) {
-#if CG_B3_UNALIGNED
-            const uint8_t *q8 = p + 64 * j;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) v[i] = *reinterpret_cast<const u32x4_a4 *>(q8 + 16 * i);
-#else
             const uint32_t *q = base + 16 * j;
 #pragma unroll
             for (int i = 0; i < 4; ++i) v[i] = *reinterpret_cast<const u32x4_a4 *>(q + 4 * i);
             v16 = q[shift ? 16 : 15];
-#endif
         }
         full_block(v, v16, j);
     }
