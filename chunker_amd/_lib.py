@@ -47,7 +47,7 @@ EXPORTS = (
     "cg_selftest", "cg_tables_verified", "cg_set_profiling", "cg_last_stage_times", "cg_synth_nars", "cg_hash",
     "cg_cas_ids_device", "cg_cas_id", "cg_node_put_batch_device", "cg_node_put", "cg_stream_new", "cg_stream_push",
     "cg_stream_finish", "cg_stream_take", "cg_stream_pending", "cg_stream_bytes_consumed", "cg_stream_free",
-    "cg_last_sha_tiers",
+    "cg_last_sha_tiers", "cg_chunk_batch_device_async", "cg_batch_wait",
 )
 # test hooks the product library exports beyond the header (tier caps, spin-guard limit)
 TEST_HOOKS = ("cg_test_sha_quad_max", "cg_test_sha_split_max", "cg_test_sha_spin_limit", "cg_test_cas_pair_max",
@@ -98,6 +98,10 @@ def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
     L.cg_chunk_batch.restype = i
     L.cg_chunk_batch_device.argtypes = [p, p, sz, u64, u64, u64, i, p, sz, p, p]
     L.cg_chunk_batch_device.restype = i
+    L.cg_chunk_batch_device_async.argtypes = [p, p, sz, u64, u64, u64, i, p, sz, p, ctypes.POINTER(p)]
+    L.cg_chunk_batch_device_async.restype = i
+    L.cg_batch_wait.argtypes = [p, p]
+    L.cg_batch_wait.restype = i
     L.cg_push_new.argtypes = [u64, u64, u64, i, ctypes.POINTER(i)]
     L.cg_push_new.restype = p
     L.cg_push_push.argtypes = [p, p, u64, p, sz, psz]

@@ -348,6 +348,46 @@ def chunk_batch_device(d_data_ptr: int, nar_offsets: np.ndarray, d_out_ptr: int,
     return first
 
 
+class BatchInFlight:
+    """A device batch queued by chunk_batch_device_async: wait() blocks until it is done,
+    raises its error (if any) and returns nar_first.  An unwaited batch is waited for when
+    collected, so its workspace always goes back to the engine's pool."""
+
+    def __init__(self, handle: int, n_nars: int):
+        self._h = handle
+        self._n = n_nars
+
+    def wait(self) -> np.ndarray:
+        if self._h is None:
+            raise IoError("batch already waited for")
+        first = np.zeros(self._n + 1, np.uint64)
+        h, self._h = self._h, None
+        _check(lib.cg_batch_wait(ctypes.c_void_p(h), first.ctypes.data))
+        return first
+
+    def __del__(self):
+        if getattr(self, "_h", None) is not None:
+            lib.cg_batch_wait(ctypes.c_void_p(self._h), None)
+            self._h = None
+
+
+def chunk_batch_device_async(d_data_ptr: int, nar_offsets: np.ndarray, d_out_ptr: int, out_cap: int,
+                             min_size=None, avg_size=None, max_size=None,
+                             hash: HashAlgorithm = HashAlgorithm.Sha256, stream: int = 0) -> BatchInFlight:
+    """chunk_batch_device without the wait (cg_chunk_batch_device_async): the pipeline is
+    queued on `stream` and the call returns; BatchInFlight.wait() gives nar_first.  Keeping
+    the next batch queued while waiting for the current one hides the host side of every
+    call behind the GPU's work."""
+    o = ChunkingOptions.resolve(min_size, avg_size, max_size)
+    offs = np.ascontiguousarray(nar_offsets, dtype=np.uint64)
+    n = len(offs) - 1
+    h = ctypes.c_void_p()
+    _check(lib.cg_chunk_batch_device_async(ctypes.c_void_p(d_data_ptr), offs.ctypes.data, n, o.min_size,
+                                           o.avg_size, o.max_size, int(hash), ctypes.c_void_p(d_out_ptr), out_cap,
+                                           ctypes.c_void_p(stream or None), ctypes.byref(h)))
+    return BatchInFlight(h.value, n)
+
+
 def batch_capacity(nar_offsets: np.ndarray, min_size=None) -> int:
     m = DEFAULT_MIN if min_size is None else int(min_size)
     lens = np.diff(np.asarray(nar_offsets, dtype=np.uint64))

@@ -154,6 +154,18 @@ int sha_err_arm(Workspace *ws, hipStream_t st);
 int sha_err_fetch(Workspace *ws, hipStream_t st);
 int sha_err_check(Workspace *ws);
 
+// What a launched batch leaves for finish_batch.
+struct BatchLaunch {
+    uint64_t *s_first = nullptr;  // pinned staging of the NAR -> first-chunk index (n_nars + 1)
+    size_t n_nars = 0, out_cap = 0;
+    bool sha_armed = false, node_put = false;
+    int pmode = 0;  // profiling mode at launch (stage events recorded)
+};
+int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, size_t n_nars, const Opts &o,
+                 int algo, cg_desc *d_out, size_t out_cap, hipStream_t st, uint8_t *d_chunk_ids,
+                 uint8_t *h_manifest_ids, bool digest, BatchLaunch *bl);
+int finish_batch(Workspace *ws, hipStream_t st, const BatchLaunch &bl, uint64_t *h_nar_first);
+
 // The device pipeline for one batch (scan -> compact -> walk -> assemble -> digest).
 int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, size_t n_nars, const Opts &o,
               int algo, cg_desc *d_out, size_t out_cap, uint64_t *h_nar_first, hipStream_t st,

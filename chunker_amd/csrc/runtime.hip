@@ -260,9 +260,12 @@ uint32_t seg_slots(const CdcParams &p) {
 // chunk's ContentId(Chunk, payload) -> d_chunk_ids[32 g], and NAR i's manifest id
 // ContentId(Level1Manifest, its chunk ids in order) -> h_manifest_ids[32 i].  The CAS
 // stage forks onto ws->side_stream after descriptor assembly and joins before return.
-int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, size_t n_nars, const Opts &o,
-              int algo, cg_desc *d_out, size_t out_cap, uint64_t *h_nar_first, hipStream_t st,
-              uint8_t *d_chunk_ids, uint8_t *h_manifest_ids, bool digest) {
+// Launch side: everything up to the copies of the NAR index (and manifest ids, and the
+// SHA-256 spin-guard word) into host memory, all queued on `st`; nothing waits.
+// finish_batch waits for `st` and checks the results.
+int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, size_t n_nars, const Opts &o,
+                 int algo, cg_desc *d_out, size_t out_cap, hipStream_t st, uint8_t *d_chunk_ids,
+                 uint8_t *h_manifest_ids, bool digest, BatchLaunch *bl) {
     if (algo != CG_BLAKE3 && algo != CG_SHA256) return fail(CG_E_INVALID_OPTIONS, "unknown hash algorithm");
     if (((uintptr_t)d_data & 15u) != 0) return fail(CG_E_IO, "device input must be 16-byte aligned");
     int rc;
@@ -453,24 +456,53 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
     if (d_man && h_manifest_ids)
         HIP_TRY(hipMemcpyAsync(h_manifest_ids, d_man, n_nars * 32, hipMemcpyDeviceToHost, st));
     if (sha_armed && (rc = sha_err_fetch(ws, st))) return rc;
+    bl->s_first = s_first;
+    bl->n_nars = n_nars;
+    bl->out_cap = out_cap;
+    bl->sha_armed = sha_armed;
+    bl->pmode = pmode;
+    bl->node_put = d_chunk_ids != nullptr;
+    return CG_OK;
+}
+
+// Wait side: the stream sync, the spin-guard check, the stage times, the NAR index.
+int finish_batch(Workspace *ws, hipStream_t st, const BatchLaunch &bl, uint64_t *h_nar_first) {
+    int rc;
     HIP_TRY(hipStreamSynchronize(st));
-    if (sha_armed && (rc = sha_err_check(ws))) return rc;
-    if (prof) {
-        t_stage_ms.assign(EV_N - 1 + (d_chunk_ids ? 1 : 0), prof_all ? 0.0 : std::nan(""));
+    if (bl.sha_armed && (rc = sha_err_check(ws))) return rc;
+    if (bl.pmode) {
+        const bool prof_all = bl.pmode == 1;
+        t_stage_ms.assign(EV_N - 1 + (bl.node_put ? 1 : 0), prof_all ? 0.0 : std::nan(""));
         for (int k = prof_all ? 1 : EV_DIGEST; k < EV_N; ++k) {
             float ms = 0;
             HIP_TRY(hipEventElapsedTime(&ms, ws->ev[k - 1], ws->ev[k]));
             t_stage_ms[k - 1] = ms;
         }
-        if (d_chunk_ids) {  // CAS stage: from descriptor assembly to the last id
+        if (bl.node_put) {  // CAS stage: from descriptor assembly to the last id
             float ms = 0;
             HIP_TRY(hipEventElapsedTime(&ms, ws->ev[EV_ASSEMBLE], ws->ev_cas));
             t_stage_ms[EV_N - 1] = ms;
         }
     }
-    if (h_nar_first) memcpy(h_nar_first, s_first, (n_nars + 1) * 8);
-    if (s_first[n_nars] > out_cap) return fail(CG_E_CAPACITY, "descriptor output array too small");
+    const size_t n = bl.n_nars;
+    if (h_nar_first) memcpy(h_nar_first, bl.s_first, (n + 1) * 8);
+    if (bl.s_first[n] > bl.out_cap) return fail(CG_E_CAPACITY, "descriptor output array too small");
     return CG_OK;
+}
+
+// The whole device pipeline for one batch, waited for.  A launch that fails part-way
+// may have queued work on `st`: it is drained before the workspace goes back to the pool.
+int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, size_t n_nars, const Opts &o,
+              int algo, cg_desc *d_out, size_t out_cap, uint64_t *h_nar_first, hipStream_t st,
+              uint8_t *d_chunk_ids, uint8_t *h_manifest_ids, bool digest) {
+    BatchLaunch bl;
+    const int rc =
+        launch_batch(ws, d_data, h_nar_off, n_nars, o, algo, d_out, out_cap, st, d_chunk_ids, h_manifest_ids, digest, &bl);
+    if (rc) {
+        (void)hipStreamSynchronize(st);
+        return rc;
+    }
+    return finish_batch(ws, st, bl, h_nar_first);
 }
 
 // The reference's golden boundary fixture, fastcdc_boundaries_match_v3_golden_fixture
@@ -655,6 +687,14 @@ using namespace cgrt;
 // The retained bytes live in HBM: each push copies only its new bytes H2D, straight
 // from the caller's buffer, after the device-resident tail (no host-side copy of
 // the stream); after a drain the tail moves to the front of the other buffer.
+// An asynchronous batch (cg_chunk_batch_device_async): its workspace stays reserved, and
+// its results unread, until cg_batch_wait.
+struct cg_batch {
+    cgrt::Workspace *ws;
+    hipStream_t st;
+    cgrt::BatchLaunch bl;
+};
+
 struct cg_push {
     Opts o;
     int algo;
@@ -855,6 +895,41 @@ int cg_chunk_batch_device(const uint8_t *d_data, const uint64_t *nar_offsets, si
     WsGuard guard{ws};
     return run_batch(ws, d_data, nar_offsets, n_nars, o, algo, d_out, out_cap, nar_first,
                      static_cast<hipStream_t>(stream));
+}
+
+int cg_chunk_batch_device_async(const uint8_t *d_data, const uint64_t *nar_offsets, size_t n_nars, uint64_t min_size,
+                                uint64_t avg_size, uint64_t max_size, int algo, cg_desc *d_out, size_t out_cap,
+                                void *stream, cg_batch **batch) {
+    clear_error();
+    if (!batch) return fail(CG_E_IO, "null batch handle pointer");
+    *batch = nullptr;
+    Opts o;
+    int rc = resolve(min_size, avg_size, max_size, &o, nullptr, 0);
+    if (rc) return rc;
+    if (n_nars && nar_offsets[0] != 0)
+        return fail_bounds(nar_offsets[n_nars], nar_offsets[0], 0, "device batch offsets must start at 0");
+    if ((rc = check_tables())) return rc;
+    Workspace *ws = nullptr;
+    if ((rc = acquire(&ws))) return rc;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    BatchLaunch bl;
+    rc = launch_batch(ws, d_data, nar_offsets, n_nars, o, algo, d_out, out_cap, st, nullptr, nullptr, true, &bl);
+    if (rc) {
+        (void)hipStreamSynchronize(st);
+        release(ws);
+        return rc;
+    }
+    *batch = new cg_batch{ws, st, bl};
+    return CG_OK;
+}
+
+int cg_batch_wait(cg_batch *batch, uint64_t *nar_first) {
+    clear_error();
+    if (!batch) return fail(CG_E_IO, "null batch handle");
+    const int rc = finish_batch(batch->ws, batch->st, batch->bl, nar_first);
+    release(batch->ws);
+    delete batch;
+    return rc;
 }
 
 int cg_hash_spans_device(const uint8_t *d_data, const uint64_t *d_offsets, const uint64_t *d_lengths, size_t n,

@@ -96,6 +96,20 @@ int cg_chunk_batch_device(const uint8_t *d_data, const uint64_t *nar_offsets, si
                           uint64_t min_size, uint64_t avg_size, uint64_t max_size, int algo,
                           cg_desc *d_out, size_t out_cap, uint64_t *nar_first, void *stream);
 
+/* The same batch without the wait: the whole pipeline is queued on `stream` and the call
+ * returns (its host side -- validation, staging, launches -- overlaps whatever the GPU is
+ * still running, so a caller that keeps one batch queued behind another leaves the GPU no
+ * idle gap between them).  `nar_offsets` is copied before the call returns; `d_data` and
+ * `d_out` must stay valid until cg_batch_wait.  cg_batch_wait(batch, nar_first) waits for
+ * the batch, reports its errors (CG_E_CAPACITY, the SHA-256 spin guard, HIP failures),
+ * fills nar_first (n_nars + 1, may be NULL) and frees the handle, whatever it returns.
+ * Every handle must be waited for exactly once; batches on one stream complete in order. */
+typedef struct cg_batch cg_batch;
+int cg_chunk_batch_device_async(const uint8_t *d_data, const uint64_t *nar_offsets, size_t n_nars,
+                                uint64_t min_size, uint64_t avg_size, uint64_t max_size, int algo,
+                                cg_desc *d_out, size_t out_cap, void *stream, cg_batch **batch);
+int cg_batch_wait(cg_batch *batch, uint64_t *nar_first);
+
 /* PushChunker (src/chunking.rs:753-829) over drain_finalized_chunks (:541-673).
  * push/finish write the chunks that became final; `out_cap` must be at least
  * cg_push_out_capacity(h, len).  push after finish -> CG_E_INVALID_OPTIONS

@@ -669,3 +669,53 @@ def test_blake3_group_map_capacity_error(ca):
     first = ca.chunk_batch_device(d.data_ptr(), offs, out.data_ptr(), cap, 4096, 16384, 65536, hash=B3,
                                   stream=torch.cuda.current_stream().cuda_stream)
     assert int(first[-1]) > 8
+
+
+def test_async_batches_match_sync(ca, O):
+    """cg_chunk_batch_device_async + cg_batch_wait: several batches queued on one stream
+    (each with its own workspace) give the synchronous entry's descriptors and index; waits
+    may come in any order; an unwaited handle is reclaimed; a capacity error surfaces at
+    the wait and the engine stays usable."""
+    import torch
+
+    from chunker_amd.nar import synth_nars
+
+    stream = torch.cuda.current_stream().cuda_stream
+    batches = []
+    for seed, algo in ((1, SHA), (2, B3), (3, SHA), (4, B3)):
+        sizes = [1 << 20] * 5 + [8 * seed + 4096, 200_008]
+        data, offs = synth_nars(sizes, first_index=100 * seed)
+        d = torch.from_numpy(data).cuda()
+        cap = ca.chunking.batch_capacity(offs, 4096)
+        ref_out = torch.zeros(cap * 48, dtype=torch.uint8, device="cuda")
+        ref_first = ca.chunk_batch_device(d.data_ptr(), offs, ref_out.data_ptr(), cap, 4096, 16384, 65536, hash=algo,
+                                          stream=stream)
+        batches.append((d, offs, cap, algo, ref_out.cpu().numpy(), ref_first, data))
+    outs = [torch.zeros(b[2] * 48, dtype=torch.uint8, device="cuda") for b in batches]
+    inflight = [ca.chunk_batch_device_async(b[0].data_ptr(), b[1], o.data_ptr(), b[2], 4096, 16384, 65536, hash=b[3],
+                                            stream=stream) for b, o in zip(batches, outs)]
+    for k in (2, 0, 3, 1):  # out of order
+        first = inflight[k].wait()
+        d, offs, cap, algo, ref_out, ref_first, data = batches[k]
+        assert np.array_equal(first, ref_first), k
+        got = outs[k].cpu().numpy()
+        n = int(first[-1])
+        assert np.array_equal(got[: n * 48], ref_out[: n * 48]), k
+        descs = got.view(ca.DESC_DTYPE)
+        ref = O.chunk_descriptors(data[offs[5]:offs[6]], 4096, 16384, 65536, algo=algo)
+        assert_same(descs[int(first[5]):int(first[6])], ref, f"batch{k} nar5")
+    with pytest.raises(ca.IoError):
+        inflight[0].wait()
+    # an unwaited handle goes back to the pool when collected
+    b = batches[0]
+    h = ca.chunk_batch_device_async(b[0].data_ptr(), b[1], outs[0].data_ptr(), b[2], 4096, 16384, 65536, hash=SHA,
+                                    stream=stream)
+    del h
+    # capacity error at the wait
+    h = ca.chunk_batch_device_async(b[0].data_ptr(), b[1], outs[0].data_ptr(), 3, 4096, 16384, 65536, hash=B3,
+                                    stream=stream)
+    with pytest.raises(ca.ChunkingError, match="too small"):
+        h.wait()
+    first = ca.chunk_batch_device_async(b[0].data_ptr(), b[1], outs[0].data_ptr(), b[2], 4096, 16384, 65536,
+                                        hash=SHA, stream=stream).wait()
+    assert np.array_equal(first, b[5])
