@@ -112,11 +112,13 @@ struct B3PlanOut {
 // exclusive scan of the per-NAR chunk counts into d_nar_first (total at [n_nars]) + the
 // descriptors and absolute chunk offsets of every NAR's chunks
 // Returns true when it also built the BLAKE3 group map `b3` (the one-launch form, up to
-// 8,192 NARs); otherwise launch_blake3 builds it.
+// 8,192 NARs); otherwise launch_blake3 builds it.  host_first (optional, a device address
+// of mapped host memory): the one-launch form also writes the NAR index there and sets
+// *wrote_host_first.
 bool launch_assemble(const uint64_t *d_nar_off, const uint64_t *d_cap_base, const uint64_t *d_wchunk,
                      const uint32_t *d_nar_nchunks, uint64_t *d_nar_first, uint64_t n_nars, void *d_out,
                      uint64_t out_cap, uint64_t *d_chunk_abs, uint64_t *d_scan_tmp, hipStream_t st,
-                     const B3PlanOut *b3 = nullptr);
+                     const B3PlanOut *b3, uint64_t *host_first, bool *wrote_host_first);
 
 // d_order_tmp (sha256_order_tmp_elems(max_chunks) u32, or nullptr = identity order) holds
 // the longest-first lane order; max_len bounds every chunk length (bucket width);

@@ -79,16 +79,20 @@ struct DevBuf {
 
 struct PinBuf {
     void *p = nullptr;
+    void *dev = nullptr;  // device address of p (mapped buffers)
     size_t cap = 0;
-    int ensure(size_t bytes) {
+    // mapped: coherent host memory the GPU writes straight into (uncached, over the link)
+    int ensure(size_t bytes, bool mapped = false) {
         if (bytes <= cap) return CG_OK;
         if (p) (void)hipHostFree(p);
-        p = nullptr;
+        p = dev = nullptr;
         cap = 0;
         size_t want = bytes + bytes / 4 + 256;
-        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        hipError_t e = hipHostMalloc(&p, want, mapped ? (hipHostMallocMapped | hipHostMallocCoherent) : hipHostMallocDefault);
+        if (e == hipSuccess && mapped) e = hipHostGetDevicePointer(&dev, p, 0);
         if (e != hipSuccess) {
-            p = nullptr;
+            if (p) (void)hipHostFree(p);
+            p = dev = nullptr;
             return hip_fail(e, "hipHostMalloc", want);
         }
         cap = want;
@@ -107,7 +111,7 @@ struct Workspace {
     DevBuf gear, seg_count, seg_cand, eoff, scan_tmp, entries, nar_off, wchunk, nar_nchunks, nar_first,
         chunk_abs, b3_gcount, b3_gbase, b3_gcv, b3_gmap, in, out, span_off, span_len, order, cas_order, ids,
         man_abs, man_desc, sha_err, pc_first, pc_count, pc_exit, pc_starts, nar_ngroups;
-    PinBuf stage, err_stage;
+    PinBuf stage, err_stage, first_host;  // first_host: mapped, the assembly writes the NAR index there
     hipEvent_t ev[EV_N] = {};
     // CAS ids run on side_stream, concurrently with the digest: both stages are bound by
     // their longest chunk's serial chain, not by the chip, so they overlap for free.

@@ -403,10 +403,16 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
                     d_nar_off, d_cap_base, n_nars, P, ws->wchunk.as<uint64_t>(),
                     ws->nar_nchunks.as<uint32_t>(), pieces, st, b3_fuse ? ws->nar_ngroups.as<uint32_t>() : nullptr);
     if (prof_all) HIP_TRY(hipEventRecord(ws->ev[EV_WALK], st));
+    // the NAR index goes straight into mapped host memory from the assembly kernel: a D2H
+    // copy after the digest cost ~40 us of idle GPU per call (blit + the runtime's gap
+    // before the next call's first copy, profiles/r03_v16_c3_async_kernel_trace.csv)
+    if ((rc = ws->first_host.ensure((n_nars + 1) * 8, /*mapped=*/true))) return rc;
+    bool first_on_host = false;
     const bool b3_planned =
         cg::launch_assemble(d_nar_off, d_cap_base, ws->wchunk.as<uint64_t>(), ws->nar_nchunks.as<uint32_t>(),
                             ws->nar_first.as<uint64_t>(), n_nars, d_out, out_cap, ws->chunk_abs.as<uint64_t>(),
-                            ws->scan_tmp.as<uint64_t>(), st, b3_fuse ? &b3plan : nullptr);
+                            ws->scan_tmp.as<uint64_t>(), st, b3_fuse ? &b3plan : nullptr,
+                            static_cast<uint64_t *>(ws->first_host.dev), &first_on_host);
     if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_ASSEMBLE], st));
     const uint64_t *d_total = ws->nar_first.as<uint64_t>() + n_nars;
     uint8_t *d_man = nullptr;
@@ -452,7 +458,11 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
     if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_DIGEST], st));
     if (d_chunk_ids) HIP_TRY(hipStreamWaitEvent(st, ws->ev_join, 0));
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(s_first, ws->nar_first.p, (n_nars + 1) * 8, hipMemcpyDeviceToHost, st));
+    if (first_on_host) {
+        s_first = ws->first_host.as<uint64_t>();
+    } else {
+        HIP_TRY(hipMemcpyAsync(s_first, ws->nar_first.p, (n_nars + 1) * 8, hipMemcpyDeviceToHost, st));
+    }
     if (d_man && h_manifest_ids)
         HIP_TRY(hipMemcpyAsync(h_manifest_ids, d_man, n_nars * 32, hipMemcpyDeviceToHost, st));
     if (sha_armed && (rc = sha_err_fetch(ws, st))) return rc;

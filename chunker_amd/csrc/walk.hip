@@ -428,7 +428,8 @@ __global__ __launch_bounds__(64) void k_assemble_counts(const uint64_t *__restri
                                                         const uint32_t *__restrict__ nar_nchunks,
                                                         uint64_t *__restrict__ nar_first, uint64_t n_nars,
                                                         DescRaw *__restrict__ out, uint64_t out_cap,
-                                                        uint64_t *__restrict__ chunk_abs, B3PlanOut b3) {
+                                                        uint64_t *__restrict__ chunk_abs, B3PlanOut b3,
+                                                        uint64_t *__restrict__ host_first) {
     const uint64_t i = blockIdx.x;
     if (i >= n_nars) return;
     const uint32_t lane = threadIdx.x;
@@ -442,6 +443,10 @@ __global__ __launch_bounds__(64) void k_assemble_counts(const uint64_t *__restri
     if (lane == 0) {
         nar_first[i] = first;
         if (i == n_nars - 1) nar_first[n_nars] = first + cnt;
+        if (host_first) {  // the caller's copy, straight into mapped host memory (no D2H copy)
+            host_first[i] = first;
+            if (i == n_nars - 1) host_first[n_nars] = first + cnt;
+        }
     }
     const uint64_t *w = wchunk + 2 * cap_base[i];
     const uint64_t base = nar_off[i];
@@ -480,13 +485,15 @@ __global__ __launch_bounds__(64) void k_assemble_counts(const uint64_t *__restri
 bool launch_assemble(const uint64_t *d_nar_off, const uint64_t *d_cap_base, const uint64_t *d_wchunk,
                      const uint32_t *d_nar_nchunks, uint64_t *d_nar_first, uint64_t n_nars, void *d_out,
                      uint64_t out_cap, uint64_t *d_chunk_abs, uint64_t *d_scan_tmp, hipStream_t st,
-                     const B3PlanOut *b3) {
+                     const B3PlanOut *b3, uint64_t *host_first, bool *wrote_host_first) {
+    *wrote_host_first = false;
     // (a forced scan path, cg_test_scan_path, takes the two-kernel form so tests reach it)
     if (n_nars > 0 && n_nars <= ASM_FUSED_MAX && g_scan_path == 0) {
         const B3PlanOut none{};
         hipLaunchKernelGGL(k_assemble_counts, dim3((uint32_t)n_nars), dim3(64), 0, st, d_nar_off, d_cap_base,
                            d_wchunk, d_nar_nchunks, d_nar_first, n_nars, (DescRaw *)d_out, out_cap, d_chunk_abs,
-                           b3 ? *b3 : none);
+                           b3 ? *b3 : none, host_first);
+        *wrote_host_first = host_first != nullptr;
         return b3 != nullptr;
     }
     launch_exclusive_scan_u32(d_nar_nchunks, d_nar_first, n_nars, 0, d_scan_tmp, st);
