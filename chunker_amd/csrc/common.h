@@ -86,6 +86,21 @@ void launch_walk(const uint8_t *d_data, const uint64_t *d_gear, const uint64_t *
                  CdcParams p, uint64_t *d_wchunk, uint32_t *d_nar_nchunks, const WalkPiecesHost &pieces,
                  hipStream_t st, uint32_t *d_nar_ngroups = nullptr);
 
+// Up to two host -> HBM copies done by one kernel reading mapped (coherent) host memory.
+struct StageIn {
+    const void *src[2] = {nullptr, nullptr};  // device addresses of mapped host memory
+    void *dst[2] = {nullptr, nullptr};
+    uint64_t bytes[2] = {0, 0};  // multiples of 4
+    int n = 0;
+    void add(const void *s, void *d, uint64_t b) {
+        src[n] = s;
+        dst[n] = d;
+        bytes[n] = b;
+        ++n;
+    }
+};
+void launch_stage_in(const StageIn &c, hipStream_t st);
+
 // A chunk's BLAKE3 64-leaf groups (k_b3_groups work units; an empty chunk is one group).
 __device__ __forceinline__ uint32_t b3_groups_of_len(uint64_t len) {
     const uint64_t leaves = len ? (len + 1023) / 1024 : 1;

@@ -304,7 +304,7 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
     // host staging: nar_off (n+1), cap_base (n+1), nar_first (n+1), then the piece
     // tables: first (n+1), base (np), nar (np, u32)
     const size_t stage_words = 4 * (n_nars + 1) + np + (np + 1) / 2;
-    if ((rc = ws->stage.ensure(stage_words * sizeof(uint64_t)))) return rc;
+    if ((rc = ws->stage.ensure(stage_words * sizeof(uint64_t), /*mapped=*/true))) return rc;
     uint64_t *s_off = ws->stage.as<uint64_t>();
     uint64_t *s_cap = s_off + (n_nars + 1);
     uint64_t *s_first = s_cap + (n_nars + 1);
@@ -319,6 +319,14 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
     }
     s_cap[n_nars] = total_cap;
     cg::WalkPiecesHost pieces;
+    // host tables -> HBM by one small kernel reading the mapped staging block (a
+    // hipMemcpyAsync from pinned memory waited ~40 us behind the previous call's last
+    // kernel before its blit ran, profiles/r03_v16_c3_async_kernel_trace.csv)
+    cg::StageIn stage_in;
+    auto dev_of = [&](const void *host) {
+        return static_cast<const uint8_t *>(ws->stage.dev) + (static_cast<const uint8_t *>(host) -
+                                                             static_cast<const uint8_t *>(ws->stage.p));
+    };
     if (np) {
         uint64_t g = 0, lb = 0;
         for (size_t i = 0; i < n_nars; ++i) {
@@ -339,7 +347,7 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
         if ((rc = ws->pc_count.ensure(np * 4, "walk pieces"))) return rc;
         if ((rc = ws->pc_exit.ensure(np * 8, "walk pieces"))) return rc;
         if ((rc = ws->pc_starts.ensure(std::max<uint64_t>(lb, pcap) * 8, "walk pieces"))) return rc;
-        HIP_TRY(hipMemcpyAsync(ws->pc_first.p, s_pfirst, (n_nars + 1) * 8 + np * 12, hipMemcpyHostToDevice, st));
+        stage_in.add(s_pfirst, ws->pc_first.p, (n_nars + 1) * 8 + np * 12);
         pieces.first = ws->pc_first.as<uint64_t>();
         pieces.base = pieces.first + (n_nars + 1);
         pieces.nar = reinterpret_cast<uint32_t *>(ws->pc_first.as<uint64_t>() + (n_nars + 1) + np);
@@ -379,11 +387,13 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
     const int pmode = g_profiling.load();
     const bool prof = pmode != 0;
     const bool prof_all = pmode == 1;
-    HIP_TRY(hipMemcpyAsync(ws->nar_off.p, s_off, 2 * (n_nars + 1) * 8, hipMemcpyHostToDevice, st));
+    stage_in.add(s_off, ws->nar_off.p, 2 * (n_nars + 1) * 8);
+    for (int k = 0; k < stage_in.n; ++k) stage_in.src[k] = dev_of(stage_in.src[k]);
     if (prof_all) HIP_TRY(hipEventRecord(ws->ev[EV_START], st));  // scan stage = the scan kernel alone
 
     cg::launch_scan(d_data, total_len, ws->gear.as<uint64_t>(), P.mask_s, P.mask_l, slots,
                     ws->seg_count.as<uint32_t>(), ws->seg_cand.as<uint32_t>(), nseg, st);
+    cg::launch_stage_in(stage_in, st);  // (the scan needs none of the tables)
     if (prof_all) HIP_TRY(hipEventRecord(ws->ev[EV_SCAN], st));
     cg::launch_scan_compact(ws->seg_count.as<uint32_t>(), ws->seg_cand.as<uint32_t>(), ws->eoff.as<uint64_t>(), slots,
                             nseg, ws->entries.as<uint64_t>(), ws->scan_tmp.as<uint64_t>(), st);
@@ -774,7 +784,7 @@ int push_drain(cg_push *h, bool eof, cg_desc *out, size_t out_cap, size_t *n_out
     if (n) {
         // digest descriptors [0, n) in place: the count goes to the device total slot
         uint64_t *d_total = ws->nar_first.as<uint64_t>() + 1;
-        if ((rc = ws->stage.ensure(64))) return rc;
+        if ((rc = ws->stage.ensure(64, /*mapped=*/true))) return rc;
         ws->stage.as<uint64_t>()[0] = n;
         HIP_TRY(hipMemcpyAsync(d_total, ws->stage.p, 8, hipMemcpyHostToDevice, st));
         uint8_t *hb = reinterpret_cast<uint8_t *>(d_out) + offsetof(cg_desc, hash);
@@ -974,7 +984,7 @@ int cg_cas_id(const uint8_t *data, uint64_t len, uint32_t kind, uint8_t out[32])
     WsGuard guard{ws};
     if ((rc = ws->in.ensure(len + 256, "input"))) return rc;
     if ((rc = ws->span_off.ensure(64, "span"))) return rc;
-    if ((rc = ws->stage.ensure(64))) return rc;
+    if ((rc = ws->stage.ensure(64, /*mapped=*/true))) return rc;
     uint64_t *s = ws->stage.as<uint64_t>();
     s[0] = 0;
     s[1] = len;
@@ -1050,7 +1060,7 @@ int cg_hash(const uint8_t *data, uint64_t len, int algo, uint8_t out[32]) {
     WsGuard guard{ws};
     if ((rc = ws->in.ensure(len + 256, "input"))) return rc;
     if ((rc = ws->span_off.ensure(64, "span"))) return rc;
-    if ((rc = ws->stage.ensure(64))) return rc;
+    if ((rc = ws->stage.ensure(64, /*mapped=*/true))) return rc;
     uint64_t *s = ws->stage.as<uint64_t>();
     s[0] = 0;
     s[1] = len;

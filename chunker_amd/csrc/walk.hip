@@ -8,6 +8,8 @@
 // the exact (restarted) hash and takes every later position's verdict from the
 // sorted candidate list produced by K1; "dense" segments (more candidates than
 // the per-segment slots) are rescanned exactly here.
+#include <algorithm>
+
 #include "common.h"
 
 namespace cg {
@@ -501,6 +503,23 @@ bool launch_assemble(const uint64_t *d_nar_off, const uint64_t *d_cap_base, cons
     hipLaunchKernelGGL(k_assemble, dim3((uint32_t)n_nars), dim3(64), 0, st, d_nar_off, d_cap_base, d_wchunk,
                        d_nar_first, n_nars, (DescRaw *)d_out, out_cap, d_chunk_abs);
     return false;
+}
+
+// Host tables (NAR offsets, capacity bases, walk pieces) into HBM: one block per copy,
+// dwords read straight from mapped host memory.
+__global__ __launch_bounds__(256) void k_stage_in(StageIn c) {
+    const uint32_t k = blockIdx.y;
+    const uint32_t *src = static_cast<const uint32_t *>(c.src[k]);
+    uint32_t *dst = static_cast<uint32_t *>(c.dst[k]);
+    const uint64_t n = c.bytes[k] / 4;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) dst[i] = src[i];
+}
+
+void launch_stage_in(const StageIn &c, hipStream_t st) {
+    if (!c.n) return;
+    const uint64_t mx = std::max<uint64_t>(c.bytes[0], c.n > 1 ? c.bytes[1] : 0) / 4;
+    const uint32_t bx = (uint32_t)std::min<uint64_t>((mx + 255) / 256, 256);
+    hipLaunchKernelGGL(k_stage_in, dim3(std::max(bx, 1u), (uint32_t)c.n), dim3(256), 0, st, c);
 }
 
 // Digest-only entry: spans (offset,length) -> desc/abs arrays + total.
