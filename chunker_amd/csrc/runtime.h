@@ -117,6 +117,9 @@ struct Workspace {
     // their longest chunk's serial chain, not by the chip, so they overlap for free.
     hipStream_t side_stream = nullptr;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_cas = nullptr;
+    // end of a launched batch: its wait syncs this event, not the stream (a batch queued
+    // behind it on the same stream must not be waited for too)
+    hipEvent_t ev_done = nullptr;
     // Streams map onto the process's few hardware queues (GPU_MAX_HW_QUEUES, 4 by default)
     // and two streams on one queue serialise: the side stream exists only where used.
     int ensure_side_stream() {
@@ -130,6 +133,7 @@ struct Workspace {
         HIP_TRY(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
         HIP_TRY(hipEventCreate(&ev_cas));
+        HIP_TRY(hipEventCreateWithFlags(&ev_done, hipEventDisableTiming));
         return CG_OK;
     }
 };

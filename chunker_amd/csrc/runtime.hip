@@ -476,6 +476,7 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
     if (d_man && h_manifest_ids)
         HIP_TRY(hipMemcpyAsync(h_manifest_ids, d_man, n_nars * 32, hipMemcpyDeviceToHost, st));
     if (sha_armed && (rc = sha_err_fetch(ws, st))) return rc;
+    HIP_TRY(hipEventRecord(ws->ev_done, st));
     bl->s_first = s_first;
     bl->n_nars = n_nars;
     bl->out_cap = out_cap;
@@ -488,7 +489,8 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
 // Wait side: the stream sync, the spin-guard check, the stage times, the NAR index.
 int finish_batch(Workspace *ws, hipStream_t st, const BatchLaunch &bl, uint64_t *h_nar_first) {
     int rc;
-    HIP_TRY(hipStreamSynchronize(st));
+    (void)st;
+    HIP_TRY(hipEventSynchronize(ws->ev_done));
     if (bl.sha_armed && (rc = sha_err_check(ws))) return rc;
     if (bl.pmode) {
         const bool prof_all = bl.pmode == 1;
