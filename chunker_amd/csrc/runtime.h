@@ -168,6 +168,7 @@ struct BatchLaunch {
     size_t n_nars = 0, out_cap = 0;
     bool sha_armed = false, node_put = false;
     int pmode = 0;  // profiling mode at launch (stage events recorded)
+    hipEvent_t done = nullptr;  // recorded after the batch's last queued operation
 };
 int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, size_t n_nars, const Opts &o,
                  int algo, cg_desc *d_out, size_t out_cap, hipStream_t st, uint8_t *d_chunk_ids,
