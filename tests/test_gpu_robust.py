@@ -190,3 +190,51 @@ def test_push_handle_survives_failed_buffer_growth(ca, nth):
     got += pc.finish()
     assert got == want
     assert b"".join(c.payload for c in got) == data
+
+
+def test_async_batches_from_threads(ca, O):
+    """Four host threads, each keeping two asynchronous batches queued on its own stream
+    (cg_chunk_batch_device_async / cg_batch_wait): every batch equals the synchronous
+    result, whatever the interleaving of launches and waits across threads."""
+    import threading
+
+    import torch
+
+    from chunker_amd.nar import synth_nars
+
+    params = (4096, 16384, 65536)
+    data, offs = synth_nars([1 << 20] * 6 + [300_016], first_index=77)
+    d = torch.from_numpy(data).cuda()
+    cap = ca.chunking.batch_capacity(offs, params[0])
+    refs = {}
+    for algo in (0, 1):
+        out = torch.zeros(cap * 48, dtype=torch.uint8, device="cuda")
+        first = ca.chunk_batch_device(d.data_ptr(), offs, out.data_ptr(), cap, *params, hash=algo)
+        refs[algo] = (first, out.cpu().numpy()[: int(first[-1]) * 48].copy())
+    errs = []
+
+    def work(t):
+        try:
+            s = torch.cuda.Stream()
+            outs = [torch.zeros(cap * 48, dtype=torch.uint8, device="cuda") for _ in range(2)]
+            algo = t % 2
+            pending = ca.chunk_batch_device_async(d.data_ptr(), offs, outs[0].data_ptr(), cap, *params, hash=algo,
+                                                  stream=s.cuda_stream)
+            for k in range(6):
+                nxt = ca.chunk_batch_device_async(d.data_ptr(), offs, outs[(k + 1) % 2].data_ptr(), cap, *params,
+                                                  hash=algo, stream=s.cuda_stream)
+                first = pending.wait()
+                got = outs[k % 2].cpu().numpy()[: int(first[-1]) * 48]
+                if not (np.array_equal(first, refs[algo][0]) and np.array_equal(got, refs[algo][1])):
+                    errs.append(f"thread {t} step {k}")
+                pending = nxt
+            pending.wait()
+        except Exception as e:  # noqa: BLE001
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs, errs[:4]
