@@ -151,17 +151,6 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, d, 64));
     return v;
 }
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, d, 64));
-    return v;
-}
-// CG_SHA_LEAN: the split consumer's block bookkeeping without per-lane selects while every
-// lane's chunk is still running (a scalar branch on the wave's shortest chunk) and with a
-// publish every lane stores (no exec-mask round trip)
-#ifndef CG_SHA_LEAN
-#define CG_SHA_LEAN 0
-#endif
 
 #ifndef CG_PC_RING
 #define CG_PC_RING 4u
@@ -211,11 +200,6 @@ __device__ __forceinline__ unsigned long long wait_slot(const uint32_t *done, ui
 __device__ __forceinline__ void publish(uint32_t *ready, uint32_t k, uint32_t lane) {
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     if (lane == 0) lds_store_release(ready, k + 1);
-}
-// The same from every lane (one value, one address): no exec-mask change around the store.
-__device__ __forceinline__ void publish_all(uint32_t *ready, uint32_t k) {
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-    lds_store_release(ready, k + 1);
 }
 
 // Words of a chunk's tail block (k == nb: tail bytes, 0x80, zeros, [bit length]) or
@@ -464,7 +448,7 @@ template <bool QUAD>
 __device__ __forceinline__ void sha_rounds_split(uint32_t st[4], const uint4 (&cur)[8], uint4 (&nxt)[8],
                                                  const uint32_t *next_row, uint32_t knext, bool prefetch,
                                                  const uint32_t *ready, bool active, const SplitLane &c,
-                                                 uint32_t &z, bool all_active = false) {
+                                                 uint32_t &z) {
     uint32_t x0 = st[0], x1 = st[1], x2 = st[2], x3 = st[3];
     const uint32_t r0 = __hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     SPL32(0, cur)
@@ -473,17 +457,10 @@ __device__ __forceinline__ void sha_rounds_split(uint32_t st[4], const uint4 (&c
     // inside a branch made the compiler drain lgkmcnt at the join, an LDS round trip per block
     load_w8(nxt, next_row);
     SPL32(32, cur)
-    if (CG_SHA_LEAN && all_active) {  // wave-uniform: every lane's chunk still has this block
-        st[0] += x0;
-        st[1] += x1;
-        st[2] += x2;
-        st[3] += x3;
-    } else {
-        st[0] = active ? st[0] + x0 : st[0];
-        st[1] = active ? st[1] + x1 : st[1];
-        st[2] = active ? st[2] + x2 : st[2];
-        st[3] = active ? st[3] + x3 : st[3];
-    }
+    st[0] = active ? st[0] + x0 : st[0];
+    st[1] = active ? st[1] + x1 : st[1];
+    st[2] = active ? st[2] + x2 : st[2];
+    st[3] = active ? st[3] + x3 : st[3];
 }
 
 // Producer wave of a split workgroup.  The pair shares the message schedule by
@@ -575,7 +552,7 @@ __device__ unsigned long long sha_produce_pair(const uint8_t *p, uint64_t len, u
 template <bool QUAD>
 __device__ void split_consumer(uint32_t (*sW)[64 * PC_ROW], uint32_t row, bool hi, uint32_t lane, uint32_t NB,
                                uint32_t nbt, uint32_t *s_ready, uint32_t *s_done, uint32_t st[4],
-                               unsigned long long *t_spin, bool timed, uint32_t NBmin) {
+                               unsigned long long *t_spin, bool timed) {
     SplitLane c;
     if (QUAD) {  // lanes 0-2 of a bank take one rotation each; lane 3 is idle garbage
         const uint32_t q = lane & 3u;
@@ -603,21 +580,14 @@ __device__ void split_consumer(uint32_t (*sW)[64 * PC_ROW], uint32_t row, bool h
         spl_z(z, st[3], wA[0].x);
     }
     for (uint32_t k = 0; k < NB; k += 2) {
-        sha_rounds_split<QUAD>(st, wA, wB, &sW[(k + 1) % PC_RING][off], k + 1, k + 1 < NB, s_ready, k < nbt, c, z,
-                               k < NBmin);
+        sha_rounds_split<QUAD>(st, wA, wB, &sW[(k + 1) % PC_RING][off], k + 1, k + 1 < NB, s_ready, k < nbt, c, z);
         spl_z(z, st[3], wB[0].x);
-        if (CG_SHA_LEAN)
-            publish_all(s_done, k);
-        else
-            publish(s_done, k, lane);
+        publish(s_done, k, lane);
         if (k + 1 >= NB) break;
         sha_rounds_split<QUAD>(st, wB, wA, &sW[(k + 2) % PC_RING][off], k + 2, k + 2 < NB, s_ready, k + 1 < nbt, c,
-                               z, k + 1 < NBmin);
+                               z);
         spl_z(z, st[3], wA[0].x);
-        if (CG_SHA_LEAN)
-            publish_all(s_done, k + 1);
-        else
-            publish(s_done, k + 1, lane);
+        publish(s_done, k + 1, lane);
     }
 }
 
@@ -698,8 +668,6 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
     const uint32_t nbt = valid ? (uint32_t)(nb + (rem < 56 ? 1 : 2)) : 0u;  // blocks incl. padding
     // identical in both waves (same chunks); scalar, so the block loops are uniform
     const uint32_t NB = __builtin_amdgcn_readfirstlane(wave_max_u32(nbt));
-    // blocks every chunk of the wave still has (lanes without a chunk do not count)
-    const uint32_t NBmin = __builtin_amdgcn_readfirstlane(wave_min_u32(valid ? nbt : 0xffffffffu));
 
     if (producer) {
         const uint8_t *p = data + (valid ? abs[ci] : 0);
@@ -718,9 +686,9 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
     } else if (split) {
         uint32_t st[4];
         if (quad)
-            split_consumer<true>(sW, row, hi, lane, NB, nbt, &s_ready, &s_done, st, &t_spin, diag != nullptr, NBmin);
+            split_consumer<true>(sW, row, hi, lane, NB, nbt, &s_ready, &s_done, st, &t_spin, diag != nullptr);
         else
-            split_consumer<false>(sW, row, hi, lane, NB, nbt, &s_ready, &s_done, st, &t_spin, diag != nullptr, NBmin);
+            split_consumer<false>(sW, row, hi, lane, NB, nbt, &s_ready, &s_done, st, &t_spin, diag != nullptr);
         if (diag && lane == 0) sha_diag_consumer(diag, t_spin, t_start, rt_start);
         if (valid && (!quad || (lane & 3u) == 0)) {  // hi: H0..H3 (bytes 0-15), lo: H4..H7 (bytes 16-31)
             uint4 *o = reinterpret_cast<uint4 *>(hash_base + ci * stride + (hi ? 0 : 16));
