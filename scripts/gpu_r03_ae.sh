@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 3 session AE: randomized device-entry parity sweep (tests/test_gpu_fuzz.py, 48 seeds).
+# Round 3 session AE: randomized device-entry parity sweep (tests/test_gpu_fuzz.py).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 mkdir -p gpurun_out

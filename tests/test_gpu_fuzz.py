@@ -27,7 +27,7 @@ def O():
     return oracle
 
 
-@pytest.mark.parametrize("seed", range(48))
+@pytest.mark.parametrize("seed", range(96))
 def test_fuzz_device_batches(ca, O, seed):
     import torch
 
