@@ -434,8 +434,12 @@ __global__ __launch_bounds__(64 * B3_WAVES) void k_b3_groups(const uint8_t *__re
 // (~17 compressions per 16 groups against 6 per group in b3_wave_fold).  Same pairing
 // as b3_wave_fold (odd node carried up; ROOT on the last parent of a single-group chunk);
 // the group's value goes to the digest (single-group chunks) or gcv (k_b3_top).
+#ifndef B3_FOLD_G
 #define B3_FOLD_G 16u
+#endif
+#ifndef B3_FOLD_T
 #define B3_FOLD_T 256u  // 4 waves: level-1 loads all in flight at once, level slots over 4 waves
+#endif
 __global__ __launch_bounds__(B3_FOLD_T) void k_b3_fold(const DescRaw *__restrict__ desc,
                                                        const uint64_t *__restrict__ total_p, uint64_t max_chunks,
                                                        const uint64_t *__restrict__ group_base,
