@@ -83,7 +83,8 @@ struct PinBuf {
     size_t cap = 0;
     // mapped: coherent host memory the GPU writes straight into (uncached, over the link)
     int ensure(size_t bytes, bool mapped = false) {
-        if (bytes <= cap) return CG_OK;
+        if (bytes <= cap && (!mapped || dev)) return CG_OK;  // (a mapped request never gets an unmapped buffer)
+        if (bytes < cap) bytes = cap;
         if (p) (void)hipHostFree(p);
         p = dev = nullptr;
         cap = 0;
