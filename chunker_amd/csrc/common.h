@@ -63,8 +63,10 @@ extern uint32_t g_scan_path;  // test hook cg_test_scan_path (scan.hip)
 
 // Exclusive scan of the per-segment candidate counts into d_eoff fused with the compaction of
 // the candidate slots into the sorted entry list.
+// `si`: host tables copied into HBM by extra blocks of the compaction's first launch.
+struct StageIn;
 void launch_scan_compact(const uint32_t *d_seg_count, const uint32_t *d_seg_cand, uint64_t *d_eoff, uint32_t cap,
-                         uint64_t nseg, uint64_t *d_entries, uint64_t *d_tmp, hipStream_t st);
+                         uint64_t nseg, uint64_t *d_entries, uint64_t *d_tmp, hipStream_t st, const StageIn &si);
 
 // Piece lists for the walk of large NARs (walk.hip, k_walk_pieces); np = 0: none.
 struct WalkPiecesHost {
@@ -100,6 +102,15 @@ struct StageIn {
     }
 };
 void launch_stage_in(const StageIn &c, hipStream_t st);
+// Blocks per copy when the stage-in rides along another launch (the compaction's first
+// kernel), and the copy itself: block b of copy k takes dwords b*T + t, b*T + t + nb*T, ...
+#define STAGE_IN_BLOCKS 8u
+__device__ __forceinline__ void stage_in_part(const StageIn &c, uint32_t k, uint32_t b, uint32_t nb) {
+    const uint32_t *src = static_cast<const uint32_t *>(c.src[k]);
+    uint32_t *dst = static_cast<uint32_t *>(c.dst[k]);
+    const uint64_t n = c.bytes[k] / 4;
+    for (uint64_t i = (uint64_t)b * blockDim.x + threadIdx.x; i < n; i += (uint64_t)nb * blockDim.x) dst[i] = src[i];
+}
 
 // A chunk's BLAKE3 64-leaf groups (k_b3_groups work units; an empty chunk is one group).
 __device__ __forceinline__ uint32_t b3_groups_of_len(uint64_t len) {

@@ -319,9 +319,9 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
     }
     s_cap[n_nars] = total_cap;
     cg::WalkPiecesHost pieces;
-    // host tables -> HBM by one small kernel reading the mapped staging block (a
-    // hipMemcpyAsync from pinned memory waited ~40 us behind the previous call's last
-    // kernel before its blit ran, profiles/r03_v16_c3_async_kernel_trace.csv)
+    // host tables -> HBM by extra blocks of the compaction's first kernel reading the mapped
+    // staging block (a hipMemcpyAsync from pinned memory waited ~40 us behind the previous
+    // call's last kernel before its blit ran, profiles/r03_v16_c3_async_kernel_trace.csv)
     cg::StageIn stage_in;
     auto dev_of = [&](const void *host) {
         return static_cast<const uint8_t *>(ws->stage.dev) + (static_cast<const uint8_t *>(host) -
@@ -393,10 +393,10 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
 
     cg::launch_scan(d_data, total_len, ws->gear.as<uint64_t>(), P.mask_s, P.mask_l, slots,
                     ws->seg_count.as<uint32_t>(), ws->seg_cand.as<uint32_t>(), nseg, st);
-    cg::launch_stage_in(stage_in, st);  // (the scan needs none of the tables)
     if (prof_all) HIP_TRY(hipEventRecord(ws->ev[EV_SCAN], st));
+    // (the host tables ride along the compaction's first launch: the scan needs none of them)
     cg::launch_scan_compact(ws->seg_count.as<uint32_t>(), ws->seg_cand.as<uint32_t>(), ws->eoff.as<uint64_t>(), slots,
-                            nseg, ws->entries.as<uint64_t>(), ws->scan_tmp.as<uint64_t>(), st);
+                            nseg, ws->entries.as<uint64_t>(), ws->scan_tmp.as<uint64_t>(), st, stage_in);
     if (prof_all) HIP_TRY(hipEventRecord(ws->ev[EV_COMPACT], st));
     // BLAKE3: the walk counts each NAR's 64-leaf groups and the assembly builds the group
     // map from them, so launch_blake3 needs no planning kernel of its own

@@ -496,8 +496,14 @@ void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint
 __device__ __forceinline__ uint64_t xform(uint32_t v, uint32_t cap) { return cap ? (v <= cap ? v : 1u) : v; }
 
 __global__ __launch_bounds__(SCAN_T) void k_tile_sums(const uint32_t *__restrict__ in, uint64_t n, uint32_t cap,
-                                                      uint64_t *__restrict__ tile_sum) {
+                                                      uint64_t *__restrict__ tile_sum, StageIn si) {
     __shared__ uint64_t s_wave[SCAN_T / 64];
+    const uint32_t ntiles = (uint32_t)((n + SCAN_TILE - 1) / SCAN_TILE);
+    if (blockIdx.x >= ntiles) {  // stage-in blocks (uniform per block)
+        const uint32_t e = blockIdx.x - ntiles;
+        stage_in_part(si, e / STAGE_IN_BLOCKS, e % STAGE_IN_BLOCKS, STAGE_IN_BLOCKS);
+        return;
+    }
     const uint64_t base = (uint64_t)blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_ITEMS;
     uint64_t s = 0;
 #pragma unroll
@@ -604,9 +610,14 @@ __global__ __launch_bounds__(SCAN_T) void k_scan_apply(const uint32_t *__restric
 #define SCAN_SMALL_MAX (4u * SCAN_SMALL_T * SCAN_ITEMS)
 template <bool COMPACT>
 __global__ __launch_bounds__(SCAN_SMALL_T) void k_scan_small(const uint32_t *__restrict__ in, uint64_t n, uint32_t cap,
-                                                             uint64_t *__restrict__ out, CompactArgs ca) {
+                                                             uint64_t *__restrict__ out, CompactArgs ca, StageIn si) {
     __shared__ uint64_t s_wave[SCAN_SMALL_T / 64];
     __shared__ uint64_t s_carry;
+    if (blockIdx.x > 0) {  // stage-in blocks (uniform per block)
+        const uint32_t e = blockIdx.x - 1;
+        stage_in_part(si, e / STAGE_IN_BLOCKS, e % STAGE_IN_BLOCKS, STAGE_IN_BLOCKS);
+        return;
+    }
     uint64_t carry = 0;
     for (uint64_t b = 0; b < n; b += (uint64_t)SCAN_SMALL_T * SCAN_ITEMS) {
         const uint64_t base = b + threadIdx.x * SCAN_ITEMS;
@@ -646,18 +657,21 @@ uint32_t g_scan_path = 0;
 
 template <bool COMPACT>
 static void launch_scan_impl(const uint32_t *d_in, uint64_t *d_out, uint64_t n, uint32_t cap, uint64_t *d_tmp,
-                             CompactArgs ca, hipStream_t st) {
+                             CompactArgs ca, hipStream_t st, const StageIn &si = StageIn{}) {
+    const uint32_t extra = (uint32_t)si.n * STAGE_IN_BLOCKS;
     if (n == 0) {
         (void)hipMemsetAsync(d_out, 0, sizeof(uint64_t), st);
+        launch_stage_in(si, st);
         return;
     }
     const uint32_t path = g_scan_path;
     if (path == 1 || (path == 0 && n <= SCAN_SMALL_MAX)) {
-        hipLaunchKernelGGL(k_scan_small<COMPACT>, dim3(1), dim3(SCAN_SMALL_T), 0, st, d_in, n, cap, d_out, ca);
+        hipLaunchKernelGGL(k_scan_small<COMPACT>, dim3(1 + extra), dim3(SCAN_SMALL_T), 0, st, d_in, n, cap, d_out, ca,
+                           si);
         return;
     }
     const uint64_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
-    hipLaunchKernelGGL(k_tile_sums, dim3((uint32_t)ntiles), dim3(SCAN_T), 0, st, d_in, n, cap, d_tmp);
+    hipLaunchKernelGGL(k_tile_sums, dim3((uint32_t)ntiles + extra), dim3(SCAN_T), 0, st, d_in, n, cap, d_tmp, si);
     if (path == 2 || (path == 0 && ntiles <= SCAN_REDUCE_MAX)) {
         hipLaunchKernelGGL((k_scan_apply<COMPACT, true>), dim3((uint32_t)ntiles), dim3(SCAN_T), 0, st, d_in, n, cap,
                            d_tmp, d_out, ntiles, ca);
@@ -678,8 +692,8 @@ void launch_exclusive_scan_u32(const uint32_t *d_in, uint64_t *d_out, uint64_t n
 // exclusive scan of the per-segment counts (eoff = each segment's first entry).
 // ---------------------------------------------------------------------------
 void launch_scan_compact(const uint32_t *d_seg_count, const uint32_t *d_seg_cand, uint64_t *d_eoff, uint32_t cap,
-                         uint64_t nseg, uint64_t *d_entries, uint64_t *d_tmp, hipStream_t st) {
-    launch_scan_impl<true>(d_seg_count, d_eoff, nseg, cap, d_tmp, CompactArgs{d_seg_cand, d_entries}, st);
+                         uint64_t nseg, uint64_t *d_entries, uint64_t *d_tmp, hipStream_t st, const StageIn &si) {
+    launch_scan_impl<true>(d_seg_count, d_eoff, nseg, cap, d_tmp, CompactArgs{d_seg_cand, d_entries}, st, si);
 }
 
 }  // namespace cg
