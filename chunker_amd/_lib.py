@@ -53,7 +53,7 @@ EXPORTS = (
 TEST_HOOKS = ("cg_test_sha_quad_max", "cg_test_sha_split_max", "cg_test_sha_spin_limit", "cg_test_cas_pair_max",
               "cg_test_fail_alloc", "cg_test_sha_quad_fill", "cg_test_sha_pair_fill", "cg_test_scan_path",
               "cg_test_stream_group_cap", "cg_test_stream_max_lanes", "cg_test_stream_eager",
-              "cg_test_b3_fused_plan")
+              "cg_test_b3_fused_plan", "cg_test_b3_packed")
 
 
 def _hw_queues_default() -> None:
@@ -164,9 +164,10 @@ def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
         for name in ("cg_test_stream_eager", "cg_test_stream_max_lanes"):
             getattr(L, name).argtypes = [u32]
             getattr(L, name).restype = u32
-    if hasattr(L, "cg_test_b3_fused_plan"):
-        L.cg_test_b3_fused_plan.argtypes = [i]
-        L.cg_test_b3_fused_plan.restype = i
+    for name in ("cg_test_b3_fused_plan", "cg_test_b3_packed"):
+        if hasattr(L, name):
+            getattr(L, name).argtypes = [i]
+            getattr(L, name).restype = i
     L.cg_test_fail_alloc.argtypes = [ctypes.c_uint32]
     L.cg_test_fail_alloc.restype = ctypes.c_uint32
     L.cg_set_profiling.argtypes = [i]

@@ -428,6 +428,50 @@ __global__ __launch_bounds__(64 * B3_WAVES) void k_b3_groups(const uint8_t *__re
     }
 }
 
+// Packed leaves (the product when the group map comes from the descriptor assembly): the
+// leaves of all chunks back to back, lane = leaf slot, so a wave covers 64 leaves whatever
+// chunk they belong to and no lane idles at a chunk's partial last group (the
+// one-group-per-wave form above idles ~32 lanes per chunk: ~3 % of the leaf compressions on
+// config 3, more for smaller chunks).  lmap[w] is the chunk of the wave's first slot; a
+// lane past that chunk's leaves steps to the next chunk (chunks of fewer than 64 leaves
+// make it several steps).  A one-leaf chunk's lane writes the digest (ROOT); every other
+// leaf value goes to its group's slot in lcv, folded by k_b3_fold as before.
+__global__ __launch_bounds__(64 * B3_WAVES) void k_b3_leaves(const uint8_t *__restrict__ data,
+                                                             const uint64_t *__restrict__ abs,
+                                                             const DescRaw *__restrict__ desc,
+                                                             const uint64_t *__restrict__ total_p,
+                                                             uint64_t max_chunks,
+                                                             const uint64_t *__restrict__ group_base,
+                                                             const uint64_t *__restrict__ leaf_base,
+                                                             const uint32_t *__restrict__ lmap,
+                                                             uint8_t *__restrict__ hash_base, size_t stride,
+                                                             uint32_t *__restrict__ lcv) {
+    uint64_t total = *total_p;
+    if (total > max_chunks) total = max_chunks;
+    const uint64_t W = (uint64_t)blockIdx.x * B3_WAVES + (threadIdx.x >> 6);
+    const uint64_t T = leaf_base[total];
+    if (W * 64 >= T) return;  // uniform per wave
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t s = W * 64 + lane;
+    if (s >= T) return;  // the batch's last wave
+    uint64_t c = lmap[W];
+    while (s >= leaf_base[c + 1]) ++c;
+    const uint64_t len = desc[c].length;
+    const uint64_t leaves = len ? (len + 1023) / 1024 : 1;
+    const uint64_t l = s - leaf_base[c];
+    const uint64_t off = l * 1024;
+    const uint32_t n = len ? (uint32_t)((len - off) < 1024 ? (len - off) : 1024) : 0u;
+    uint32_t cv[8];
+    b3_leaf<false>(data + abs[c] + off, n, l, leaves == 1, cv);
+    if (leaves == 1) {
+        store_digest(hash_base + c * stride, cv);
+    } else {
+        uint4 *o = reinterpret_cast<uint4 *>(lcv + ((group_base[c] + l / 64) * 64 + l % 64) * 8);
+        o[0] = make_uint4(cv[0], cv[1], cv[2], cv[3]);
+        o[1] = make_uint4(cv[4], cv[5], cv[6], cv[7]);
+    }
+}
+
 // Fold the leaf chaining values of B3_FOLD_G consecutive 64-leaf groups per wave, level
 // by level in LDS: at each level every (group, parent) slot is a lane, so a level of the
 // 16 groups costs (16 x parents) / 64 wave-wide compressions instead of one per group
@@ -720,6 +764,9 @@ __global__ void k_diag_b3_chain_g4(uint32_t iters, uint32_t *out) {
 }
 #endif
 
+size_t blake3_leaf_wave_bound(uint64_t total_bytes, uint64_t max_chunks) {
+    return (total_bytes / 1024 + max_chunks + 63) / 64 + 1;
+}
 size_t blake3_group_bound(uint64_t total_bytes, uint64_t max_chunks) {
     return total_bytes / 65536 + max_chunks + 1;  // an upper bound for every leaves-per-lane setting
 }
@@ -732,7 +779,8 @@ size_t blake3_cv_bytes(uint64_t total_bytes, uint64_t max_chunks, bool with_lcv)
 void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
                    uint64_t max_chunks, uint64_t total_bytes, uint8_t *d_hash_base, size_t hash_stride,
                    uint32_t *d_gmap, uint64_t *d_group_base, uint32_t *d_gcount_u32, uint64_t *d_scan_tmp,
-                   uint32_t *d_gcv, bool with_lcv, hipStream_t st, bool plan_ready) {
+                   uint32_t *d_gcv, bool with_lcv, hipStream_t st, bool plan_ready, const uint64_t *d_leaf_base,
+                   const uint32_t *d_lmap) {
     if (max_chunks == 0) return;
     const DescRaw *desc = (const DescRaw *)d_desc;
     const uint32_t cblocks = (uint32_t)((max_chunks + 255) / 256);
@@ -773,9 +821,17 @@ void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
         launch_exclusive_scan_u32(d_gcount_u32, d_group_base, max_chunks, 0, d_scan_tmp, st);
         hipLaunchKernelGGL(k_b3_map, dim3(cblocks), dim3(256), 0, st, d_group_base, d_total, max_chunks, d_gmap);
     }
-    hipLaunchKernelGGL(groups,
-                       dim3((uint32_t)((gbound + B3_WAVES - 1) / B3_WAVES)), dim3(64 * B3_WAVES), 0, st, d_data, d_abs,
-                       desc, d_total, max_chunks, d_group_base, d_gmap, d_hash_base, hash_stride, d_gcv, d_lcv);
+    if (plan_ready && d_leaf_base && defer) {
+        // packed leaves: at most total_bytes / 1 KiB + one partial leaf per chunk
+        const uint64_t wbound = (total_bytes / 1024 + max_chunks + 63) / 64;
+        hipLaunchKernelGGL(k_b3_leaves, dim3((uint32_t)((wbound + B3_WAVES - 1) / B3_WAVES)), dim3(64 * B3_WAVES), 0, st,
+                           d_data, d_abs, desc, d_total, max_chunks, d_group_base, d_leaf_base, d_lmap, d_hash_base,
+                           hash_stride, d_lcv);
+    } else {
+        hipLaunchKernelGGL(groups, dim3((uint32_t)((gbound + B3_WAVES - 1) / B3_WAVES)), dim3(64 * B3_WAVES), 0, st,
+                           d_data, d_abs, desc, d_total, max_chunks, d_group_base, d_gmap, d_hash_base, hash_stride,
+                           d_gcv, d_lcv);
+    }
     if (defer)
         hipLaunchKernelGGL(k_b3_fold, dim3((uint32_t)((gbound + B3_FOLD_G - 1) / B3_FOLD_G)), dim3(B3_FOLD_T), 0, st, desc,
                            d_total, max_chunks, d_group_base, d_gmap, d_lcv, d_hash_base, hash_stride, d_gcv);

@@ -113,10 +113,8 @@ __device__ __forceinline__ void stage_in_part(const StageIn &c, uint32_t k, uint
 }
 
 // A chunk's BLAKE3 64-leaf groups (k_b3_groups work units; an empty chunk is one group).
-__device__ __forceinline__ uint32_t b3_groups_of_len(uint64_t len) {
-    const uint64_t leaves = len ? (len + 1023) / 1024 : 1;
-    return (uint32_t)((leaves + 63) / 64);
-}
+__device__ __forceinline__ uint32_t b3_leaves_of_len(uint64_t len) { return len ? (uint32_t)((len + 1023) / 1024) : 1u; }
+__device__ __forceinline__ uint32_t b3_groups_of_len(uint64_t len) { return (b3_leaves_of_len(len) + 63) / 64; }
 __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) {
@@ -128,11 +126,18 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
 }
 // The BLAKE3 group map written by the descriptor assembly (launch_blake3 with
 // plan_ready): group_base [bound + 1], gmap (one entry per group), from d_nar_ngroups.
+// Packed leaves (leaf_base / lmap set): the leaves of all chunks back to back, 64 per
+// wave whatever chunk they belong to (no idle lanes at chunk tails); leaf_base [bound + 1]
+// = leaves of chunks 0..g-1, lmap[w] = the chunk holding leaf slot 64 w.  nar_ngroups holds
+// each NAR's group count at [i] and its leaf count at [n_nars + 1 + i].
 struct B3PlanOut {
     const uint32_t *nar_ngroups = nullptr;
     uint64_t *group_base = nullptr;
     uint32_t *gmap = nullptr;
     uint64_t bound = 0;
+    uint64_t *leaf_base = nullptr;
+    uint32_t *lmap = nullptr;
+    uint64_t lmap_cap = 0;
 };
 
 // exclusive scan of the per-NAR chunk counts into d_nar_first (total at [n_nars]) + the
@@ -176,7 +181,10 @@ void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
                    uint64_t max_chunks, uint64_t total_bytes, uint8_t *d_hash_base, size_t hash_stride,
                    uint32_t *d_gmap, uint64_t *d_group_base, uint32_t *d_gcount_u32,
                    uint64_t *d_scan_tmp, uint32_t *d_gcv, bool with_lcv, hipStream_t st,
-                   bool plan_ready = false);  // plan_ready: d_group_base / d_gmap built by launch_assemble
+                   bool plan_ready = false, const uint64_t *d_leaf_base = nullptr, const uint32_t *d_lmap = nullptr);
+// (plan_ready: d_group_base / d_gmap built by launch_assemble; with d_leaf_base / d_lmap
+// from it too, the leaves run packed, k_b3_leaves)
+size_t blake3_leaf_wave_bound(uint64_t total_bytes, uint64_t max_chunks);  // lmap entries
 size_t blake3_group_bound(uint64_t total_bytes, uint64_t max_chunks);
 size_t blake3_cv_bytes(uint64_t total_bytes, uint64_t max_chunks, bool with_lcv);  // launch_blake3's d_gcv
 

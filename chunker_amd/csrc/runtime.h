@@ -111,7 +111,7 @@ struct Workspace {
     uint64_t gear_epoch = 0;
     DevBuf gear, seg_count, seg_cand, eoff, scan_tmp, entries, nar_off, wchunk, nar_nchunks, nar_first,
         chunk_abs, b3_gcount, b3_gbase, b3_gcv, b3_gmap, in, out, span_off, span_len, order, cas_order, ids,
-        man_abs, man_desc, sha_err, pc_first, pc_count, pc_exit, pc_starts, nar_ngroups;
+        man_abs, man_desc, sha_err, pc_first, pc_count, pc_exit, pc_starts, nar_ngroups, b3_lbase, b3_lmap;
     PinBuf stage, err_stage, first_host;  // first_host: mapped, the assembly writes the NAR index there
     hipEvent_t ev[EV_N] = {};
     // CAS ids run on side_stream, concurrently with the digest: both stages are bound by

@@ -35,6 +35,12 @@ std::atomic<int> g_profiling{0};
 // BLAKE3 group map built by the walk + assembly (1) or by k_b3_plan (0): test hook
 // cg_test_b3_fused_plan
 std::atomic<int> g_b3_fused_plan{CG_B3_FUSED_PLAN};
+#ifndef CG_B3_PACKED
+#define CG_B3_PACKED 1
+#endif
+// BLAKE3 leaves packed across chunks (k_b3_leaves, with the assembly-built map) or one
+// 64-leaf group per wave (k_b3_groups): test hook cg_test_b3_packed
+std::atomic<int> g_b3_packed{CG_B3_PACKED};
 
 int fail(int code, const std::string &msg) {
     t_err = msg;
@@ -401,13 +407,20 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
     // BLAKE3: the walk counts each NAR's 64-leaf groups and the assembly builds the group
     // map from them, so launch_blake3 needs no planning kernel of its own
     const bool b3_fuse = algo == CG_BLAKE3 && digest && g_b3_fused_plan.load(std::memory_order_relaxed);
-    if (b3_fuse && (rc = ws->nar_ngroups.ensure((n_nars + 1) * 4, "nar_ngroups"))) return rc;
+    if (b3_fuse && (rc = ws->nar_ngroups.ensure(2 * (n_nars + 1) * 4, "nar_ngroups"))) return rc;
     cg::B3PlanOut b3plan;
     if (b3_fuse) {
         b3plan.nar_ngroups = ws->nar_ngroups.as<uint32_t>();
         b3plan.group_base = ws->b3_gbase.as<uint64_t>();
         b3plan.gmap = ws->b3_gmap.as<uint32_t>();
         b3plan.bound = chunk_bound;
+        if (g_b3_packed.load(std::memory_order_relaxed)) {  // packed leaves (k_b3_leaves)
+            b3plan.lmap_cap = cg::blake3_leaf_wave_bound(total_len, chunk_bound);
+            if ((rc = ws->b3_lbase.ensure((chunk_bound + 1) * 8, "b3_lbase"))) return rc;
+            if ((rc = ws->b3_lmap.ensure(b3plan.lmap_cap * 4, "b3_lmap"))) return rc;
+            b3plan.leaf_base = ws->b3_lbase.as<uint64_t>();
+            b3plan.lmap = ws->b3_lmap.as<uint32_t>();
+        }
     }
     cg::launch_walk(d_data, ws->gear.as<uint64_t>(), ws->entries.as<uint64_t>(), ws->eoff.as<uint64_t>(), nseg,
                     d_nar_off, d_cap_base, n_nars, P, ws->wchunk.as<uint64_t>(),
@@ -463,7 +476,7 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
         cg::launch_blake3(d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, total_len, hash_base,
                           sizeof(cg_desc), ws->b3_gmap.as<uint32_t>(), ws->b3_gbase.as<uint64_t>(),
                           ws->b3_gcount.as<uint32_t>(), ws->scan_tmp.as<uint64_t>(), ws->b3_gcv.as<uint32_t>(), true,
-                          st, b3_planned);
+                          st, b3_planned, b3_planned ? b3plan.leaf_base : nullptr, b3plan.lmap);
     }
     if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_DIGEST], st));
     if (d_chunk_ids) HIP_TRY(hipStreamWaitEvent(st, ws->ev_join, 0));
@@ -882,6 +895,10 @@ uint32_t cg_test_fail_alloc(uint32_t n) { return cgrt::g_fail_alloc.exchange(n);
 // Test hook: BLAKE3 group map from the walk + assembly (1) or from k_b3_plan (0); returns
 // the previous setting.
 int cg_test_b3_fused_plan(int on) { return cgrt::g_b3_fused_plan.exchange(on ? 1 : 0); }
+
+// Test hook: BLAKE3 leaves packed across chunks (1) or one group per wave (0); returns the
+// previous setting.
+int cg_test_b3_packed(int on) { return cgrt::g_b3_packed.exchange(on ? 1 : 0); }
 
 const char *cg_last_error_message(void) { return t_err.c_str(); }
 

@@ -370,13 +370,23 @@ __global__ __launch_bounds__(64) void k_walk(const uint8_t *__restrict__ data, c
         __syncthreads();
     }
     if (lane == 0) nar_nchunks[nar] = (uint32_t)k;
-    if (nar_ngroups) {  // BLAKE3 batches: the NAR's 64-leaf groups, for the fused group map (k_assemble_counts)
+    if (nar_ngroups) {  // BLAKE3 batches: the NAR's 64-leaf groups and leaves, for the fused maps (k_assemble_counts)
         __syncthreads();  // out[] lengths written by lane 0 / other lanes are read below
-        uint32_t ng = 0;
-        for (uint64_t j = lane; j < k; j += 64) ng += b3_groups_of_len(ld_l2(out + 2 * j + 1));
+        uint32_t ng = 0, nl = 0;
+        for (uint64_t j = lane; j < k; j += 64) {
+            const uint64_t len = ld_l2(out + 2 * j + 1);
+            ng += b3_groups_of_len(len);
+            nl += b3_leaves_of_len(len);
+        }
 #pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) ng += (uint32_t)__shfl_xor((int)ng, d, 64);
-        if (lane == 0) nar_ngroups[nar] = ng;
+        for (int d = 32; d >= 1; d >>= 1) {
+            ng += (uint32_t)__shfl_xor((int)ng, d, 64);
+            nl += (uint32_t)__shfl_xor((int)nl, d, 64);
+        }
+        if (lane == 0) {
+            nar_ngroups[nar] = ng;
+            nar_ngroups[n_nars + 1 + nar] = nl;
+        }
     }
 }
 
@@ -435,10 +445,11 @@ __global__ __launch_bounds__(64) void k_assemble_counts(const uint64_t *__restri
     const uint64_t i = blockIdx.x;
     if (i >= n_nars) return;
     const uint32_t lane = threadIdx.x;
-    uint64_t pre = 0, pre_g = 0;
+    uint64_t pre = 0, pre_g = 0, pre_l = 0;
     for (uint64_t j = lane; j < i; j += 64) {
         pre += nar_nchunks[j];
         if (b3.group_base) pre_g += b3.nar_ngroups[j];
+        if (b3.leaf_base) pre_l += b3.nar_ngroups[n_nars + 1 + j];
     }
     pre = wave_sum_u64(pre);
     const uint64_t first = pre, cnt = nar_nchunks[i];
@@ -482,6 +493,26 @@ __global__ __launch_bounds__(64) void k_assemble_counts(const uint64_t *__restri
         run += (uint32_t)__shfl((int)inc, 63, 64);
     }
     if (i == n_nars - 1 && lane == 0 && first + cnt <= b3.bound) b3.group_base[first + cnt] = run;
+    if (!b3.leaf_base) return;
+    // packed leaves: leaf_base[g] for g <= bound, lmap[w] = g for every wave w whose first
+    // slot 64 w lies in chunk g's leaves
+    uint64_t run_l = wave_sum_u64(pre_l);
+    for (uint64_t kb = 0; kb < cnt; kb += 64) {
+        const uint64_t k = kb + lane, g = first + k;
+        const uint32_t lc = k < cnt ? b3_leaves_of_len(w[2 * k + 1]) : 0u;
+        uint32_t inc = lc;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t t = (uint32_t)__shfl_up((int)inc, d, 64);
+            if (lane >= (uint32_t)d) inc += t;
+        }
+        const uint64_t lb = run_l + inc - lc;
+        if (k < cnt && g <= b3.bound) b3.leaf_base[g] = lb;
+        if (k < cnt && g < b3.bound)
+            for (uint64_t wv = (lb + 63) / 64; wv * 64 < lb + lc && wv < b3.lmap_cap; ++wv) b3.lmap[wv] = (uint32_t)g;
+        run_l += (uint32_t)__shfl((int)inc, 63, 64);
+    }
+    if (i == n_nars - 1 && lane == 0 && first + cnt <= b3.bound) b3.leaf_base[first + cnt] = run_l;
 }
 
 bool launch_assemble(const uint64_t *d_nar_off, const uint64_t *d_cap_base, const uint64_t *d_wchunk,

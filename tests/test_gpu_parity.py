@@ -626,17 +626,24 @@ def test_scan_paths_agree(ca, O, path):
         ca.lib.cg_test_scan_path(old)
 
 
-@pytest.mark.parametrize("fused", [1, 0], ids=["assembly_map", "plan_kernel"])
-def test_blake3_group_map_paths(ca, O, fused):
+@pytest.mark.parametrize("fused,packed", [(1, 1), (1, 0), (0, 0)], ids=["packed_leaves", "assembly_map", "plan_kernel"])
+def test_blake3_group_map_paths(ca, O, fused, packed):
     """The BLAKE3 group map (group_base / gmap) comes from the walk + descriptor assembly
-    (each NAR's group count, k_assemble_counts) or from k_b3_plan (cg_test_b3_fused_plan):
-    both give the oracle's digests on ragged NARs (empty ones, sub-leaf chunks, chunks of
-    1 .. 256 groups: max 16 MiB on zeros) and many-NAR batches."""
+    (each NAR's group count, k_assemble_counts) or from k_b3_plan (cg_test_b3_fused_plan),
+    and with the assembly's map the leaves run packed across chunks (k_b3_leaves,
+    cg_test_b3_packed) or one group per wave: every form gives the oracle's digests on
+    ragged NARs (empty ones, sub-leaf chunks, chunks of 1 .. 256 groups: max 16 MiB on
+    zeros; tiny chunks that put many chunks in one wave) and many-NAR batches."""
     rng = np.random.default_rng(57)
     lens = [0, 1, 1023, 1024, 1025, 65_536, 65_537, 0, 3_000_001, 131_072 * 3 + 5, 7]
     nars = [rng.integers(0, 256, n, dtype=np.uint8) for n in lens] + [np.zeros(40 << 20, np.uint8)]
     old = ca.lib.cg_test_b3_fused_plan(fused)
+    old_p = ca.lib.cg_test_b3_packed(packed)
     try:
+        tiny = [rng.integers(0, 256, int(n), dtype=np.uint8) for n in rng.integers(0, 5000, 300)]
+        got = ca.chunk_batch(tiny, 64, 256, 1024, hash=B3)
+        for i in (0, 1, 150, 299):
+            assert_same(got[i], O.chunk_descriptors(tiny[i], 64, 256, 1024, algo=B3), f"tiny nar{i}")
         for params in ((4096, 16384, 65536), (1 << 20, 4 << 20, 16 << 20)):
             got = ca.chunk_batch(nars, *params, hash=B3)
             for i, nar in enumerate(nars):
@@ -647,6 +654,7 @@ def test_blake3_group_map_paths(ca, O, fused):
             assert_same(got[i], O.chunk_descriptors(many[i], 4096, 16384, 65536, algo=B3), f"many nar{i}")
     finally:
         ca.lib.cg_test_b3_fused_plan(old)
+        ca.lib.cg_test_b3_packed(old_p)
 
 
 def test_blake3_group_map_capacity_error(ca):
