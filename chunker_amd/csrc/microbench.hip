@@ -159,6 +159,32 @@ extern "C" void cg_diag_b3_mode(uint32_t mode) { cg::g_b3_diag = mode; }
 // consumer timing: out[8*wg + {0,1,2,3}] = producer spin, producer total, consumer
 // spin, consumer total (shader clocks); + {4,5} consumer start/end (s_memrealtime,
 // 100 MHz), {6,7} consumer/producer wave location (HW_ID | XCC_ID << 32).  Diagnostics only.
+namespace cg {
+extern unsigned long long *g_walk_diag;
+}
+// Per-NAR k_walk phase clocks (8 u64 per NAR, see walk.hip): n = 0 disarms, out = NULL
+// arms a zeroed buffer for n NARs, else copies it out after a device sync.
+extern "C" int cg_diag_walk_stats(uint32_t n, unsigned long long *out) {
+    static unsigned long long *buf = nullptr;
+    static uint32_t cap = 0;
+    if (n == 0) {
+        cg::g_walk_diag = nullptr;
+        return 0;
+    }
+    if (out == nullptr) {
+        if (n > cap) {
+            if (buf) (void)hipFree(buf);
+            if (hipMalloc(&buf, (size_t)n * 64) != hipSuccess) return 2;
+            cap = n;
+        }
+        (void)hipMemset(buf, 0, (size_t)n * 64);
+        cg::g_walk_diag = buf;
+        return 0;
+    }
+    (void)hipDeviceSynchronize();
+    return hipMemcpy(out, buf, (size_t)n * 64, hipMemcpyDeviceToHost) == hipSuccess ? 0 : 2;
+}
+
 extern "C" int cg_diag_sha_stats(uint32_t n_wg, unsigned long long *out) {
     static unsigned long long *buf = nullptr;
     static uint32_t cap = 0;

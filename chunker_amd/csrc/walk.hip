@@ -246,13 +246,25 @@ __global__ __launch_bounds__(64) void k_walk_pieces(const uint8_t *__restrict__ 
 // chunk.  Both produce the crate's cut sequence exactly.  With piece lists (wp.np,
 // spec only) the walk takes whole runs of chunks from them (k_walk_pieces); they come
 // from the same candidate-list walk, so the verification below covers them too.
+#ifdef CG_DIAG
+// diagnostics build: per-NAR walk phase clocks {walk, verify, chunks, piece runs, re-walks,
+// piece-search, piece-copy, chunk_len} (cg_diag_walk_stats)
+unsigned long long *g_walk_diag = nullptr;
+#define WALK_DIAG(expr) expr
+#else
+#define WALK_DIAG(expr)
+#endif
+
 __global__ __launch_bounds__(64) void k_walk(const uint8_t *__restrict__ data, const uint64_t *__restrict__ gear_g,
                                              const uint64_t *__restrict__ entries,
                                              const uint64_t *__restrict__ eoff, uint64_t nseg,
                                              const uint64_t *__restrict__ nar_off,
                                              const uint64_t *__restrict__ cap_base, uint64_t n_nars, CdcParams P,
                                              uint64_t *__restrict__ wchunk, uint32_t *__restrict__ nar_nchunks,
-                                             int spec, WalkPieces wp, uint32_t *__restrict__ nar_ngroups) {
+                                             int spec, WalkPieces wp, uint32_t *__restrict__ nar_ngroups,
+                                             unsigned long long *__restrict__ wdiag) {
+    unsigned long long t_walk = 0, t_ver = 0, t_srch = 0, t_copy = 0, t_len = 0, n_runs = 0, t0 = 0, t1 = 0;
+    (void)t_walk, (void)t_ver, (void)t_srch, (void)t_copy, (void)t_len, (void)n_runs, (void)t0, (void)t1;
     __shared__ uint64_t gear[256];
     for (uint32_t i = threadIdx.x; i < 256; i += 64) gear[i] = gear_g[i];
     __syncthreads();
@@ -271,6 +283,7 @@ __global__ __launch_bounds__(64) void k_walk(const uint8_t *__restrict__ data, c
     uint32_t rewalks = 0;
     bool exact = spec == 0;
     for (;;) {
+        WALK_DIAG(if (wdiag) t0 = __builtin_amdgcn_s_memtime());
         const uint64_t k_start = k;
         uint64_t cur = ~0ull, ci = 0;  // piece being searched, and the search cursor in its list
         uint64_t wbase = ~0ull, wv = ~0ull;  // the 64 list entries from wbase, one per lane
@@ -289,6 +302,7 @@ __global__ __launch_bounds__(64) void k_walk(const uint8_t *__restrict__ data, c
                 // c among the piece's recorded starts (sorted) from the cursor on, 64 per
                 // wave-load, the loaded window kept while the cursor stays inside it
                 uint64_t hit = NONE;
+                WALK_DIAG(if (wdiag) t1 = __builtin_amdgcn_s_memtime());
                 while (ci < m) {
                     const uint64_t blk = ci & ~63ull;
                     if (blk != wbase) {
@@ -308,6 +322,7 @@ __global__ __launch_bounds__(64) void k_walk(const uint8_t *__restrict__ data, c
                     }
                     ci = blk + 64;
                 }
+                WALK_DIAG(if (wdiag) { const unsigned long long t = __builtin_amdgcn_s_memtime(); t_srch += t - t1; t1 = t; });
                 if (hit != NONE) {  // the rest of the piece's list is the NAR's sequence
                     const uint64_t ex = wp.exit[pg];
                     for (uint64_t t = hit; t < m; t += 64) {
@@ -320,6 +335,7 @@ __global__ __launch_bounds__(64) void k_walk(const uint8_t *__restrict__ data, c
                     }
                     k += m - hit;
                     c = ex;
+                    WALK_DIAG(if (wdiag) { t_copy += __builtin_amdgcn_s_memtime() - t1; ++n_runs; });
                     seek = true;  // the entry window is behind c now
                     continue;
                 }
@@ -328,7 +344,9 @@ __global__ __launch_bounds__(64) void k_walk(const uint8_t *__restrict__ data, c
                 win_seek(w, entries, n_entries, eoff, c, lane);
                 seek = false;
             }
+            WALK_DIAG(if (wdiag) t1 = __builtin_amdgcn_s_memtime());
             const uint64_t len = chunk_len(data, gear, w, entries, n_entries, c, end, P, exact, lane);
+            WALK_DIAG(if (wdiag) t_len += __builtin_amdgcn_s_memtime() - t1);
             if (lane == 0) {
                 out[2 * k] = c;
                 out[2 * k + 1] = len;
@@ -336,6 +354,7 @@ __global__ __launch_bounds__(64) void k_walk(const uint8_t *__restrict__ data, c
             ++k;
             c += len;
         }
+        WALK_DIAG(if (wdiag) { t1 = __builtin_amdgcn_s_memtime(); t_walk += t1 - t0; });
         if (exact) break;
         // verify warm-ups of chunks [k_start, k): lane i takes chunk k_start + i + 64t
         __syncthreads();  // out[] written by other lanes is read below
@@ -359,6 +378,7 @@ __global__ __launch_bounds__(64) void k_walk(const uint8_t *__restrict__ data, c
                 bad_cut = rd_u64(my_cut, L);
             }
         }
+        WALK_DIAG(if (wdiag) t_ver += __builtin_amdgcn_s_memtime() - t1);
         if (bad == NONE) break;
         // chunk `bad` really ends at bad_cut: fix it and re-walk from there
         const uint64_t cb = rd_u64(lane == 0 ? ld_l2(out + 2 * bad) : 0ull, 0);
@@ -370,6 +390,10 @@ __global__ __launch_bounds__(64) void k_walk(const uint8_t *__restrict__ data, c
         __syncthreads();
     }
     if (lane == 0) nar_nchunks[nar] = (uint32_t)k;
+    WALK_DIAG(if (wdiag && lane == 0) {
+        unsigned long long *d = wdiag + 8 * nar;
+        d[0] = t_walk; d[1] = t_ver; d[2] = k; d[3] = n_runs; d[4] = rewalks; d[5] = t_srch; d[6] = t_copy; d[7] = t_len;
+    });
     if (nar_ngroups) {  // BLAKE3 batches: the NAR's 64-leaf groups and leaves, for the fused maps (k_assemble_counts)
         __syncthreads();  // out[] lengths written by lane 0 / other lanes are read below
         uint32_t ng = 0, nl = 0;
@@ -402,7 +426,13 @@ void launch_walk(const uint8_t *d_data, const uint64_t *d_gear, const uint64_t *
         hipLaunchKernelGGL(k_walk_pieces, dim3((uint32_t)wp.np), dim3(64), 0, st, d_data, d_gear, d_entries, d_eoff,
                            nseg, d_nar_off, p, wp);
     hipLaunchKernelGGL(k_walk, dim3((uint32_t)n_nars), dim3(64), 0, st, d_data, d_gear, d_entries, d_eoff, nseg,
-                       d_nar_off, d_cap_base, n_nars, p, d_wchunk, d_nar_nchunks, spec, wp, d_nar_ngroups);
+                       d_nar_off, d_cap_base, n_nars, p, d_wchunk, d_nar_nchunks, spec, wp, d_nar_ngroups,
+#ifdef CG_DIAG
+                       g_walk_diag
+#else
+                       nullptr
+#endif
+    );
 }
 
 // One wave per NAR: copy the walker's (abs offset, length) list into the caller's
