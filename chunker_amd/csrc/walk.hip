@@ -69,34 +69,54 @@ __device__ __forceinline__ uint64_t warmup_exact(const uint8_t *__restrict__ dat
 }
 
 // The same warm-up for one chunk on ONE lane (the speculative walk's verification,
-// one lane per chunk): first cut among the n <= 47 positions from s, or NONE.  The
-// bytes come in as 13 dword loads issued together (one memory round trip; byte loads
-// in the hash loop would make it 47 dependent ones), never reading at or past `lim`.
-__device__ __forceinline__ uint64_t warmup_lane(const uint8_t *__restrict__ data, const uint64_t *gear, uint64_t s,
-                                                uint32_t n, uint64_t lim, uint64_t cs, const CdcParams &P) {
-    const uint64_t a0 = s & ~3ull;
-    const uint32_t sh = (uint32_t)(s - a0);
-    const uint32_t *q = reinterpret_cast<const uint32_t *>(data + a0);
+// one lane per chunk), in two halves so a lane can hold several chunks' loads in
+// flight at once.  warm_load: the 13 dwords covering [s, s + 52), never reading at
+// or past `lim` (one memory round trip; byte loads in the hash would make it 47
+// dependent ones).  warm_cut: first cut among the n <= 47 positions from s (the
+// first n_s of them under mask_s), or NONE -- branch-free, so the 47 gear lookups
+// issue back to back instead of one LDS round trip per byte.
+#ifndef CG_VERIFY_U
+#define CG_VERIFY_U 4  // chunks per lane per verification pass
+#endif
+struct WarmWin {
     uint32_t w[13];
+    uint64_t s;
+    uint32_t n, n_s;
+};
+__device__ __forceinline__ void warm_load(WarmWin &v, const uint8_t *__restrict__ data, uint64_t s, uint32_t n,
+                                          uint32_t n_s, uint64_t lim) {
+    v.s = s;
+    v.n = n;
+    v.n_s = n_s;
+    const uint64_t a0 = s & ~3ull;
+    const uint32_t *q = reinterpret_cast<const uint32_t *>(data + a0);
 #pragma unroll
-    for (int i = 0; i < 13; ++i) w[i] = a0 + 4 * i + 4 <= lim ? q[i] : 0u;
-    if (a0 + 52 > lim) {  // the NAR's last bytes: finish the partial dword byte by byte
+    for (int i = 0; i < 13; ++i) v.w[i] = n && a0 + 4 * i + 4 <= lim ? q[i] : 0u;
+    if (n && a0 + 52 > lim) {  // the NAR's last bytes: finish the partial dword byte by byte
         const uint64_t full = (lim - a0) / 4;
         if (full < 13) {
-            uint32_t v = 0;
-            for (uint64_t b = a0 + 4 * full; b < lim; ++b) v |= (uint32_t)data[b] << (8 * (uint32_t)(b & 3));
-            w[full] = v;  // dynamic index: rare path
+            uint32_t x = 0;
+            for (uint64_t b = a0 + 4 * full; b < lim; ++b) x |= (uint32_t)data[b] << (8 * (uint32_t)(b & 3));
+#pragma unroll
+            for (uint32_t i = 0; i < 13; ++i)
+                if (i == full) v.w[i] = x;  // static indices keep w[] in registers
         }
     }
-    uint64_t h = 0;
+}
+__device__ __forceinline__ uint64_t warm_cut(const WarmWin &v, const uint64_t *gear, const CdcParams &P) {
+    const uint32_t sh = (uint32_t)(v.s & 3u);
+    uint32_t a[12];  // the window realigned to s
+#pragma unroll
+    for (int i = 0; i < 12; ++i) a[i] = __builtin_amdgcn_alignbyte(v.w[i + 1], v.w[i], sh);
+    uint64_t h = 0, hits = 0;
 #pragma unroll
     for (uint32_t i = 0; i < 47; ++i) {
-        const uint32_t j = sh + i;  // byte j of the dword window
-        const uint32_t byte = (w[j >> 2] >> (8 * (j & 3))) & 0xffu;
-        h = (h << 1) + gear[byte];
-        if (i < n && (h & (s + i < cs ? P.mask_s : P.mask_l)) == 0) return s + i;
+        h = (h << 1) + gear[(a[i >> 2] >> (8 * (i & 3))) & 0xffu];
+        const uint64_t m = i < v.n_s ? P.mask_s : P.mask_l;
+        hits |= (uint64_t)((h & m) == 0) << i;
     }
-    return NONE;
+    hits &= v.n >= 64 ? ~0ull : (1ull << v.n) - 1;
+    return hits ? v.s + (uint64_t)__builtin_ctzll(hits) : NONE;
 }
 
 // Windowed (48-byte) hash verdict for positions [lo, hi) of a dense segment,
@@ -356,26 +376,44 @@ __global__ __launch_bounds__(64) void k_walk(const uint8_t *__restrict__ data, c
         }
         WALK_DIAG(if (wdiag) { t1 = __builtin_amdgcn_s_memtime(); t_walk += t1 - t0; });
         if (exact) break;
-        // verify warm-ups of chunks [k_start, k): lane i takes chunk k_start + i + 64t
+        // verify warm-ups of chunks [k_start, k): lane i takes chunks b + i + 64u, u < VU,
+        // all VU chunks' loads in flight together
         __syncthreads();  // out[] written by other lanes is read below
         uint64_t bad = NONE, bad_cut = 0;
-        for (uint64_t b = k_start; b < k && bad == NONE; b += 64) {
-            const uint64_t j = b + lane;
-            uint64_t my_cut = NONE;
-            if (j < k) {
-                const uint64_t cj = ld_l2(out + 2 * j);
-                const uint64_t rem = end - cj;
-                if (rem > P.min) {
-                    const Geo g = geometry(cj, rem, P);
-                    const uint64_t wend = g.s + 47 < g.ce ? g.s + 47 : g.ce;
-                    my_cut = warmup_lane(data, gear, g.s, (uint32_t)(wend - g.s), end, g.cs, P);
-                }
+        constexpr uint32_t VU = CG_VERIFY_U;
+        for (uint64_t b = k_start; b < k && bad == NONE; b += 64 * VU) {
+            uint64_t cj[VU];
+#pragma unroll
+            for (uint32_t u = 0; u < VU; ++u) {
+                const uint64_t j = b + 64 * u + lane;
+                cj[u] = j < k ? ld_l2(out + 2 * j) : end;
             }
-            const uint64_t bal = __ballot(my_cut != NONE);
-            if (bal) {
-                const int L = __builtin_ctzll(bal);
-                bad = b + (uint64_t)L;
-                bad_cut = rd_u64(my_cut, L);
+            WarmWin v[VU];
+#pragma unroll
+            for (uint32_t u = 0; u < VU; ++u) {
+                const uint64_t rem = end - cj[u];
+                uint32_t n = 0, n_s = 0;
+                uint64_t s = cj[u];
+                if (rem > P.min) {
+                    const Geo g = geometry(cj[u], rem, P);
+                    const uint64_t wend = g.s + 47 < g.ce ? g.s + 47 : g.ce;
+                    s = g.s;
+                    n = (uint32_t)(wend - g.s);
+                    n_s = g.cs > g.s ? (uint32_t)(g.cs - g.s < 47 ? g.cs - g.s : 47) : 0;
+                }
+                warm_load(v[u], data, s, n, n_s, end);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < VU; ++u) {
+                if (b + 64 * u >= k) break;  // uniform
+                const uint64_t my_cut = warm_cut(v[u], gear, P);
+                const uint64_t bal = __ballot(my_cut != NONE);
+                if (bal) {
+                    const int L = __builtin_ctzll(bal);
+                    bad = b + 64 * u + (uint64_t)L;
+                    bad_cut = rd_u64(my_cut, L);
+                    break;
+                }
             }
         }
         WALK_DIAG(if (wdiag) t_ver += __builtin_amdgcn_s_memtime() - t1);
