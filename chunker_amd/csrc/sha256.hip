@@ -578,6 +578,9 @@ __device__ void split_consumer(uint32_t (*sW)[64 * PC_ROW], uint32_t row, bool h
         *t_spin += wait_ready(s_ready, 0, timed);
         load_w8(wA, &sW[0][off]);
         spl_z(z, st[3], wA[0].x);
+        // block 0's words are all in before the loop: the compiler's wait for them would
+        // otherwise sit at the loop head, an LDS round trip on every iteration
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     }
     for (uint32_t k = 0; k < NB; k += 2) {
         sha_rounds_split<QUAD>(st, wA, wB, &sW[(k + 1) % PC_RING][off], k + 1, k + 1 < NB, s_ready, k < nbt, c, z);
@@ -701,6 +704,7 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
         uint4 wA[16], wB[16];
         t_spin += wait_ready(&s_ready, 0, diag != nullptr);
         load_w(wA, &sW[0][lane * PC_ROW]);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): as in split_consumer, keep the wait out of the loop head
         // Every lane runs every block's rounds (lanes whose chunk is done work on stale
         // words and keep their state by select): with part of the wave masked off, the
         // dependent round chain ran up to 1.7x slower per round on gfx950.
