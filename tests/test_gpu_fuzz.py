@@ -5,6 +5,8 @@ index written into mapped host memory, host tables through the stage-in kernel, 
 BLAKE3 group map from the assembly) and the host entry; every NAR bit-exact vs the oracle.
 In the spirit of the reference's tests/proptest_suite.rs and fuzz/fuzz_targets/chunking.rs.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -27,7 +29,8 @@ def O():
     return oracle
 
 
-@pytest.mark.parametrize("seed", range(96))
+# CHUNKER_AMD_FUZZ_SEEDS widens the sweep for a dedicated run (profiles/r03_v36_fuzz_*)
+@pytest.mark.parametrize("seed", range(int(os.environ.get("CHUNKER_AMD_FUZZ_SEEDS", "96"))))
 def test_fuzz_device_batches(ca, O, seed):
     import torch
 
