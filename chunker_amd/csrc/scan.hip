@@ -464,13 +464,19 @@ void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint
                            mask_l, cap, d_seg_count, d_seg_cand, nseg);
         return;
     }
-    // segments per wave: 4..32 -- two or more waves per SIMD-slot on 256 CUs at 1 GiB, and runs
-    // of at most 128 KiB, so that the waves in flight (one stream each, advancing together)
-    // stay within a window of ~0.5 GiB rather than spread at a power-of-two stride of several
-    // MiB (measured: 4 MiB runs at config 4 read ~20 % slower; 256 KiB runs 2-5 % slower
-    // than 128 KiB at configs 2 and 5)
+    // segments per wave: 4..32 below 4 GiB (two dispatch rounds of waves at 1 GiB, runs of at
+    // most 128 KiB: 256 KiB runs were 2-5 % slower at configs 2 and 5 in round 2), 64 from
+    // 4 GiB on -- runs short enough that the waves in flight (one stream each, advancing
+    // together) stay within a window of ~1 GiB rather than spread at a power-of-two stride
+    // of several MiB (4 MiB runs at config 4 read ~20 % slower).  Same box, alternating
+    // builds (profiles/r03_v37_ab_scan_runs.txt): 256 KiB runs read the 16 GiB configs 4 / 5
+    // in 3.63 / 3.76 ms against 3.76 / 3.85 for 128 KiB (5 and 3 pairs); 64 KiB runs 3-5 %
+    // slower, 512 KiB mixed; config 3's 1 GiB equal within the box's spread
     uint64_t spw = (nseg + 4095) / 4096;
-    uint64_t spw_max = 32;
+#ifndef CG_SCAN_SPW_MAX
+#define CG_SCAN_SPW_MAX (nseg >= (1ull << 20) ? 64 : 32)
+#endif
+    uint64_t spw_max = CG_SCAN_SPW_MAX;
 #ifdef CG_DIAG
     if (g_scan_spw_max) spw_max = g_scan_spw_max;
 #endif
