@@ -334,6 +334,18 @@ __device__ __forceinline__ uint32_t w_at(const uint4 (&W)[8]) {
         return W[I >> 2].w;
 }
 
+// Every instruction of a round is 8 bytes; the s_nop hipcc puts between asm statements
+// (4 bytes) would leave every other 8-round statement at 4 mod 8 -- so each starts on an
+// 8-byte boundary (one more s_nop when needed).
+#ifndef CG_SHA_ALIGN
+#define CG_SHA_ALIGN 1
+#endif
+#if CG_SHA_ALIGN
+#define RALIGN ".p2align 3\n\t"
+#else
+#define RALIGN ""
+#endif
+
 // One split round as asm text, registers named by role: A = X0 (newest) .. D = X3;
 // the new X0 is written into D.  ZOP prepares the next round's Z.
 #define SR(A, B, C, D, ZOP)                                                               \
@@ -352,7 +364,7 @@ __device__ __forceinline__ uint32_t w_at(const uint4 (&W)[8]) {
 #define ZHI(C, W) "v_add_u32_dpp %[z], %[" #W "], %[" #C "] row_shl:4 row_mask:0xf bank_mask:0x5\n\t"
 #define ZNONE "s_nop 0\n\t"
 #define SR8_HEAD                                                                       \
-    SR(x0, x1, x2, x3, ZHI(x2, w0)) SR(x3, x0, x1, x2, ZLO(x1, w1)) SR(x2, x3, x0, x1, ZHI(x0, w1)) \
+    RALIGN SR(x0, x1, x2, x3, ZHI(x2, w0)) SR(x3, x0, x1, x2, ZLO(x1, w1)) SR(x2, x3, x0, x1, ZHI(x0, w1)) \
     SR(x1, x2, x3, x0, ZLO(x3, w2)) SR(x0, x1, x2, x3, ZHI(x2, w2)) SR(x3, x0, x1, x2, ZLO(x1, w3)) \
     SR(x2, x3, x0, x1, ZHI(x0, w3))
 #define SR8_OUTS                                                                                                 \
@@ -393,7 +405,7 @@ __device__ __forceinline__ void spl_round8(uint32_t &x0, uint32_t &x1, uint32_t 
     "v_add_u32_dpp %[" #D "], %[" #D "], %[p] row_shl:4 row_mask:0xf bank_mask:0x5\n\t"   \
     ZOP "v_add_u32_dpp %[" #D "], %[p], %[p] row_shr:4 row_mask:0xf bank_mask:0xa\n\t"
 #define QR8_HEAD                                                                       \
-    QR(x0, x1, x2, x3, ZHI(x2, w0)) QR(x3, x0, x1, x2, ZLO(x1, w1)) QR(x2, x3, x0, x1, ZHI(x0, w1)) \
+    RALIGN QR(x0, x1, x2, x3, ZHI(x2, w0)) QR(x3, x0, x1, x2, ZLO(x1, w1)) QR(x2, x3, x0, x1, ZHI(x0, w1)) \
     QR(x1, x2, x3, x0, ZLO(x3, w2)) QR(x0, x1, x2, x3, ZHI(x2, w2)) QR(x3, x0, x1, x2, ZLO(x1, w3)) \
     QR(x2, x3, x0, x1, ZHI(x0, w3))
 #define QR8_OUTS                                                                                              \
