@@ -432,15 +432,16 @@ def e2e_rates(ca, torch, args, n_per, nar_bytes, params, algo, want):
 def sha_chain_floor(ca, descs, dig_ms):
     """The SHA-256 digest stage cannot end before the longest chunk's serial chain of
     64-round compressions has issued: blocks x 64 x (VALU per round x ~4.64 clocks,
-    lone-wave issue cost measured by scripts/diag_sha_split.py: 41.8 quad, 46.5 pair,
-    59.4 one-lane) at 2.4 GHz.  The tier is the one the library's last digest launch
+    lone-wave issue cost of the round code as built, measured by scripts/diag_sha_lone.py:
+    37.95 quad, 42.2 pair, 59.4 one-lane since the round asm is 8-byte aligned -- round 3
+    v39; 41.8 / 46.5 before) at 2.4 GHz.  The tier is the one the library's last digest launch
     gave the longest chunk (cg_last_sha_tiers: the length order hands the longest
     chunks to the quad workgroups first, then pairs, then one-lane workgroups)."""
     tiers = (np.ctypeslib.ctypes.c_uint32 * 4)()
     ca.lib.cg_last_sha_tiers(tiers)
     nquad, npair, nlane, pad = (int(t) for t in tiers)
     tier = "quad" if nquad else "pair" if npair else "one-lane"
-    cyc = {"quad": 41.8, "pair": 46.5, "one-lane": 59.4}[tier]
+    cyc = {"quad": 37.95, "pair": 42.2, "one-lane": 59.4}[tier]
     longest = int(descs["length"].max()) if len(descs) else 0
     blocks = (longest + 9 + 63) // 64
     floor_ms = blocks * 64 * cyc / 2.4e9 * 1e3
