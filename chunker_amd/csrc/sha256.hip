@@ -96,6 +96,7 @@ __device__ __forceinline__ void load_w(uint4 (&w)[16], const uint32_t *row) {
 // 64 rounds on `cur`; half-way through, once the producer has published block
 // `knext`, the next block's schedule is read from LDS into `nxt`, so its LDS
 // latency hides under the remaining 32 rounds.
+template <bool SEL>
 __device__ __forceinline__ void sha_rounds_pf(uint32_t st[8], const uint4 (&cur)[16], uint4 (&nxt)[16],
                                               const uint32_t *next_row, uint32_t knext, bool prefetch,
                                               const uint32_t *ready, bool active) {
@@ -116,6 +117,7 @@ __device__ __forceinline__ void sha_rounds_pf(uint32_t st[8], const uint4 (&cur)
     // not a branch, so the round code always runs under a full exec mask; the empty asm
     // stops the compiler from sinking the last rounds under an `active` branch)
     asm volatile("" : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(e), "+v"(f), "+v"(g), "+v"(h));
+    if (!SEL) active = true;  // every valid lane is inside its chunk (k_sha256's main loop)
     st[0] = active ? st[0] + a : st[0];
     st[1] = active ? st[1] + b : st[1];
     st[2] = active ? st[2] + c : st[2];
@@ -197,9 +199,11 @@ __device__ __forceinline__ unsigned long long wait_slot(const uint32_t *done, ui
     return timed ? __builtin_amdgcn_s_memtime() - t0 : 0ull;
 }
 // This wave's schedule writes for block k have landed: publish k + 1.
+// Every lane stores the same value (one ds_write, no exec-mask change around it).
 __device__ __forceinline__ void publish(uint32_t *ready, uint32_t k, uint32_t lane) {
+    (void)lane;
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-    if (lane == 0) lds_store_release(ready, k + 1);
+    lds_store_release(ready, k + 1);
 }
 
 // Words of a chunk's tail block (k == nb: tail bytes, 0x80, zeros, [bit length]) or
@@ -456,7 +460,7 @@ __device__ __forceinline__ void load_w8(uint4 (&w)[8], const uint32_t *row) {
 
 // 64 split rounds on `cur` (this lane's 32 schedule words); half-way through, once
 // the producer has published block `knext`, the next block's words are read into `nxt`.
-template <bool QUAD>
+template <bool QUAD, bool SEL = true>
 __device__ __forceinline__ void sha_rounds_split(uint32_t st[4], const uint4 (&cur)[8], uint4 (&nxt)[8],
                                                  const uint32_t *next_row, uint32_t knext, bool prefetch,
                                                  const uint32_t *ready, bool active, const SplitLane &c,
@@ -469,6 +473,7 @@ __device__ __forceinline__ void sha_rounds_split(uint32_t st[4], const uint4 (&c
     // inside a branch made the compiler drain lgkmcnt at the join, an LDS round trip per block
     load_w8(nxt, next_row);
     SPL32(32, cur)
+    if (!SEL) active = true;  // every valid lane is inside its chunk (split_consumer's main loop)
     st[0] = active ? st[0] + x0 : st[0];
     st[1] = active ? st[1] + x1 : st[1];
     st[2] = active ? st[2] + x2 : st[2];
@@ -563,7 +568,7 @@ __device__ unsigned long long sha_produce_pair(const uint8_t *p, uint64_t len, u
 // lane each) or quad (QUAD = true: the same banks, 4 lanes each) workgroup.
 template <bool QUAD>
 __device__ void split_consumer(uint32_t (*sW)[64 * PC_ROW], uint32_t row, bool hi, uint32_t lane, uint32_t NB,
-                               uint32_t nbt, uint32_t *s_ready, uint32_t *s_done, uint32_t st[4],
+                               uint32_t NBmin, uint32_t nbt, uint32_t *s_ready, uint32_t *s_done, uint32_t st[4],
                                unsigned long long *t_spin, bool timed) {
     SplitLane c;
     if (QUAD) {  // lanes 0-2 of a bank take one rotation each; lane 3 is idle garbage
@@ -594,7 +599,19 @@ __device__ void split_consumer(uint32_t (*sW)[64 * PC_ROW], uint32_t row, bool h
         // otherwise sit at the loop head, an LDS round trip on every iteration
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     }
-    for (uint32_t k = 0; k < NB; k += 2) {
+    uint32_t k = 0;
+    // blocks every valid lane's chunk still has: no per-lane select of the state
+    for (; k + 1 < NBmin; k += 2) {
+        sha_rounds_split<QUAD, false>(st, wA, wB, &sW[(k + 1) % PC_RING][off], k + 1, k + 1 < NB, s_ready, true, c,
+                                      z);
+        spl_z(z, st[3], wB[0].x);
+        publish(s_done, k, lane);
+        sha_rounds_split<QUAD, false>(st, wB, wA, &sW[(k + 2) % PC_RING][off], k + 2, k + 2 < NB, s_ready, true, c,
+                                      z);
+        spl_z(z, st[3], wA[0].x);
+        publish(s_done, k + 1, lane);
+    }
+    for (; k < NB; k += 2) {
         sha_rounds_split<QUAD>(st, wA, wB, &sW[(k + 1) % PC_RING][off], k + 1, k + 1 < NB, s_ready, k < nbt, c, z);
         spl_z(z, st[3], wB[0].x);
         publish(s_done, k, lane);
@@ -683,6 +700,8 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
     const uint32_t nbt = valid ? (uint32_t)(nb + (rem < 56 ? 1 : 2)) : 0u;  // blocks incl. padding
     // identical in both waves (same chunks); scalar, so the block loops are uniform
     const uint32_t NB = __builtin_amdgcn_readfirstlane(wave_max_u32(nbt));
+    // blocks every valid lane's chunk has (the consumers' select-free main loop)
+    const uint32_t NBmin = __builtin_amdgcn_readfirstlane(~wave_max_u32(valid ? ~nbt : 0u));
 
     if (producer) {
         const uint8_t *p = data + (valid ? abs[ci] : 0);
@@ -701,9 +720,9 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
     } else if (split) {
         uint32_t st[4];
         if (quad)
-            split_consumer<true>(sW, row, hi, lane, NB, nbt, &s_ready, &s_done, st, &t_spin, diag != nullptr);
+            split_consumer<true>(sW, row, hi, lane, NB, NBmin, nbt, &s_ready, &s_done, st, &t_spin, diag != nullptr);
         else
-            split_consumer<false>(sW, row, hi, lane, NB, nbt, &s_ready, &s_done, st, &t_spin, diag != nullptr);
+            split_consumer<false>(sW, row, hi, lane, NB, NBmin, nbt, &s_ready, &s_done, st, &t_spin, diag != nullptr);
         if (diag && lane == 0) sha_diag_consumer(diag, t_spin, t_start, rt_start);
         if (valid && (!quad || (lane & 3u) == 0)) {  // hi: H0..H3 (bytes 0-15), lo: H4..H7 (bytes 16-31)
             uint4 *o = reinterpret_cast<uint4 *>(hash_base + ci * stride + (hi ? 0 : 16));
@@ -720,17 +739,28 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
         // Every lane runs every block's rounds (lanes whose chunk is done work on stale
         // words and keep their state by select): with part of the wave masked off, the
         // dependent round chain ran up to 1.7x slower per round on gfx950.
-        for (uint32_t k = 0; k < NB; k += 2) {
+        uint32_t k = 0;
+        for (; k + 1 < NBmin; k += 2) {  // blocks every valid lane's chunk has: no select
+            sha_rounds_pf<false>(st, wA, wB, &sW[(k + 1) % PC_RING][lane * PC_ROW], k + 1, k + 1 < NB && mode != 2,
+                                 &s_ready, true);
+            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+            lds_store_release(&s_done, k + 1);
+            sha_rounds_pf<false>(st, wB, wA, &sW[(k + 2) % PC_RING][lane * PC_ROW], k + 2, k + 2 < NB && mode != 2,
+                                 &s_ready, true);
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            lds_store_release(&s_done, k + 2);
+        }
+        for (; k < NB; k += 2) {
             // block k from wA, block k+1's schedule prefetched into wB
-            sha_rounds_pf(st, wA, wB, &sW[(k + 1) % PC_RING][lane * PC_ROW], k + 1, k + 1 < NB && mode != 2,
+            sha_rounds_pf<true>(st, wA, wB, &sW[(k + 1) % PC_RING][lane * PC_ROW], k + 1, k + 1 < NB && mode != 2,
                           &s_ready, k < nbt);
             __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-            if (lane == 0) lds_store_release(&s_done, k + 1);
+            lds_store_release(&s_done, k + 1);
             if (k + 1 >= NB) break;
-            sha_rounds_pf(st, wB, wA, &sW[(k + 2) % PC_RING][lane * PC_ROW], k + 2, k + 2 < NB && mode != 2,
+            sha_rounds_pf<true>(st, wB, wA, &sW[(k + 2) % PC_RING][lane * PC_ROW], k + 2, k + 2 < NB && mode != 2,
                           &s_ready, k + 1 < nbt);
             __builtin_amdgcn_s_waitcnt(0xc07f);
-            if (lane == 0) lds_store_release(&s_done, k + 2);
+            lds_store_release(&s_done, k + 2);
         }
         if (diag && lane == 0) sha_diag_consumer(diag, t_spin, t_start, rt_start);
         if (valid) {
