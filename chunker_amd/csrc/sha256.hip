@@ -480,6 +480,42 @@ __device__ __forceinline__ void sha_rounds_split(uint32_t st[4], const uint4 (&c
     st[3] = active ? st[3] + x3 : st[3];
 }
 
+// Two blocks of split_consumer's select-free main loop (k even, every valid lane inside
+// its chunk): one readiness probe for both (the producer normally runs PC_RING - 1 blocks
+// ahead; a stale probe only sends the second block to wait_ready, which re-reads), the
+// ring rows addressed by the caller's toggled offsets instead of per-block slot
+// arithmetic, and no end-of-chunk guard on the prefetch (the producer publishes ~0 after
+// its last block).  A wave issues about one instruction per 4 clocks, so each one dropped
+// here counts like a VALU op of the round chain.
+template <bool QUAD>
+__device__ __forceinline__ void split_pair_main(uint32_t st[4], uint4 (&wA)[8], uint4 (&wB)[8], const uint32_t *rowB,
+                                                const uint32_t *rowA, uint32_t k, const uint32_t *ready,
+                                                uint32_t *done, uint32_t lane, const SplitLane &c, uint32_t &z) {
+    uint32_t x0 = st[0], x1 = st[1], x2 = st[2], x3 = st[3];
+    const uint32_t r0 = __hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    SPL32(0, wA)
+    if (__builtin_expect(r0 <= k + 1, 0)) wait_ready(ready, k + 1, false);
+    load_w8(wB, rowB);
+    SPL32(32, wA)
+    st[0] += x0;
+    st[1] += x1;
+    st[2] += x2;
+    st[3] += x3;
+    spl_z(z, st[3], wB[0].x);
+    publish(done, k, lane);
+    x0 = st[0], x1 = st[1], x2 = st[2], x3 = st[3];
+    SPL32(0, wB)
+    if (__builtin_expect(r0 <= k + 2, 0)) wait_ready(ready, k + 2, false);
+    load_w8(wA, rowA);
+    SPL32(32, wB)
+    st[0] += x0;
+    st[1] += x1;
+    st[2] += x2;
+    st[3] += x3;
+    spl_z(z, st[3], wA[0].x);
+    publish(done, k + 1, lane);
+}
+
 // Producer wave of a split workgroup.  The pair shares the message schedule by
 // parity: lo lanes own the even words w[2i], hi lanes the odd words w[2i+1].  In
 //   w[t] = s1(w[t-2]) + w[t-16] + (w[t-7] + s0(w[t-15]))
@@ -561,6 +597,7 @@ __device__ unsigned long long sha_produce_pair(const uint8_t *p, uint64_t len, u
         }
         publish(s_ready, k, lane);
     }
+    publish(s_ready, 0xfffffffeu, lane);  // ~0: every later block "ready" (split_pair_main's guard-free prefetch)
     return t_spin;
 }
 
@@ -600,16 +637,32 @@ __device__ void split_consumer(uint32_t (*sW)[64 * PC_ROW], uint32_t row, bool h
         __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     }
     uint32_t k = 0;
-    // blocks every valid lane's chunk still has: no per-lane select of the state
-    for (; k + 1 < NBmin; k += 2) {
-        sha_rounds_split<QUAD, false>(st, wA, wB, &sW[(k + 1) % PC_RING][off], k + 1, k + 1 < NB, s_ready, true, c,
-                                      z);
-        spl_z(z, st[3], wB[0].x);
-        publish(s_done, k, lane);
-        sha_rounds_split<QUAD, false>(st, wB, wA, &sW[(k + 2) % PC_RING][off], k + 2, k + 2 < NB, s_ready, true, c,
-                                      z);
-        spl_z(z, st[3], wA[0].x);
-        publish(s_done, k + 1, lane);
+    // blocks every valid lane's chunk still has: no per-lane select of the state.  Blocks
+    // k + 1 and k + 2 sit in ring slots (1, 2) and (3, 0) in turn: each row offset toggles
+    // by one subtraction from a constant.
+    static_assert(PC_RING == 4, "split_pair_main's slot toggling assumes a 4-slot ring");
+    constexpr uint32_t SLOT = 64 * PC_ROW;
+    const uint32_t *ring = &sW[0][0];
+    uint32_t oB = off + SLOT, oA = off + 2 * SLOT;
+    const uint32_t cB = 2 * off + 4 * SLOT, cA = 2 * off + 2 * SLOT;
+    if constexpr (QUAD) {  // (the pair tier measured faster with the per-block body below)
+        for (; k + 1 < NBmin; k += 2) {
+            split_pair_main<QUAD>(st, wA, wB, ring + oB, ring + oA, k, s_ready, s_done, lane, c, z);
+            oB = cB - oB;
+            oA = cA - oA;
+        }
+    } else {
+        (void)ring, (void)oB, (void)oA, (void)cB, (void)cA;
+        for (; k + 1 < NBmin; k += 2) {
+            sha_rounds_split<QUAD, false>(st, wA, wB, &sW[(k + 1) % PC_RING][off], k + 1, k + 1 < NB, s_ready, true,
+                                          c, z);
+            spl_z(z, st[3], wB[0].x);
+            publish(s_done, k, lane);
+            sha_rounds_split<QUAD, false>(st, wB, wA, &sW[(k + 2) % PC_RING][off], k + 2, k + 2 < NB, s_ready, true,
+                                          c, z);
+            spl_z(z, st[3], wA[0].x);
+            publish(s_done, k + 1, lane);
+        }
     }
     for (; k < NB; k += 2) {
         sha_rounds_split<QUAD>(st, wA, wB, &sW[(k + 1) % PC_RING][off], k + 1, k + 1 < NB, s_ready, k < nbt, c, z);
