@@ -75,6 +75,9 @@ def parse_args():
     ap.add_argument("--e2e", default="1,8,16", help="K values of the host-to-host in-flight measurement ('' = skip)")
     ap.add_argument("--hw-queues", type=int, default=16, choices=range(0, 33), metavar="0..32",
                     help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's)")
+    ap.add_argument("--no-clock", action="store_true", help="skip the digest clock measurement (scripts/sha_clock.py)")
+    ap.add_argument("--no-coalesce", action="store_true",
+                    help="concurrent callers digest their batches alone (cg_test_coalesce(0)); A/B of the coalescer")
     ap.add_argument("--dist-force", action="store_true",
                     help="run the N > 1 code (process group, gather to rank 0, rank-0 check) even at one rank: "
                          "rehearses the RCCL path on a one-GPU box")
@@ -130,10 +133,12 @@ def main():
         torch.cuda.set_device(0)
 
     import chunker_amd as ca
-    from chunker_amd.dist import check_gathered_batch, gather_batch, shard_nars
+    from chunker_amd.dist import check_gathered_batch, gather_batch, gather_batch_async, gather_shape, shard_nars
     from chunker_amd.nar import synth_nars_device
 
     n_per, nar_bytes, params, algo, desc = CONFIGS[args.config]
+    if args.no_coalesce:
+        ca.lib.cg_test_coalesce(0)
     if args.concurrent_only:
         print(json.dumps({"concurrent": concurrent_rates(ca, torch, args, n_per, nar_bytes, params, algo)}))
         return
@@ -142,24 +147,37 @@ def main():
     d_data, offs = synth_nars_device(sizes, zeros=args.zeros, first_index=mine.start)
     total_bytes = int(offs[-1])
     cap = ca.chunking.batch_capacity(offs, params[0])
+    # RCCL gather: fixed per-rank sizes agreed once here, so a step's gather needs no count
+    # exchange and no host sync (chunker_amd.dist.gather_batch_async)
+    gcap, gnars = gather_shape(cap, len(mine)) if multi and nccl else (cap, len(mine))
     # two output arrays, alternate steps: while step k's descriptors are gathered, step k + 1
-    # (already queued on the same stream) writes the other one
-    d_outs = [torch.empty(cap * 48, dtype=torch.uint8, device="cuda") for _ in range(2)]
-    stream = torch.cuda.current_stream()
-    sptr = stream.cuda_stream
-
+    # writes the other one
+    d_outs = [torch.empty(gcap * 48, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    # The batches run on a stream of their own.  The gather of step k is queued on torch's
+    # current stream (RCCL's stream waits for that one), which holds none of the batches, so
+    # it runs while step k + 1's kernels do instead of queueing behind them; an event after
+    # it holds back step k + 2, the next writer of the same output array.
+    bstream = torch.cuda.Stream()
+    sptr = bstream.cuda_stream
+    gathered_ev = [None, None]
     gathered = [None]
 
     def issue(k):
-        return ca.chunk_batch_device_async(d_data.data_ptr(), offs, d_outs[k % 2].data_ptr(), cap, *params,
+        ev = gathered_ev[k % 2]
+        if ev is not None:
+            bstream.wait_event(ev)
+        return ca.chunk_batch_device_async(d_data.data_ptr(), offs, d_outs[k % 2].data_ptr(), gcap, *params,
                                            hash=algo, stream=sptr)
 
     def complete(k, batch):
         first = batch.wait()
-        if multi:  # descriptors + NAR index to rank 0 over RCCL (the path's only exchange)
-            d_out = d_outs[k % 2]
-            mine_d = d_out if nccl else d_out[: int(first[-1]) * 48].cpu()
-            gathered[0] = gather_batch(mine_d, first)
+        if multi and nccl:  # descriptors + NAR index to rank 0 over RCCL (the path's only exchange)
+            gathered[0] = gather_batch_async(d_outs[k % 2], first, gcap, gnars)
+            ev = torch.cuda.Event()
+            ev.record()
+            gathered_ev[k % 2] = ev
+        elif multi:  # gloo rehearsal: host copies
+            gathered[0] = gather_batch(d_outs[k % 2][: int(first[-1]) * 48].cpu(), first)
         return first
 
     def step(k=0):  # one batch, waited for
@@ -198,7 +216,7 @@ def main():
         stage[k] = list(buf)
         pending = nxt
     last = (args.steps - 1) % 2
-    torch.cuda.synchronize()
+    torch.cuda.synchronize()  # every stream: the batches' and the last gather
     if multi:
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -224,7 +242,7 @@ def main():
     check_gathered_batch(descs, first, sizes)
     gather_check = None
     if multi and rank == 0:
-        g_desc, g_first = gathered[0]
+        g_desc, g_first = gathered[0].assemble() if nccl else gathered[0]
         g_np = g_desc.cpu().numpy().view(ca.DESC_DTYPE)
         check_gathered_batch(g_np, g_first, np.full(n_per * world, nar_bytes, np.uint64))
         gather_check = {"nars": n_per * world, "chunks": int(g_first[-1]), "backend": args.dist_backend,
@@ -253,7 +271,8 @@ def main():
                         "traffic": None},
     }
     if algo == 1:
-        roofline["latency_floor"] = sha_chain_floor(ca, descs, dig_ms)
+        clk = sha_clock(args) if world == 1 and not args.no_clock else None
+        roofline["latency_floor"] = sha_chain_floor(ca, descs, dig_ms, clk)
     dig_kernels = ["k_sha256"] if algo == 1 else ["k_b3_groups", "k_b3_fold", "k_b3_top"]
     traffic, src = pmc_traffic(args.config, dig_kernels)
     if traffic is not None:
@@ -329,8 +348,12 @@ def concurrent_rates(ca, torch, args, n_per, nar_bytes, params, algo):
         jobs.append((d, offs, out, cap, torch.cuda.Stream()))
     torch.cuda.synchronize()
     batch_bytes = int(jobs[0][1][-1])
+    coal = bool(ca.lib.cg_test_coalesce(1))
+    ca.lib.cg_test_coalesce(int(coal))
     res = {"unit": "GiB/s", "batch": f"{n_per}x{nar_bytes >> 20}MiB", "reps": 3,
-           "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default (4)")}
+           "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default (4)"),
+           "digests": "coalesced (one SHA-256 launch per group of concurrent callers)" if coal and algo == 1
+           else "one launch per batch"}
     for K in ks:
         for timed in (False, True):
             reps = res["reps"] if timed else 1
@@ -429,7 +452,19 @@ def e2e_rates(ca, torch, args, n_per, nar_bytes, params, algo, want):
     return res
 
 
-def sha_chain_floor(ca, descs, dig_ms):
+def sha_clock(args):
+    """The clock the digest's longest chain ran at (scripts/sha_clock.py: the diagnostics
+    build's per-workgroup shader-clock and wall-clock record of the same batch, in a child
+    process so this one keeps the product library only)."""
+    try:
+        r = subprocess.run([sys.executable, str(ROOT / "scripts" / "sha_clock.py"), "--config", args.config],
+                           capture_output=True, text=True, timeout=300)
+        return json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else None
+    except (subprocess.TimeoutExpired, ValueError, IndexError):
+        return None
+
+
+def sha_chain_floor(ca, descs, dig_ms, clk=None):
     """The SHA-256 digest stage cannot end before the longest chunk's serial chain of
     64-round compressions has issued: blocks x 64 x (VALU per round x ~4.64 clocks,
     lone-wave issue cost of the round code as built, measured by scripts/diag_sha_lone.py:
@@ -445,10 +480,18 @@ def sha_chain_floor(ca, descs, dig_ms):
     longest = int(descs["length"].max()) if len(descs) else 0
     blocks = (longest + 9 + 63) // 64
     floor_ms = blocks * 64 * cyc / 2.4e9 * 1e3
-    return {"longest_chunk_bytes": longest, "blocks": blocks, "tier": tier,
-            "workgroups": {"quad": nquad, "pair": npair, "one_lane": nlane, "lds_pad": pad},
-            "cycles_per_round": cyc, "clock_GHz": 2.4, "floor_ms": round(floor_ms, 3),
-            "frac": round(floor_ms / dig_ms, 4) if dig_ms else None}
+    res = {"longest_chunk_bytes": longest, "blocks": blocks, "tier": tier,
+           "workgroups": {"quad": nquad, "pair": npair, "one_lane": nlane, "lds_pad": pad},
+           "cycles_per_round": cyc, "clock_GHz": 2.4, "floor_ms": round(floor_ms, 3),
+           "frac": round(floor_ms / dig_ms, 4) if dig_ms else None}
+    if clk and clk.get("clock_GHz"):
+        # the same floor at the clock the longest chain ran at (scripts/sha_clock.py)
+        g = float(clk["clock_GHz"])
+        f = blocks * 64 * cyc / (g * 1e9) * 1e3
+        res["measured_clock"] = {"clock_GHz": g, "floor_ms": round(f, 3), "frac": round(f / dig_ms, 4) if dig_ms else None,
+                                 "cycles_per_round_in_place": clk.get("cycles_per_round_wg0"),
+                                 "source": "scripts/sha_clock.py (diagnostics build, same batch shape)"}
+    return res
 
 
 def scan_kernel_name(ca, avg):
@@ -489,7 +532,8 @@ def cpu_baseline(args, n_per, nar_bytes, params, algo):
       FastCDC scan, then per-chunk digests on a pool of `cores` threads (rayon's role)
       -- over the whole 1 GiB batch (c2/c3) or one 1 GiB NAR (c4/c5);
     * nar_parallel: the CPU upper bound, NARs spread over the same pool, one
-      single-threaded chunk_descriptors per NAR;
+      single-threaded chunk_descriptors per NAR, over at least one NAR per thread (for
+      c4/c5: `cores` NARs of 1 GiB, not the one-NAR sample);
     * config1: BASELINE config 1 (benches/throughput.rs:39-43), chunk_data on 10 MiB
       with payload copies (:265-296), D params, SHA-256, median of 7 runs, on zeros
       (the published bench's data, 1.055 GiB/s in benchmarks/latest.md:12) and on
@@ -514,13 +558,22 @@ def cpu_baseline(args, n_per, nar_bytes, params, algo):
         dts.append(time.perf_counter() - t0)
     dt = float(np.median(dts))
     nbytes = int(offs[-1])
+    # the NAR-parallel bound needs at least one NAR per thread: for the 1 GiB-NAR configs
+    # that is `nt` NARs of the config's size (the sample above is one)
+    par = nars
+    if len(par) < nt:
+        extra, eoffs = synth_nars(np.full(nt - len(par), nar_bytes, np.uint64), zeros=args.zeros, first_index=k)
+        par = par + [extra[int(eoffs[i]):int(eoffs[i + 1])] for i in range(nt - len(nars))]
+    par_bytes = sum(len(a) for a in par)
+    par_reps = reps if par_bytes <= (4 << 30) else 3
     with ThreadPoolExecutor(nt) as ex:
         dps = []
-        for _ in range(reps):
+        for _ in range(par_reps):
             t1 = time.perf_counter()
-            list(ex.map(lambda a: O.chunk_descriptors(a, *params, algo=algo, nthreads=1), nars))
+            list(ex.map(lambda a: O.chunk_descriptors(a, *params, algo=algo, nthreads=1), par))
             dps.append(time.perf_counter() - t1)
         dt_par = float(np.median(dps))
+    del par
 
     def chunk_data(buf):  # chunk_data_with_hash: descriptors + an owned payload copy per chunk
         return [(bytes(buf[int(d["offset"]):int(d["offset"] + d["length"])]), d)
@@ -545,7 +598,9 @@ def cpu_baseline(args, n_per, nar_bytes, params, algo):
             "sample": f"{k} NAR(s) ({nbytes / GIB:.3f} GiB) of the same workload, one chunk_descriptors call "
                       f"per NAR, median of {reps} passes, SHA-NI={'yes' if O.lib().or_sha256_uses_shani() else 'no'}",
             "seconds": round(dt, 3),
-            "nar_parallel": round(nbytes / dt_par / GIB, 4),
+            "nar_parallel": round(par_bytes / dt_par / GIB, 4),
+            "nar_parallel_sample": f"{max(k, nt)} NAR(s) of {nar_bytes >> 20} MiB, one single-threaded "
+                                   f"chunk_descriptors per NAR on {nt} threads, median of {par_reps}",
             "config1_chunk_data_10MiB_D_sha256": c1,
             "cpu_model": cpu_model()}
 

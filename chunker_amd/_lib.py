@@ -51,25 +51,12 @@ EXPORTS = (
 )
 # test hooks the product library exports beyond the header (tier caps, spin-guard limit)
 TEST_HOOKS = ("cg_test_sha_quad_max", "cg_test_sha_split_max", "cg_test_sha_spin_limit", "cg_test_cas_pair_max",
-              "cg_test_fail_alloc", "cg_test_sha_quad_fill", "cg_test_sha_pair_fill", "cg_test_scan_path",
+              "cg_test_fail_alloc", "cg_test_sha_quad_fill", "cg_test_sha_pair_fill", "cg_test_scan_path", "cg_test_scan_kernel", "cg_test_coalesce",
               "cg_test_stream_group_cap", "cg_test_stream_max_lanes", "cg_test_stream_eager",
               "cg_test_b3_fused_plan", "cg_test_b3_packed")
 
 
-def _hw_queues_default() -> None:
-    """HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default) and streams
-    sharing a queue serialise; the engine's concurrent callers and a ChunkStream's digest
-    lanes need more.  Like the Rust shim's `available()` (INTEGRATION.md
-    §3), ask for 16 unless the environment says otherwise.  HIP reads the variable when
-    it initialises, so this only takes effect if nothing in the process has touched the
-    GPU yet (importing torch does not)."""
-    import os
-
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
-
-
 def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
-    _hw_queues_default()
     # PyTorch-ROCm ships its own libamdhip64 (SONAME libamdhip64.so.7) and links it as
     # "libamdhip64.so".  Loading torch first makes our DT_NEEDED libamdhip64.so.7
     # resolve to that same copy, so one process never holds two HIP runtimes.
@@ -153,7 +140,7 @@ def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
     L.cg_tables_verified.restype = i
     u32 = ctypes.c_uint32
     for name in ("cg_test_sha_quad_max", "cg_test_sha_split_max", "cg_test_sha_spin_limit", "cg_test_sha_quad_fill",
-                 "cg_test_sha_pair_fill", "cg_test_scan_path"):
+                 "cg_test_sha_pair_fill", "cg_test_scan_path", "cg_test_scan_kernel", "cg_test_coalesce"):
         getattr(L, name).argtypes = [u32]
         getattr(L, name).restype = u32
     L.cg_test_cas_pair_max.argtypes = [ctypes.c_int64]

@@ -29,6 +29,7 @@ device-resident inputs): chunk_batch, chunk_batch_device.
 """
 from __future__ import annotations
 
+import asyncio
 import ctypes
 import enum
 import os
@@ -464,14 +465,26 @@ class PushChunker:
             self._h = None
 
 
+_USIZE_MAX = 2 ** 64 - 1
+
+
+def _parse_usize(s: str | None) -> int | None:
+    """Rust's `s.parse::<usize>().ok()`: ASCII decimal digits with an optional leading '+',
+    no whitespace, no '-', no '_', at most usize::MAX; anything else is None."""
+    if not s:
+        return None
+    body = s[1:] if s[0] == "+" else s
+    if not body or not all("0" <= ch <= "9" for ch in body):
+        return None
+    v = int(body)
+    return v if v <= _USIZE_MAX else None
+
+
 def effective_read_slice_cap() -> int:
     """src/chunking.rs:427-433."""
-    try:
-        v = int(os.environ.get("CHUNKER_READ_SLICE_CAP_BYTES", ""))
-        if MIN_READ_SLICE_CAP <= v <= MAX_READ_SLICE_CAP:
-            return v
-    except ValueError:
-        pass
+    v = _parse_usize(os.environ.get("CHUNKER_READ_SLICE_CAP_BYTES"))
+    if v is not None and MIN_READ_SLICE_CAP <= v <= MAX_READ_SLICE_CAP:
+        return v
     return DEFAULT_READ_SLICE_CAP
 
 
@@ -491,13 +504,8 @@ def stream_inflight_bytes() -> int:
     CHUNKER_AMD_STREAM_INFLIGHT_BYTES, default 2 GiB (the engine's own default).  The
     host keeps the same slices alive until their chunks are emitted (payloads are
     slices of them)."""
-    try:
-        v = int(os.environ.get("CHUNKER_AMD_STREAM_INFLIGHT_BYTES", ""))
-        if v > 0:
-            return v
-    except ValueError:
-        pass
-    return DEFAULT_STREAM_INFLIGHT
+    v = _parse_usize(os.environ.get("CHUNKER_AMD_STREAM_INFLIGHT_BYTES"))
+    return v if v else DEFAULT_STREAM_INFLIGHT
 
 
 class StreamMetrics:
@@ -716,12 +724,10 @@ class ChunkStream(_StreamCore):
 
 def effective_async_buffer_limit() -> int:
     """src/chunking.rs:435-445: CHUNKER_ASYNC_BUFFER_LIMIT_BYTES (default 2 GiB), clamped
-    to 64 MiB..3 GiB."""
-    v = DEFAULT_ASYNC_BUFFER_LIMIT
-    try:
-        v = int(os.environ.get("CHUNKER_ASYNC_BUFFER_LIMIT_BYTES", ""))
-    except ValueError:
-        pass
+    to 64 MiB..3 GiB; a value usize's parser rejects ('-1', ' 5 ', '1_000') means the default."""
+    v = _parse_usize(os.environ.get("CHUNKER_ASYNC_BUFFER_LIMIT_BYTES"))
+    if v is None:
+        v = DEFAULT_ASYNC_BUFFER_LIMIT
     return min(max(v, MIN_ASYNC_BUFFER_LIMIT), MAX_ASYNC_BUFFER_LIMIT)
 
 
@@ -787,10 +793,14 @@ class ChunkStreamAsync(_StreamCore):
                 continue
             try:
                 buf = await self._reader.read(self._read_size)
-            except OSError as e:
+            except asyncio.CancelledError:
+                raise  # cancellation is not a stream error: the stream stays usable
+            except Exception as e:  # noqa: BLE001 -- the first reader error ends the stream (try_stream!)
                 self._done = True
                 self._release()
-                raise IoError(str(e)) from e
+                if isinstance(e, OSError):
+                    raise IoError(str(e)) from e
+                raise
             if not buf:
                 await self._call(self._finish)
                 continue

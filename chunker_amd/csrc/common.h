@@ -51,8 +51,19 @@ __device__ __forceinline__ uint64_t block_inclusive_scan(uint64_t v, uint64_t *s
 }
 
 
+// Work queue of the persistent candidate scan (scan.hip k_scan_flat32p): one head counter
+// per XCD and a leave counter, each on its own 64-B line; zero between launches (the last
+// wave of a launch resets it).
+struct ScanQueue {
+    uint32_t head[8][16];
+    uint32_t done[16];
+};
+
+// d_queue: a zeroed ScanQueue owned by the caller's workspace (nullptr: the one-shot kernel)
 void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint64_t mask_s, uint64_t mask_l,
-                 uint32_t cap, uint32_t *d_seg_count, uint32_t *d_seg_cand, uint64_t nseg, hipStream_t st);
+                 uint32_t cap, uint32_t *d_seg_count, uint32_t *d_seg_cand, uint64_t nseg, hipStream_t st,
+                 ScanQueue *d_queue = nullptr);
+uint64_t scan_resident_wgs();
 
 // Exclusive prefix sum of per-segment entry counts; writes d_out[0..n] (d_out[n] = total).
 // `cap` > 0 applies the entry transform (count <= cap ? count : 1).
@@ -159,6 +170,26 @@ void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
                    uint64_t max_chunks, uint64_t expected, uint64_t max_len, uint32_t *d_order_tmp,
                    uint8_t *d_hash_base, size_t hash_stride, uint32_t *d_err, hipStream_t st);
 size_t sha256_order_tmp_elems(uint64_t max_chunks);
+
+// Coalesced SHA-256 digest (runtime.hip's per-device coalescer): the chunks of up to
+// CG_COAL_MAX batches that are ready at the same time digested by ONE launch_sha256.
+// Member b's chunks are (data[b] + abs[b][i], out[b][i].length) for i < min(*total[b],
+// bound[b]); their digests land in out[b][i].hash and a spin-guard failure in *err[b].
+#define CG_COAL_MAX 32
+struct CoalTable {
+    uint32_t n;
+    const uint8_t *data[CG_COAL_MAX];
+    const uint64_t *abs[CG_COAL_MAX];
+    DescRaw *out[CG_COAL_MAX];
+    const uint64_t *total[CG_COAL_MAX];
+    uint64_t bound[CG_COAL_MAX];
+    uint32_t *err[CG_COAL_MAX];
+};
+// merged arrays: mdesc / mabs bound_sum entries, mtotal one u64, morder_tmp
+// sha256_order_tmp_elems(bound_sum) u32, merr one u32
+void launch_sha256_coalesced(const CoalTable &t, uint64_t bound_sum, uint64_t expected, uint64_t max_len,
+                             DescRaw *mdesc, uint64_t *mabs, uint64_t *mtotal, uint32_t *morder_tmp, uint32_t *merr,
+                             hipStream_t st);
 
 // Longest-first order of the first min(*d_total, max_chunks) descriptors (counting sort
 // on SHA-256 block count, max_len bounding every length); returns the order inside

@@ -111,7 +111,8 @@ struct Workspace {
     uint64_t gear_epoch = 0;
     DevBuf gear, seg_count, seg_cand, eoff, scan_tmp, entries, nar_off, wchunk, nar_nchunks, nar_first,
         chunk_abs, b3_gcount, b3_gbase, b3_gcv, b3_gmap, in, out, span_off, span_len, order, cas_order, ids,
-        man_abs, man_desc, sha_err, pc_first, pc_count, pc_exit, pc_starts, nar_ngroups, b3_lbase, b3_lmap;
+        man_abs, man_desc, sha_err, pc_first, pc_count, pc_exit, pc_starts, nar_ngroups, b3_lbase, b3_lmap,
+        scanq;  // scanq: the persistent scan's work queue (cg::ScanQueue), zeroed once
     PinBuf stage, err_stage, first_host;  // first_host: mapped, the assembly writes the NAR index there
     hipEvent_t ev[EV_N] = {};
     // CAS ids run on side_stream, concurrently with the digest: both stages are bound by
@@ -155,6 +156,8 @@ struct Opts {
 
 int resolve(uint64_t mn, uint64_t avg, uint64_t mx, Opts *o, char *msg, size_t cap);
 uint64_t capacity_of(uint64_t len, uint64_t mn);
+// every workspace buffer a boundary pass over one NAR of len bytes grows, allocated now
+int reserve_pass(Workspace *ws, uint64_t len, const Opts &o, int algo);
 uint32_t logarithm2(uint32_t v);
 
 // SHA-256 spin-guard word of a workspace: arm before a digest launch, fetch with the
@@ -173,12 +176,38 @@ struct BatchLaunch {
 };
 int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, size_t n_nars, const Opts &o,
                  int algo, cg_desc *d_out, size_t out_cap, hipStream_t st, uint8_t *d_chunk_ids,
-                 uint8_t *h_manifest_ids, bool digest, BatchLaunch *bl);
+                 uint8_t *h_manifest_ids, bool digest, BatchLaunch *bl, bool coalesce = false);
 int finish_batch(Workspace *ws, hipStream_t st, const BatchLaunch &bl, uint64_t *h_nar_first);
 
 // The device pipeline for one batch (scan -> compact -> walk -> assemble -> digest).
 int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, size_t n_nars, const Opts &o,
               int algo, cg_desc *d_out, size_t out_cap, uint64_t *h_nar_first, hipStream_t st,
-              uint8_t *d_chunk_ids = nullptr, uint8_t *h_manifest_ids = nullptr, bool digest = true);
+              uint8_t *d_chunk_ids = nullptr, uint8_t *h_manifest_ids = nullptr, bool digest = true,
+              bool coalesce = false);
+
+// Digest coalescer (runtime.hip): a SHA-256 device-entry caller is counted from entry
+// (CoalActive) until it submits its chunk list, so a leader can wait for it to join.
+struct CoalActive {
+    int dev;
+    bool left = false;
+    explicit CoalActive(int dev);
+    void leave();
+    ~CoalActive() { leave(); }
+};
+struct CoalGroup;
+struct CoalEntry {
+    Workspace *ws;
+    const uint8_t *d_data;
+    const uint64_t *d_abs;
+    cg_desc *d_out;
+    const uint64_t *d_total;
+    uint64_t bound, expected, max_len;
+    hipStream_t st;
+    CoalActive *active = nullptr;
+    hipEvent_t ready = nullptr;
+    std::shared_ptr<CoalGroup> group;
+    int rc = 0;
+};
+int coalesced_sha256(CoalEntry *e);
 
 }  // namespace cgrt

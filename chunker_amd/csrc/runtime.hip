@@ -10,7 +10,10 @@
 #include <atomic>
 #include <cmath>
 #include <cstdio>
+#include <chrono>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -259,6 +262,220 @@ uint32_t seg_slots(const CdcParams &p) {
     return c;
 }
 
+// ---------------------------------------------------------------------------
+// Digest coalescer (round 4).  Concurrent callers of the synchronous device entry (the
+// reference's callers are concurrent: thread-per-connection HTTP,
+// crates/proto/nix/src/lib.rs:153-162; BEAM dirty schedulers, src/nif.rs:188-234) each
+// run their boundary stages on their own stream; their SHA-256 digests are then merged:
+// a caller whose boundary stages are queued submits its chunk list and blocks; when no
+// merged digest is in flight, one waiting caller becomes the leader, lets the callers
+// still launching their boundary stages submit too (at most kCoalWindow), and launches
+// ONE k_sha256 over every pending batch's chunks on the device's coalescer stream, after
+// each member's boundary stages (events).  Each member's stream then waits for that
+// launch's end, so its own tail (NAR index, spin-guard word) and its completion event
+// follow the merged digest.  A group of one runs the ordinary per-batch launch on the
+// member's own stream, so a lone caller's latency is unchanged.
+// ---------------------------------------------------------------------------
+struct CoalGroup {
+    hipEvent_t done = nullptr;
+    ~CoalGroup() {
+        if (done) (void)hipEventDestroy(done);
+    }
+};
+
+struct Coalescer {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<CoalEntry *> pending;
+    int active = 0;        // SHA-256 device-entry callers that have not submitted yet
+    bool inflight = false;  // a merged digest is launched and not yet known to be complete
+    hipStream_t stream = nullptr;
+    DevBuf mdesc, mabs, mtotal, morder, merr;
+};
+Coalescer g_coal[64];
+thread_local CoalActive *t_coal_active = nullptr;
+std::atomic<uint32_t> g_coalesce{1};  // test hook cg_test_coalesce
+constexpr auto kCoalWindow = std::chrono::microseconds(3000);
+
+Coalescer &coalescer(int dev) { return g_coal[(dev >= 0 && dev < 64) ? dev : 0]; }
+
+// the device entry's caller is about to launch a SHA-256 batch (CoalActive) / is done
+CoalActive::CoalActive(int dev) : dev(dev) {
+    Coalescer &C = coalescer(dev);
+    std::lock_guard<std::mutex> g(C.mu);
+    ++C.active;
+}
+void CoalActive::leave() {
+    if (left) return;
+    left = true;
+    Coalescer &C = coalescer(dev);
+    {
+        std::lock_guard<std::mutex> g(C.mu);
+        --C.active;
+    }
+    C.cv.notify_all();
+}
+
+// Launch one group (called by its leader without the lock).  Sets every member's group.
+static int launch_group(Coalescer &C, std::vector<CoalEntry *> &grp, std::shared_ptr<CoalGroup> &G) {
+    G = std::make_shared<CoalGroup>();
+    HIP_TRY(hipEventCreateWithFlags(&G->done, hipEventDisableTiming));
+    if (grp.size() == 1) {  // a group of one: the ordinary launch on the member's stream
+        CoalEntry *e = grp[0];
+        Workspace *ws = e->ws;
+        cg::launch_sha256(e->d_data, e->d_abs, e->d_out, e->d_total, e->bound, e->expected, e->max_len,
+                          ws->order.as<uint32_t>(), reinterpret_cast<uint8_t *>(e->d_out) + offsetof(cg_desc, hash),
+                          sizeof(cg_desc), ws->sha_err.as<uint32_t>(), e->st);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(G->done, e->st));
+        return CG_OK;
+    }
+    int rc;
+    if (!C.stream) HIP_TRY(hipStreamCreateWithFlags(&C.stream, hipStreamNonBlocking));
+    cg::CoalTable t{};
+    uint64_t bound = 0, expected = 0, max_len = 0;
+    t.n = (uint32_t)grp.size();
+    for (size_t b = 0; b < grp.size(); ++b) {
+        CoalEntry *e = grp[b];
+        t.data[b] = e->d_data;
+        t.abs[b] = e->d_abs;
+        t.out[b] = reinterpret_cast<DescRaw *>(e->d_out);
+        t.total[b] = e->d_total;
+        t.bound[b] = e->bound;
+        t.err[b] = e->ws->sha_err.as<uint32_t>();
+        bound += e->bound;
+        expected += e->expected;
+        max_len = std::max<uint64_t>(max_len, e->max_len);
+        HIP_TRY(hipStreamWaitEvent(C.stream, e->ready, 0));
+    }
+    // (growing a buffer frees the old one: only while no merged digest is in flight)
+    if ((rc = C.mdesc.ensure((bound + 1) * sizeof(DescRaw), "coalesced descriptors"))) return rc;
+    if ((rc = C.mabs.ensure((bound + 1) * 8, "coalesced addresses"))) return rc;
+    if ((rc = C.mtotal.ensure(64, "coalesced total"))) return rc;
+    if ((rc = C.morder.ensure(cg::sha256_order_tmp_elems(bound) * 4, "coalesced order"))) return rc;
+    if ((rc = C.merr.ensure(64, "coalesced spin guard"))) return rc;
+    cg::launch_sha256_coalesced(t, bound, expected, max_len, C.mdesc.as<DescRaw>(), C.mabs.as<uint64_t>(),
+                                C.mtotal.as<uint64_t>(), C.morder.as<uint32_t>(), C.merr.as<uint32_t>(), C.stream);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(G->done, C.stream));
+    return CG_OK;
+}
+
+int coalesced_sha256(CoalEntry *e) {
+    Coalescer &C = coalescer(e->ws->device);
+    HIP_TRY(hipEventCreateWithFlags(&e->ready, hipEventDisableTiming));
+    struct EvGuard {
+        hipEvent_t ev;
+        ~EvGuard() { (void)hipEventDestroy(ev); }
+    } evg{e->ready};
+    HIP_TRY(hipEventRecord(e->ready, e->st));  // the member's boundary stages (and spin-guard arm) are queued
+    std::unique_lock<std::mutex> lk(C.mu);
+    C.pending.push_back(e);
+    if (e->active) {
+        e->active->left = true;  // submitted: no longer holds back a leader
+        --C.active;
+    }
+    C.cv.notify_all();
+    while (!e->group && !e->rc) {
+        if (!C.inflight && !C.pending.empty()) {
+            C.inflight = true;  // this thread leads the next group
+            const auto t0 = std::chrono::steady_clock::now();
+            while (C.active > 0 && C.pending.size() < CG_COAL_MAX && std::chrono::steady_clock::now() - t0 < kCoalWindow)
+                C.cv.wait_for(lk, std::chrono::microseconds(100));
+            std::vector<CoalEntry *> grp;
+            while (!C.pending.empty() && grp.size() < CG_COAL_MAX) {
+                grp.push_back(C.pending.front());
+                C.pending.pop_front();
+            }
+            lk.unlock();
+            std::shared_ptr<CoalGroup> G;
+            const int rc = launch_group(C, grp, G);
+            lk.lock();
+            for (CoalEntry *m : grp) {
+                if (rc) m->rc = rc;
+                else m->group = G;
+            }
+            C.cv.notify_all();
+            lk.unlock();
+            // the next group launches once this one has ended (its merged buffers are reused)
+            if (!rc) (void)hipEventSynchronize(G->done);
+            lk.lock();
+            C.inflight = false;
+            C.cv.notify_all();
+            continue;
+        }
+        C.cv.wait(lk);
+    }
+    lk.unlock();
+    if (e->rc) return e->rc;
+    HIP_TRY(hipStreamWaitEvent(e->st, e->group->done, 0));
+    return CG_OK;
+}
+
+CdcParams cdc_params(const Opts &o, const Tables &t) {
+    CdcParams P;
+    const uint32_t bits = logarithm2((uint32_t)o.avg);
+    P.min = o.min;
+    P.avg = o.avg;
+    P.max = o.max;
+    P.mask_s = t.masks[bits + 1];
+    P.mask_l = t.masks[bits - 1];
+    return P;
+}
+
+// The workspace buffers a pass over n_nars NARs of total_len bytes needs (boundary
+// stages, and the BLAKE3 tree's), sized without launching anything.  launch_batch calls
+// it; a stream handle calls it (reserve_pass) to size its workspace for a full slot
+// before any digest is in flight, since growing a buffer later frees the old one and
+// hipFree waits for the whole device.
+int ensure_pass_buffers(Workspace *ws, uint64_t total_len, size_t n_nars, uint64_t total_cap, uint64_t chunk_bound,
+                        uint32_t slots, int algo) {
+    int rc;
+    const uint64_t nseg = (total_len + CG_SEG - 1) / CG_SEG;
+    if ((rc = ws->seg_count.ensure((nseg + 1) * 4, "seg_count"))) return rc;
+    if ((rc = ws->seg_cand.ensure((nseg * slots + 1) * 4, "seg_cand"))) return rc;
+    if ((rc = ws->eoff.ensure((nseg + 1) * 8, "eoff"))) return rc;
+    const uint64_t scan_n = std::max<uint64_t>({nseg, (uint64_t)n_nars, total_cap, 1});
+    if ((rc = ws->scan_tmp.ensure(cg::exclusive_scan_tmp_elems(scan_n) * 8 + 64, "scan_tmp"))) return rc;
+    if ((rc = ws->entries.ensure((nseg * slots + 1) * 8, "entries"))) return rc;
+    if ((rc = ws->nar_off.ensure(2 * (n_nars + 1) * 8, "nar_off"))) return rc;
+    if ((rc = ws->wchunk.ensure((total_cap + 1) * 16, "wchunk"))) return rc;
+    if ((rc = ws->nar_nchunks.ensure((n_nars + 1) * 4, "nar_nchunks"))) return rc;
+    if ((rc = ws->nar_first.ensure((n_nars + 1) * 8, "nar_first"))) return rc;
+    if ((rc = ws->chunk_abs.ensure((total_cap + 1) * 8, "chunk_abs"))) return rc;
+    if (algo == CG_BLAKE3) {
+        if ((rc = ws->b3_gcount.ensure((chunk_bound + 1) * 4, "b3_gcount"))) return rc;
+        if ((rc = ws->b3_gbase.ensure((chunk_bound + 1) * 8, "b3_gbase"))) return rc;
+        if ((rc = ws->b3_gcv.ensure(cg::blake3_cv_bytes(total_len, chunk_bound, true), "b3_gcv"))) return rc;
+        if ((rc = ws->b3_gmap.ensure((cg::blake3_group_bound(total_len, chunk_bound) + 1) * 4, "b3_gmap"))) return rc;
+    }
+    return CG_OK;
+}
+
+// The persistent scan's queue: allocated and zeroed (on the batch's stream, ahead of its
+// first scan) once per workspace; every scan launch leaves it zeroed again.
+int ensure_scan_queue(Workspace *ws, hipStream_t st) {
+    if (ws->scanq.p) return CG_OK;
+    int rc;
+    if ((rc = ws->scanq.ensure(sizeof(cg::ScanQueue), "scan queue"))) return rc;
+    HIP_TRY(hipMemsetAsync(ws->scanq.p, 0, ws->scanq.cap, st));
+    return CG_OK;
+}
+
+// One NAR of len bytes, boundaries only: every buffer launch_batch would grow for it
+// (its staging blocks and the descriptor array included), allocated now.
+int reserve_pass(Workspace *ws, uint64_t len, const Opts &o, int algo) {
+    int rc;
+    const std::shared_ptr<const Tables> tab = tables();
+    const CdcParams P = cdc_params(o, *tab);
+    const uint64_t cap = capacity_of(len, o.min);
+    if ((rc = ensure_gear(ws, *tab))) return rc;
+    if ((rc = ws->out.ensure((cap + 1) * sizeof(cg_desc), "descriptors"))) return rc;
+    if ((rc = ws->stage.ensure(8 * sizeof(uint64_t), /*mapped=*/true))) return rc;
+    if ((rc = ws->first_host.ensure(2 * 8, /*mapped=*/true))) return rc;
+    return ensure_pass_buffers(ws, len, 1, cap, cap, seg_slots(P), algo);
+}
+
 // The whole device pipeline for one batch.  d_out receives descriptors; the
 // digest of descriptor g is written in place at d_out[g].hash.
 //
@@ -271,7 +488,7 @@ uint32_t seg_slots(const CdcParams &p) {
 // finish_batch waits for `st` and checks the results.
 int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, size_t n_nars, const Opts &o,
                  int algo, cg_desc *d_out, size_t out_cap, hipStream_t st, uint8_t *d_chunk_ids,
-                 uint8_t *h_manifest_ids, bool digest, BatchLaunch *bl) {
+                 uint8_t *h_manifest_ids, bool digest, BatchLaunch *bl, bool coalesce) {
     if (algo != CG_BLAKE3 && algo != CG_SHA256) return fail(CG_E_INVALID_OPTIONS, "unknown hash algorithm");
     if (((uintptr_t)d_data & 15u) != 0) return fail(CG_E_IO, "device input must be 16-byte aligned");
     int rc;
@@ -284,13 +501,7 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
 
     // one table snapshot for the whole call: GEAR on the device and MASKS in P agree
     const std::shared_ptr<const Tables> tab = tables();
-    CdcParams P;
-    const uint32_t bits = logarithm2((uint32_t)o.avg);
-    P.min = o.min;
-    P.avg = o.avg;
-    P.max = o.max;
-    P.mask_s = tab->masks[bits + 1];
-    P.mask_l = tab->masks[bits - 1];
+    const CdcParams P = cdc_params(o, *tab);
 
     // Walk pieces (walk.hip k_walk_pieces): NARs of at least two piece lengths are also
     // walked piece by piece in parallel; a piece is long enough (32 max-size chunks, at
@@ -368,25 +579,10 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
     const uint32_t slots = seg_slots(P);
     const uint64_t chunk_bound = std::min<uint64_t>(total_cap, out_cap);
     if ((rc = ensure_gear(ws, *tab))) return rc;
-    if ((rc = ws->seg_count.ensure((nseg + 1) * 4, "seg_count"))) return rc;
-    if ((rc = ws->seg_cand.ensure((nseg * slots + 1) * 4, "seg_cand"))) return rc;
-    if ((rc = ws->eoff.ensure((nseg + 1) * 8, "eoff"))) return rc;
-    const uint64_t scan_n = std::max<uint64_t>({nseg, (uint64_t)n_nars, total_cap, 1});
-    if ((rc = ws->scan_tmp.ensure(cg::exclusive_scan_tmp_elems(scan_n) * 8 + 64, "scan_tmp"))) return rc;
-    if ((rc = ws->entries.ensure((nseg * slots + 1) * 8, "entries"))) return rc;
+    if ((rc = ensure_pass_buffers(ws, total_len, n_nars, total_cap, chunk_bound, slots, algo))) return rc;
+    if ((rc = ensure_scan_queue(ws, st))) return rc;
     // nar_off (n+1) then cap_base (n+1): one block, one copy (s_cap follows s_off in staging)
-    if ((rc = ws->nar_off.ensure(2 * (n_nars + 1) * 8, "nar_off"))) return rc;
     const uint64_t *d_nar_off = ws->nar_off.as<uint64_t>(), *d_cap_base = d_nar_off + (n_nars + 1);
-    if ((rc = ws->wchunk.ensure((total_cap + 1) * 16, "wchunk"))) return rc;
-    if ((rc = ws->nar_nchunks.ensure((n_nars + 1) * 4, "nar_nchunks"))) return rc;
-    if ((rc = ws->nar_first.ensure((n_nars + 1) * 8, "nar_first"))) return rc;
-    if ((rc = ws->chunk_abs.ensure((total_cap + 1) * 8, "chunk_abs"))) return rc;
-    if (algo == CG_BLAKE3) {
-        if ((rc = ws->b3_gcount.ensure((chunk_bound + 1) * 4, "b3_gcount"))) return rc;
-        if ((rc = ws->b3_gbase.ensure((chunk_bound + 1) * 8, "b3_gbase"))) return rc;
-        if ((rc = ws->b3_gcv.ensure(cg::blake3_cv_bytes(total_len, chunk_bound, true), "b3_gcv"))) return rc;
-        if ((rc = ws->b3_gmap.ensure((cg::blake3_group_bound(total_len, chunk_bound) + 1) * 4, "b3_gmap"))) return rc;
-    }
 
     // A timing event between two kernels holds the second back by ~6 us (the event's
     // end-of-pipe timestamp), so mode 2 records only the two around the digest stage.
@@ -398,7 +594,7 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
     if (prof_all) HIP_TRY(hipEventRecord(ws->ev[EV_START], st));  // scan stage = the scan kernel alone
 
     cg::launch_scan(d_data, total_len, ws->gear.as<uint64_t>(), P.mask_s, P.mask_l, slots,
-                    ws->seg_count.as<uint32_t>(), ws->seg_cand.as<uint32_t>(), nseg, st);
+                    ws->seg_count.as<uint32_t>(), ws->seg_cand.as<uint32_t>(), nseg, st, ws->scanq.as<cg::ScanQueue>());
     if (prof_all) HIP_TRY(hipEventRecord(ws->ev[EV_SCAN], st));
     // (the host tables ride along the compaction's first launch: the scan needs none of them)
     cg::launch_scan_compact(ws->seg_count.as<uint32_t>(), ws->seg_cand.as<uint32_t>(), ws->eoff.as<uint64_t>(), slots,
@@ -470,8 +666,15 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
         const uint64_t expected = std::min<uint64_t>(chunk_bound, total_len / (o.min + o.avg) + n_nars);
         if ((rc = sha_err_arm(ws, st))) return rc;
         sha_armed = true;
-        cg::launch_sha256(d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, expected, o.max,
-                          ws->order.as<uint32_t>(), hash_base, sizeof(cg_desc), ws->sha_err.as<uint32_t>(), st);
+        if (coalesce && chunk_bound) {
+            CoalEntry e{ws, d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, expected, o.max, st};
+            e.active = t_coal_active;
+            if ((rc = coalesced_sha256(&e))) return rc;
+        } else {
+            if (t_coal_active) t_coal_active->leave();  // nothing to merge: do not hold a leader back
+            cg::launch_sha256(d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, expected, o.max,
+                              ws->order.as<uint32_t>(), hash_base, sizeof(cg_desc), ws->sha_err.as<uint32_t>(), st);
+        }
     } else {
         cg::launch_blake3(d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, total_len, hash_base,
                           sizeof(cg_desc), ws->b3_gmap.as<uint32_t>(), ws->b3_gbase.as<uint64_t>(),
@@ -537,10 +740,10 @@ int finish_batch(Workspace *ws, hipStream_t st, const BatchLaunch &bl, uint64_t 
 // may have queued work on `st`: it is drained before the workspace goes back to the pool.
 int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, size_t n_nars, const Opts &o,
               int algo, cg_desc *d_out, size_t out_cap, uint64_t *h_nar_first, hipStream_t st,
-              uint8_t *d_chunk_ids, uint8_t *h_manifest_ids, bool digest) {
+              uint8_t *d_chunk_ids, uint8_t *h_manifest_ids, bool digest, bool coalesce) {
     BatchLaunch bl;
-    const int rc =
-        launch_batch(ws, d_data, h_nar_off, n_nars, o, algo, d_out, out_cap, st, d_chunk_ids, h_manifest_ids, digest, &bl);
+    const int rc = launch_batch(ws, d_data, h_nar_off, n_nars, o, algo, d_out, out_cap, st, d_chunk_ids,
+                                h_manifest_ids, digest, &bl, coalesce);
     if (rc) {
         (void)hipStreamSynchronize(st);
         return rc;
@@ -884,6 +1087,10 @@ int push_append(cg_push *h, const uint8_t *data, uint64_t len) {
 
 }  // namespace cgrt
 
+extern "C" uint32_t cg_test_coalesce(uint32_t v) {  // 0 = every device-entry call digests alone
+    return cgrt::g_coalesce.exchange(v ? 1u : 0u);
+}
+
 extern "C" {
 
 uint32_t cg_abi_version(void) { return CG_ABI_VERSION; }
@@ -940,8 +1147,17 @@ int cg_chunk_batch_device(const uint8_t *d_data, const uint64_t *nar_offsets, si
     Workspace *ws = nullptr;
     if ((rc = acquire(&ws))) return rc;
     WsGuard guard{ws};
-    return run_batch(ws, d_data, nar_offsets, n_nars, o, algo, d_out, out_cap, nar_first,
-                     static_cast<hipStream_t>(stream));
+    // concurrent SHA-256 callers share one digest launch (coalesced_sha256)
+    if (algo != CG_SHA256 || !g_coalesce.load(std::memory_order_relaxed))
+        return run_batch(ws, d_data, nar_offsets, n_nars, o, algo, d_out, out_cap, nar_first,
+                         static_cast<hipStream_t>(stream));
+    CoalActive active(ws->device);
+    t_coal_active = &active;
+    rc = run_batch(ws, d_data, nar_offsets, n_nars, o, algo, d_out, out_cap, nar_first,
+                   static_cast<hipStream_t>(stream), nullptr, nullptr, true, true);
+    t_coal_active = nullptr;
+    active.leave();
+    return rc;
 }
 
 int cg_chunk_batch_device_async(const uint8_t *d_data, const uint64_t *nar_offsets, size_t n_nars, uint64_t min_size,

@@ -10,6 +10,7 @@
 // least 47 bytes past the chunk's hash start.  The 47
 // positions before that are recomputed exactly by the walker.
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 
 #include "scan_common.h"
@@ -234,8 +235,11 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
     // faulting, so no per-lane address arithmetic or clamp is left in the row loop (the
     // bytes past the end only feed candidates the tail rows mask off).
     typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+    // The range ends at the batch end rounded up to its 16-byte granule (the input is
+    // 16-byte aligned, so the granule is allocated): a dwordx4 load of the last granule
+    // then returns its bytes whatever the hardware's range check does with a partial one.
     const uint64_t run_bytes = nrow * F32_ROW;  // <= spw x 4 KiB: 32-bit offsets
-    const uint64_t avail = active ? n - r0 : 0;
+    const uint64_t avail = active ? ((n - r0 + 15) & ~15ull) : 0;
     const __amdgpu_buffer_rsrc_t run_rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t *>(data + (active ? r0 : 0)), (short)0, (int)(avail < run_bytes ? avail : run_bytes),
         0x00027000);
@@ -425,6 +429,296 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
     }
 }
 
+// ---------------------------------------------------------------------------
+// K1, persistent form (round 4, the product for prefilterable masks): the row work of
+// k_scan_flat32 above, but the grid is only the workgroups the chip holds at once and every
+// wave takes units of SPU segments (32 KiB at SPU = 8) from a queue until it is empty.
+//
+// Why: a one-shot grid (one run per wave, 8,192 waves at 1 GiB) kept only ~2.5 of the 4
+// resident waves per SIMD busy on average (SQ_WAVE_CYCLES / kernel cycles,
+// profiles/r04_pmc_sq_c2.json): a 512-thread workgroup's LDS is held until its slowest
+// wave ends, and waves on one SIMD finish at different times (the oldest gets the VALU
+// first), so dispatch rounds drain unevenly.  Here all waves live until the queue is
+// empty, and the tail is at most one unit per wave.
+//
+// Queue: the batch's units split into 8 contiguous ranges, one per XCD (HW_REG_XCC_ID);
+// a wave takes from its own XCD's range first (consecutive units stay in one L2, so a
+// unit's halo row -- the row before it, read by the wave that took the previous unit a
+// moment earlier -- is usually an L2 hit), then from the others'.  One returning agent-
+// scope atomic per unit, dequeued a unit ahead so its latency hides behind the current
+// unit's rows; the next unit's halo row and first two rows are in flight when the current
+// unit's last rows are hashed.  The last wave to leave resets the counters, so every launch
+// starts from zero without a memset.
+// ---------------------------------------------------------------------------
+#ifndef CG_SCAN_SPU
+#define CG_SCAN_SPU 8u
+#endif
+static_assert(sizeof(ScanQueue) == 9 * 64, "one 64-B line per counter");
+
+template <uint32_t SPU>
+__global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data, uint64_t n,
+                                                           const uint64_t *__restrict__ gear_g, uint64_t mask_s,
+                                                           uint64_t mask_l, uint32_t cap,
+                                                           uint32_t *__restrict__ seg_count,
+                                                           uint32_t *__restrict__ seg_cand, uint64_t nseg,
+                                                           ScanQueue *queue, uint32_t nunits) {
+    __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * GEAR_COPIES];
+    __shared__ uint32_t s_slots[SCAN2_T / 64][64];  // the open segment's candidate slots, per wave
+    constexpr uint32_t R = SPU * F32_RPS;           // rows per unit (even: the 2-row ring starts each unit at slot 0)
+    constexpr uint32_t UNIT = SPU * CG_SEG;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= 7u;
+    typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+    // a unit's rows through a buffer resource based at the unit, its size ending at the batch
+    // end rounded up to the 16-byte granule (k_scan_flat32)
+    auto rsrc_of = [&](uint32_t u) {
+        const uint64_t r0 = (uint64_t)u * UNIT;
+        const uint64_t avail = r0 < n ? ((n - r0 + 15) & ~15ull) : 0;
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(data + (r0 < n ? r0 : 0)), (short)0,
+                                                 (int)(avail < UNIT ? avail : UNIT), 0x00027000);
+    };
+    const uint32_t lane_off = 32u * lane;
+    auto blk = [&](__amdgpu_buffer_rsrc_t rs, uint32_t row, uint4 (&v)[2]) {
+        const uint32_t so = row * F32_ROW;
+        const u32x4_t x0 = __builtin_amdgcn_raw_buffer_load_b128(rs, lane_off, so, 2);  // aux 2: nt
+        const u32x4_t x1 = __builtin_amdgcn_raw_buffer_load_b128(rs, lane_off + 16u, so, 2);
+        v[0] = uint4{x0.x, x0.y, x0.z, x0.w};
+        v[1] = uint4{x1.x, x1.y, x1.z, x1.w};
+    };
+    // the row before unit u (its hash carries into the unit's first lanes); unit 0 has none
+    auto halo = [&](uint32_t u, uint4 (&v)[2]) {
+        const uint64_t r0 = (uint64_t)u * UNIT;
+        const uint64_t a = (r0 >= F32_ROW && r0 < n ? r0 - F32_ROW : 0) + lane_off;
+        v[0] = *reinterpret_cast<const uint4 *>(data + a);
+        v[1] = *reinterpret_cast<const uint4 *>(data + a + 16);
+    };
+    // one unit index, wave-uniform; nunits when every range is empty
+    auto dequeue = [&]() -> uint32_t {
+        for (uint32_t k = 0; k < 8; ++k) {
+            const uint32_t x = (xcc + k) & 7u;
+            const uint32_t lo = (uint32_t)((uint64_t)nunits * x / 8), hi = (uint32_t)((uint64_t)nunits * (x + 1) / 8);
+            if (lo == hi) continue;
+            uint32_t i = 0;
+            if (lane == 0) i = __hip_atomic_fetch_add(&queue->head[x][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            i = __builtin_amdgcn_readfirstlane(i);
+            if (i < hi - lo) return lo + i;
+        }
+        return nunits;
+    };
+
+    static_assert(SCAN2_T == 2 * 256 && GEAR_COPIES == 32, "two threads per Gear entry, 16 copies each");
+    const uint32_t ge = threadIdx.x >> 1;
+    const uint64_t gv = gear_g[ge] << SCAN_SHIFT;
+    uint32_t u = dequeue();
+    const bool any = u < nunits;
+    __amdgpu_buffer_rsrc_t rs = rsrc_of(any ? u : 0);
+    uint4 ring[2][2], pro[2];
+    blk(rs, 0, ring[0]);
+    blk(rs, 1, ring[1]);
+    halo(any ? u : 0, pro);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j) s_gear[ge * GEAR_COPIES + (((threadIdx.x & 1u) * 16u + j + ge) & 31u)] = gv;
+    __syncthreads();
+    const char *gbase = reinterpret_cast<const char *>(s_gear);
+    uint32_t *slots = s_slots[wv];
+    const uint32_t lo8 = (threadIdx.x & 31u) * 8u;
+    uint32_t ad[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) ad[i][b] = lo8;
+    const uint64_t ms = mask_s << SCAN_SHIFT, ml = mask_l << SCAN_SHIFT;
+    const uint32_t mh = (uint32_t)((mask_s & mask_l) >> (32 - SCAN_SHIFT));
+    const uint32_t m0 = lane == 0 ? 0xffffffffu : 0u;
+    uint32_t zero = 0;
+    asm volatile("" : "+v"(zero));
+    const uint32_t ms_lo = (uint32_t)ms, ms_hi = (uint32_t)(ms >> 32), ml_lo = (uint32_t)ml, ml_hi = (uint32_t)(ml >> 32);
+
+    auto partials = [&](const uint4 (&v)[2], uint64_t (&q)[8][4]) {
+        lookup4(gbase, ad[0], v[0].x, q[0]);
+        lookup4(gbase, ad[0], v[0].y, q[1]);
+        lookup4(gbase, ad[0], v[0].z, q[2]);
+        lookup4(gbase, ad[0], v[0].w, q[3]);
+        lookup4(gbase, ad[0], v[1].x, q[4]);
+        lookup4(gbase, ad[0], v[1].y, q[5]);
+        lookup4(gbase, ad[0], v[1].z, q[6]);
+        lookup4(gbase, ad[0], v[1].w, q[7]);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            q[k][1] = shl1_add(q[k][0], q[k][1]);
+            q[k][2] = shl1_add(q[k][1], q[k][2]);
+            q[k][3] = shl1_add(q[k][2], q[k][3]);
+        }
+    };
+    auto block_p = [&](const uint64_t (&q)[8][4]) {
+        uint64_t P = q[0][3];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) P = shl_add<4>(P, q[k][3]);
+        return P;
+    };
+
+    while (any) {
+        const uint64_t r0 = (uint64_t)u * UNIT;
+        const uint64_t seg0 = (uint64_t)u * SPU;
+        const uint64_t end_rel = n - r0;  // > 0: units start inside the batch
+        // the next unit: dequeued now, its halo row and first two rows issued as the current
+        // unit's rows free their ring slots
+        const uint32_t un = dequeue();
+        const bool more = un < nunits;
+        const __amdgpu_buffer_rsrc_t rs_next = rsrc_of(more ? un : u);
+        // zero state at the batch start, as the crate's hash restart
+        uint64_t R1 = 0;
+        uint32_t R2 = 0;
+        if (r0 >= F32_ROW) {
+            uint64_t q[8][4];
+            partials(pro, q);
+            const uint64_t P = block_p(q);
+            R1 = ((uint64_t)wave_ror1((uint32_t)(P >> 32)) << 32) | wave_ror1((uint32_t)P);
+            R2 = wave_ror1((uint32_t)R1);
+        }
+        halo(more ? un : u, pro);
+        uint32_t segc = 0;
+#pragma unroll 1
+        for (uint32_t r = 0; r < R; r += 2) {
+#pragma unroll
+            for (uint32_t uu = 0; uu < 2; ++uu) {
+                const uint32_t row = r + uu;
+                const bool nx_here = row + 2 < R;  // uniform: the slot's next row is in this unit
+                const uint64_t rowb = (uint64_t)row * F32_ROW;
+                if (rowb >= end_rel) {  // a row past the batch end (the last unit only): nothing to hash
+                    blk(nx_here ? rs : rs_next, nx_here ? row + 2 : row + 2 - R, ring[uu]);
+                    if (uu == 1) {
+                        const uint64_t seg = seg0 + row / F32_RPS;
+                        if (seg < nseg) {
+                            if (lane < min(segc, cap)) seg_cand[seg * cap + lane] = slots[lane];
+                            if (lane == 0) seg_count[seg] = segc;
+                        }
+                        segc = 0;
+                    }
+                    continue;
+                }
+                uint64_t q[8][4];
+                partials(ring[uu], q);
+                blk(nx_here ? rs : rs_next, nx_here ? row + 2 : row + 2 - R, ring[uu]);  // re-issue the slot now
+                const uint64_t P = block_p(q);
+                const uint32_t a_lo = wave_ror1_add((uint32_t)P, zero), a_hi = wave_ror1_add((uint32_t)(P >> 32), zero);
+                const uint32_t p1_lo = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)R1, a_lo, 0xCA);
+                const uint32_t p1_hi = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)(R1 >> 32), a_hi, 0xCA);
+                R1 = ((uint64_t)a_hi << 32) | a_lo;
+                const uint32_t b_lo = wave_ror1_add(p1_lo, zero);
+                const uint32_t p2_lo = __builtin_amdgcn_bitop3_b32(m0, R2, b_lo, 0xCA);
+                R2 = b_lo;
+                // C = P_{L-1} + (P_{L-2} << 32)
+                const uint64_t C = ((uint64_t)(p1_hi + p2_lo) << 32) | p1_lo;
+                uint32_t acc = 0xffffffffu;
+                {
+                    uint64_t E = C;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const uint64_t h0 = shl_add<1>(E, q[k][0]), h1 = shl_add<2>(E, q[k][1]);
+                        const uint64_t h2 = shl_add<3>(E, q[k][2]), h3 = shl_add<4>(E, q[k][3]);
+                        acc = min(min(acc, (uint32_t)(h0 >> 32) & mh), (uint32_t)(h1 >> 32) & mh);
+                        acc = min(min(acc, (uint32_t)(h2 >> 32) & mh), (uint32_t)(h3 >> 32) & mh);
+                        E = h3;
+                    }
+                }
+                auto step = [&](uint64_t &x, uint32_t j) -> uint64_t {
+                    const uint64_t qj = q[j >> 2][j & 3];
+                    switch (j & 3) {
+                    case 0: return shl_add<1>(x, qj);
+                    case 1: return shl_add<2>(x, qj);
+                    case 2: return shl_add<3>(x, qj);
+                    default: return x = shl_add<4>(x, qj);
+                    }
+                };
+                const bool tail = rowb + F32_ROW > end_rel;  // uniform
+                if (__builtin_amdgcn_ballot_w64(acc == 0) != 0 || tail) {
+                    bool exact = tail;
+                    if (!tail) {
+                        uint32_t ex = 0xffffffffu;
+                        uint64_t x = C;
+#pragma unroll
+                        for (uint32_t j = 0; j < 32; ++j) {
+                            const uint64_t hx = step(x, j);
+                            const uint32_t lo = (uint32_t)hx, hi = (uint32_t)(hx >> 32);
+                            ex = min(ex, min((lo & ms_lo) | (hi & ms_hi), (lo & ml_lo) | (hi & ml_hi)));
+                        }
+                        exact = __builtin_amdgcn_ballot_w64(ex == 0) != 0;
+                    }
+                    if (exact) {
+                        const uint64_t prel = rowb + 32u * lane;
+                        const uint32_t nb = prel < end_rel ? (end_rel - prel < 32 ? (uint32_t)(end_rel - prel) : 32u) : 0u;
+                        uint32_t sm = 0, lm = 0;
+                        uint64_t x = C;
+#pragma unroll
+                        for (uint32_t j = 0; j < 32; ++j) {
+                            const uint64_t hx = step(x, j);
+                            const uint64_t zs = hx & ms, zl = hx & ml;
+                            const uint32_t ts = (uint32_t)zs | (uint32_t)(zs >> 32), tl = (uint32_t)zl | (uint32_t)(zl >> 32);
+                            sm |= (1u - min(ts, 1u)) << j;
+                            lm |= (1u - min(tl, 1u)) << j;
+                        }
+                        const uint32_t vm = nb >= 32 ? 0xffffffffu : (1u << nb) - 1u;
+                        sm &= vm;
+                        lm &= vm;
+                        const uint32_t anyb = sm | lm, c = (uint32_t)__builtin_popcount(anyb);
+                        uint32_t excl, total;
+                        if (__builtin_amdgcn_ballot_w64(c > 1) == 0) {
+                            const uint64_t bal = __builtin_amdgcn_ballot_w64(c != 0);
+                            excl = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0));
+                            total = (uint32_t)__builtin_popcountll(bal);
+                        } else {
+                            uint32_t incl = c;
+#pragma unroll
+                            for (uint32_t d = 1; d < 64; d <<= 1) {
+                                const uint32_t y = (uint32_t)__shfl_up((int)incl, d, 64);
+                                if (lane >= d) incl += y;
+                            }
+                            excl = incl - c;
+                            total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                        }
+                        const uint32_t pos0 = (row % F32_RPS) * F32_ROW + 32u * lane;
+                        uint32_t idx = segc + excl;
+                        for (uint32_t m = anyb; m; m &= m - 1) {
+                            const uint32_t j = (uint32_t)__builtin_ctz(m);
+                            const uint32_t f = (((sm >> j) & 1u) * CG_FLAG_S) | (((lm >> j) & 1u) * CG_FLAG_L);
+                            if (idx < cap) slots[idx] = ((pos0 + j) << 2) | f;
+                            ++idx;
+                        }
+                        segc += total;
+                    }
+                }
+                if (uu == 1) {  // segment end: flush its slots and count
+                    const uint64_t seg = seg0 + row / F32_RPS;
+                    if (seg < nseg) {
+                        if (lane < min(segc, cap)) seg_cand[seg * cap + lane] = slots[lane];
+                        if (lane == 0) seg_count[seg] = segc;
+                    }
+                    segc = 0;
+                }
+            }
+        }
+        if (!more) break;
+        u = un;
+        rs = rs_next;
+    }
+    // leave: the last wave of the grid resets the queue for the next launch
+    if (lane == 0) {
+        const uint32_t waves = gridDim.x * (SCAN2_T / 64);
+        const uint32_t old = __hip_atomic_fetch_add(&queue->done[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == waves - 1) {
+#pragma unroll
+            for (int x = 0; x < 8; ++x) __hip_atomic_store(&queue->head[x][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&queue->done[0], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 #ifdef CG_DIAG
 // diagnostics build (scan_diag.hip): the alternative scan kernels of DESIGN.md §4's A/B
 extern uint32_t g_scan_spw_max, g_scan_variant;
@@ -445,8 +739,12 @@ void launch_k_scan_pre(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear
 }
 #endif
 
+// test hook (cg_test_scan_kernel): 1 = the one-shot k_scan_flat32 instead of the persistent form
+uint32_t g_scan_oneshot = 0;
+
 void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint64_t mask_s, uint64_t mask_l,
-                 uint32_t cap, uint32_t *d_seg_count, uint32_t *d_seg_cand, uint64_t nseg, hipStream_t st) {
+                 uint32_t cap, uint32_t *d_seg_count, uint32_t *d_seg_cand, uint64_t nseg, hipStream_t st,
+                 ScanQueue *d_queue) {
     if (nseg == 0) return;
     const uint64_t blocks = (nseg + SCAN2_T - 1) / SCAN2_T;
     // prefilter when the bits of mask_s & mask_l it tests leave hits rarer than ~1 per 16 KiB
@@ -483,14 +781,47 @@ void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint
     spw = spw < 4 ? 4 : (spw > spw_max ? spw_max : (spw + 3) & ~3ull);
     const uint64_t waves = (nseg + spw - 1) / spw;
     const uint64_t wgs = (waves + SCAN2_T / 64 - 1) / (SCAN2_T / 64);
-    // product: 32-byte lane blocks in 2 KiB rows (k_scan_flat32; the 16-byte row forms of
-    // k_scan_flat are the diagnostics build's A/B)
+    // product: the persistent form (k_scan_flat32p) when the caller passes its queue and the
+    // one-shot k_scan_flat32 was not asked for (cg_test_scan_kernel); the 16-byte row forms of
+    // k_scan_flat are the diagnostics build's A/B
+#ifdef CG_DIAG
+    const bool diag_variant = g_scan_variant == 5;
+#else
+    const bool diag_variant = false;
+#endif
+    if (d_queue && !g_scan_oneshot && !diag_variant) {
+        const uint64_t nunits = (nseg + CG_SCAN_SPU - 1) / CG_SCAN_SPU;
+        const uint64_t resident = scan_resident_wgs();
+        const uint64_t want = (nunits + SCAN2_T / 64 - 1) / (SCAN2_T / 64);  // >= one unit per wave
+        const uint64_t grid = std::max<uint64_t>(1, std::min(want, resident));
+        hipLaunchKernelGGL(k_scan_flat32p<CG_SCAN_SPU>, dim3((uint32_t)grid), dim3(SCAN2_T), 0, st, d_data, n, d_gear,
+                           mask_s, mask_l, cap, d_seg_count, d_seg_cand, nseg, d_queue, (uint32_t)nunits);
+        return;
+    }
     auto k = k_scan_flat32<2, true>;
 #ifdef CG_DIAG
-    if (g_scan_variant == 5) k = scan_flat_diag_kernel(k);
+    if (diag_variant) k = scan_flat_diag_kernel(k);
 #endif
     hipLaunchKernelGGL(k, dim3((uint32_t)wgs), dim3(SCAN2_T), 0, st, d_data, n, d_gear, mask_s, mask_l, cap,
                        d_seg_count, d_seg_cand, nseg, (uint32_t)spw);
+}
+
+// Workgroups of k_scan_flat32p the current device holds at once (CUs x the occupancy
+// query), cached per device.
+uint64_t scan_resident_wgs() {
+    static std::atomic<uint64_t> cache[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    uint64_t v = cache[dev].load(std::memory_order_relaxed);
+    if (v) return v;
+    int cus = 0, per_cu = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_scan_flat32p<CG_SCAN_SPU>, SCAN2_T, 0) != hipSuccess ||
+        per_cu <= 0)
+        per_cu = 2;
+    v = (uint64_t)cus * (uint64_t)per_cu;
+    cache[dev].store(v, std::memory_order_relaxed);
+    return v;
 }
 // ---------------------------------------------------------------------------
 // Exclusive prefix sum u32 -> u64 (one launch for small inputs; tile sums + apply otherwise).
@@ -703,6 +1034,12 @@ void launch_scan_compact(const uint32_t *d_seg_count, const uint32_t *d_seg_cand
 }
 
 }  // namespace cg
+
+extern "C" uint32_t cg_test_scan_kernel(uint32_t v) {
+    const uint32_t old = cg::g_scan_oneshot;
+    cg::g_scan_oneshot = v ? 1u : 0u;
+    return old;
+}
 
 extern "C" uint32_t cg_test_scan_path(uint32_t v) {
     const uint32_t old = cg::g_scan_path;

@@ -7,6 +7,7 @@
 // loaded as aligned dwords and realigned + byte-swapped with one v_perm_b32 per
 // word (chunk offsets are arbitrary bytes).  Rotates are v_alignbit_b32.
 #include <algorithm>
+#include <cstddef>
 
 #include "common.h"
 
@@ -992,6 +993,81 @@ void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
     hipLaunchKernelGGL(k_sha256, dim3(nwg), dim3(128), pad, st, d_data, d_abs,
                        (const DescRaw *)d_desc, d_total, max_chunks, order, d_hash_base, hash_stride, g_sha_diag,
                        g_sha_mode, nquad, npair, g_sha_spin_limit, d_err);
+}
+
+// ---------------------------------------------------------------------------
+// Coalesced digest of several batches (runtime.hip coalescer, round 4).  One batch's
+// digest is a ~55 ms chain of its longest chunk on ~700 waves, so K concurrent callers
+// each running their own launch leave the chip mostly idle and serialise on the hardware
+// queues; merging the K chunk lists into one launch gives one GPU-filling k_sha256 whose
+// length order spreads every batch's chunks over the quad / pair / one-lane tiers.
+// k_coal_merge builds the merged list (lengths + addresses relative to member 0's base,
+// so an idle lane's address stays inside a real buffer); k_coal_scatter copies the
+// digests back into each member's descriptors and the spin-guard word into each member's.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void coal_prefix(const CoalTable &t, uint64_t *pre) {
+    if (threadIdx.x == 0) {
+        uint64_t s = 0;
+        for (uint32_t b = 0; b < t.n; ++b) {
+            pre[b] = s;
+            const uint64_t c = *t.total[b];
+            s += c < t.bound[b] ? c : t.bound[b];
+        }
+        pre[t.n] = s;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t coal_member(const uint64_t *pre, uint32_t n, uint64_t g) {
+    uint32_t b = 0;
+    while (b + 1 < n && pre[b + 1] <= g) ++b;
+    return b;
+}
+
+__global__ __launch_bounds__(256) void k_coal_merge(CoalTable t, DescRaw *__restrict__ mdesc,
+                                                    uint64_t *__restrict__ mabs, uint64_t *__restrict__ mtotal) {
+    __shared__ uint64_t pre[CG_COAL_MAX + 1];
+    coal_prefix(t, pre);
+    const uint64_t total = pre[t.n];
+    if (blockIdx.x == 0 && threadIdx.x == 0) *mtotal = total;
+    const uint64_t base = (uint64_t)t.data[0];
+    for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < total; g += (uint64_t)gridDim.x * 256) {
+        const uint32_t b = coal_member(pre, t.n, g);
+        const uint64_t i = g - pre[b];
+        mdesc[g].length = t.out[b][i].length;
+        mabs[g] = (uint64_t)t.data[b] + t.abs[b][i] - base;  // data[0] + mabs[g] = the chunk's address
+    }
+}
+
+__global__ __launch_bounds__(256) void k_coal_scatter(CoalTable t, const DescRaw *__restrict__ mdesc,
+                                                      const uint32_t *__restrict__ merr) {
+    __shared__ uint64_t pre[CG_COAL_MAX + 1];
+    coal_prefix(t, pre);
+    const uint64_t total = pre[t.n];
+    if (blockIdx.x == 0 && threadIdx.x < t.n) {
+        const uint32_t e = *merr;
+        if (e) *t.err[threadIdx.x] = e;
+    }
+    for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < total; g += (uint64_t)gridDim.x * 256) {
+        const uint32_t b = coal_member(pre, t.n, g);
+        const uint64_t i = g - pre[b];
+        const uint4 *src = reinterpret_cast<const uint4 *>(mdesc[g].hash);
+        uint4 *dst = reinterpret_cast<uint4 *>(t.out[b][i].hash);
+        dst[0] = src[0];
+        dst[1] = src[1];
+    }
+}
+
+void launch_sha256_coalesced(const CoalTable &t, uint64_t bound_sum, uint64_t expected, uint64_t max_len,
+                             DescRaw *mdesc, uint64_t *mabs, uint64_t *mtotal, uint32_t *morder_tmp, uint32_t *merr,
+                             hipStream_t st) {
+    if (t.n == 0 || bound_sum == 0) return;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((bound_sum + 255) / 256, 1024);
+    (void)hipMemsetAsync(merr, 0, sizeof(uint32_t), st);
+    hipLaunchKernelGGL(k_coal_merge, dim3(grid), dim3(256), 0, st, t, mdesc, mabs, mtotal);
+    launch_sha256(t.data[0], mabs, mdesc, mtotal, bound_sum, expected, max_len, morder_tmp,
+                  reinterpret_cast<uint8_t *>(mdesc) + offsetof(DescRaw, hash), sizeof(DescRaw), merr, st);
+    hipLaunchKernelGGL(k_coal_scatter, dim3(grid), dim3(256), 0, st, t, mdesc, merr);
 }
 
 #ifdef CG_DIAG

@@ -372,6 +372,19 @@ int stream_drain(cg_stream *h, uint64_t len, bool eof) {
 
 }  // namespace cgrt
 
+namespace {
+// Hardware queues HIP gives this process: GPU_MAX_HW_QUEUES as the environment held it
+// when this library was loaded (HIP's default 4 when unset).  HIP reads the variable once,
+// when it initialises, and the library makes no HIP call before it is loaded, so this is
+// the value HIP applies -- unless the caller initialised HIP earlier under another value
+// (the library never changes the variable on the caller's behalf).
+const int g_hw_queues_at_load = [] {
+    const char *q = std::getenv("GPU_MAX_HW_QUEUES");
+    const int v = q ? std::atoi(q) : 0;
+    return v > 0 ? v : 4;
+}();
+}  // namespace
+
 extern "C" {
 
 cg_stream *cg_stream_new(uint64_t min_size, uint64_t avg_size, uint64_t max_size, int algo, uint64_t slice_bytes,
@@ -402,9 +415,7 @@ cg_stream *cg_stream_new(uint64_t min_size, uint64_t avg_size, uint64_t max_size
     h->slot_bytes = (o.max + slice + 256 + 255) & ~255ull;
     const uint64_t budget = inflight_bytes ? inflight_bytes : 2048ull << 20;
     h->max_slots = std::max<uint64_t>(budget / h->slot_bytes, 4);
-    int queues = 4;
-    if (const char *q = std::getenv("GPU_MAX_HW_QUEUES")) queues = std::atoi(q) > 0 ? std::atoi(q) : 4;
-    h->max_lanes = (size_t)std::min(std::max(queues - 2, 2), 8);
+    h->max_lanes = (size_t)std::min(std::max(g_hw_queues_at_load - 2, 2), 8);
     if (g_stream_max_lanes) h->max_lanes = g_stream_max_lanes;
     h->lanes.reserve(h->max_lanes);
     // A group's SHA-256 launch takes one CU per 8 chunks (quad workgroups, padded to a CU
@@ -448,18 +459,8 @@ int check_poisoned(const cg_stream *h) {
 
 // Size the workspace for the largest boundary pass (a full slot) before any digest is in
 // flight: a workspace buffer that grew later would hipFree, which waits for the whole
-// device.  The pass reads the fresh arena's (uninitialised) first slot; its cuts are
-// discarded.
-int prime_workspace(cg_stream *h) {
-    int rc;
-    Workspace *ws = h->ws;
-    const uint64_t len = h->slot_bytes - 256;
-    const uint64_t cap = capacity_of(len, h->o.min);
-    if ((rc = ws->out.ensure((cap + 1) * sizeof(cg_desc), "descriptors"))) return rc;
-    uint64_t offs[2] = {0, len}, first[2] = {0, 0};
-    return run_batch(ws, h->arena.p, offs, 1, h->o, h->algo, ws->out.as<cg_desc>(), cap, first, ws->stream, nullptr,
-                     nullptr, /*digest=*/false);
-}
+// device.  Allocation only: nothing is launched over the fresh (uninitialised) arena.
+int prime_workspace(cg_stream *h) { return reserve_pass(h->ws, h->slot_bytes - 256, h->o, h->algo); }
 
 int stream_push(cg_stream *h, const uint8_t *data, uint64_t len) {
     int rc;

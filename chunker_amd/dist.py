@@ -4,7 +4,9 @@ descriptors gathered to rank 0.
 The reference has no distributed compute: NARs are independent
 (FastCDC state never crosses files), so the only exchange is collecting every
 rank's descriptors on one rank.  On MI355X that is a torch.distributed gather over
-RCCL/xGMI ("nccl" backend); the same code runs over gloo on CPU for tests.
+RCCL/xGMI ("nccl" backend); the same code runs over gloo on CPU for tests.  The
+per-step gather (gather_batch_async) has fixed sizes agreed once (gather_shape), so it
+is queued without a host sync and overlaps the next batch's kernels.
 """
 from __future__ import annotations
 
@@ -47,36 +49,85 @@ def gather_descriptors(desc: torch.Tensor, n: int, group=None) -> list[torch.Ten
     return [g[: c * DESC_BYTES] for g, c in zip(gl, counts)]
 
 
-def gather_batch(desc: torch.Tensor, nar_first, group=None):
-    """Gather a sharded batch to rank 0: each rank's descriptors (desc holds its
-    nar_first[-1] descriptors, 48 B each) and its NAR -> first-descriptor index.
-    Shards are contiguous NAR ranges in rank order (shard_nars), so rank 0 rebuilds the
-    whole batch in global NAR order: returns (uint8 tensor of all descriptors on rank
-    0's device, global nar_first as np.uint64[n_total + 1]) on rank 0, None elsewhere."""
+def gather_shape(desc_cap: int, n_nars: int, group=None) -> tuple[int, int]:
+    """(largest descriptor capacity, largest NAR count) over the ranks: the padded sizes
+    of gather_batch_async's two per-rank buffers.  One all_gather, once per batch shape
+    (bench.py calls it before the timed region), so the per-step gather needs no count
+    exchange and no host sync."""
+    dev = _device_for(group)
+    t = torch.tensor([desc_cap, n_nars], dtype=torch.int64, device=dev)
+    world = dist.get_world_size(group)
+    parts = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(parts, t, group=group)
+    both = torch.stack(parts).cpu()
+    return int(both[:, 0].max()), int(both[:, 1].max())
+
+
+def _device_for(group=None):
+    return torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+
+
+class GatheredBatch:
+    """A gather queued by gather_batch_async: on rank 0 the per-rank padded buffers
+    (filled when the current stream reaches the collectives); `assemble()` waits for them
+    and returns (uint8 tensor of every descriptor in global NAR order, global nar_first
+    as np.uint64[n_total + 1])."""
+
+    def __init__(self, meta, descs):
+        self.meta, self.descs = meta, descs
+
+    def assemble(self):
+        metas = [m.cpu().numpy() for m in self.meta]  # the one host sync, off the step's path
+        parts, firsts, base = [], [np.zeros(1, np.uint64)], 0
+        for m, d in zip(metas, self.descs):
+            n_nars, n_desc = int(m[0]), int(m[1])
+            f = m[2:3 + n_nars].astype(np.uint64)
+            parts.append(d[: n_desc * DESC_BYTES])
+            firsts.append(f[1:] + np.uint64(base))
+            base += n_desc
+        return torch.cat(parts), np.concatenate(firsts)
+
+
+def gather_batch_async(desc: torch.Tensor, nar_first, max_cap: int, max_nars: int, group=None):
+    """Queue the gather of this rank's batch to rank 0 on the current stream, with no host
+    sync: two collectives of fixed size (gather_shape), the rank's metadata {n_nars,
+    n_descriptors, nar_first[0..n_nars]} padded to max_nars and its descriptor array
+    padded to max_cap (desc must hold max_cap * 48 bytes, or it is copied into a buffer
+    that does).  Returns a GatheredBatch on rank 0, None elsewhere.  The collectives read
+    `desc` on the process group's stream after the current stream's queued work: record
+    an event after this call before anything overwrites `desc` (bench.py)."""
     first = np.asarray(nar_first, dtype=np.uint64)
-    n = int(first[-1])
-    parts = gather_descriptors(desc, n, group=group)
-    dev = desc.device
-    # NAR indices travel as one more gather (n_nars + 1 u64 per rank, padded)
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    cnt = torch.tensor([len(first)], dtype=torch.int64, device=dev)
-    cnts = [torch.zeros_like(cnt) for _ in range(world)]
-    dist.all_gather(cnts, cnt, group=group)
-    lens = [int(c.item()) for c in cnts]
-    mx = max(lens)
-    buf = torch.zeros(mx, dtype=torch.int64, device=dev)
-    buf[: len(first)] = torch.from_numpy(first.astype(np.int64)).to(dev)
-    gl = [torch.empty(mx, dtype=torch.int64, device=dev) for _ in range(world)] if rank == 0 else None
-    dist.gather(buf, gl, dst=0, group=group)
-    if rank != 0:
-        return None
-    firsts, base = [np.zeros(1, np.uint64)], 0
-    for g, ln in zip(gl, lens):
-        f = g[:ln].cpu().numpy().astype(np.uint64)
-        firsts.append(f[1:] + np.uint64(base))
-        base += int(f[-1])
-    return torch.cat(parts) if parts else desc[:0], np.concatenate(firsts)
+    dev = desc.device
+    meta_h = np.zeros(max_nars + 3, np.int64)
+    meta_h[0], meta_h[1] = len(first) - 1, int(first[-1])
+    meta_h[2:2 + len(first)] = first.astype(np.int64)
+    meta = torch.from_numpy(meta_h)
+    if dev.type == "cuda":
+        meta = meta.pin_memory().to(dev, non_blocking=True)
+    want = max_cap * DESC_BYTES
+    buf = desc[:want]
+    if buf.numel() < want:
+        buf = torch.cat([buf, torch.zeros(want - buf.numel(), dtype=torch.uint8, device=dev)])
+    gm = [torch.empty_like(meta) for _ in range(world)] if rank == 0 else None
+    gd = [torch.empty(want, dtype=torch.uint8, device=dev) for _ in range(world)] if rank == 0 else None
+    dist.gather(meta, gm, dst=0, group=group)
+    dist.gather(buf.contiguous(), gd, dst=0, group=group)
+    return GatheredBatch(gm, gd) if rank == 0 else None
+
+
+def gather_batch(desc: torch.Tensor, nar_first, group=None):
+    """Gather a sharded batch to rank 0 and wait for it: each rank's descriptors (desc
+    holds its nar_first[-1] descriptors, 48 B each) and its NAR -> first-descriptor index.
+    Shards are contiguous NAR ranges in rank order (shard_nars), so rank 0 rebuilds the
+    whole batch in global NAR order: returns (uint8 tensor of all descriptors on rank 0's
+    device, global nar_first as np.uint64[n_total + 1]) on rank 0, None elsewhere."""
+    first = np.asarray(nar_first, dtype=np.uint64)
+    n = int(first[-1])
+    max_cap, max_nars = gather_shape(max(n, 1), len(first) - 1, group=group)
+    g = gather_batch_async(desc[: n * DESC_BYTES], first, max_cap, max_nars, group=group)
+    return g.assemble() if g is not None else None
 
 
 def check_gathered_batch(descs: np.ndarray, first, nar_sizes) -> None:

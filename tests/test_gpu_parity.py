@@ -138,6 +138,63 @@ def test_piece_walks(ca, O, params):
 
 
 @pytest.mark.parametrize("algo", [SHA, B3], ids=["sha256", "blake3"])
+def tail_cut_case(O, params, tail_len, back, seed):
+    """Bytes whose FastCDC cut lands `back` bytes before the end of a buffer whose length
+    is 2 or 3 (mod 4): the last partial dword's bytes decide the cut.  (cut_gear tests
+    positions up to 2 floor(len/2) - 1, so with len = 2 (mod 4) back is 1 or 2, with
+    len = 3 (mod 4) it is 2 or 3.)  Built by choosing three bytes so that the Gear hash at
+    position len - back matches mask_s, then keeping a case whose first cut the oracle
+    puts there (no earlier position in the hashed region matches)."""
+    mn, avg, mx = params
+    bits = int(round(np.log2(avg)))
+    mask_s = int(O.MASKS[bits + 1])
+    G = O.GEAR.astype(np.uint64)
+    rng = np.random.default_rng(seed)
+    n = mn + 96 + tail_len
+    assert n % 4 in (2, 3) and n < avg and n - back <= 2 * (n // 2) - 1
+    for _ in range(64):
+        data = rng.integers(0, 256, n, dtype=np.uint8)
+        p = n - back  # the position whose hash must match
+        w = 0  # windowed Gear hash up to p - 3 (bits <= 47 are exact after 48 bytes)
+        for b in data[p - 3 - 60:p - 2]:
+            w = ((w << 1) + int(G[b])) & (2 ** 64 - 1)
+        x = np.arange(1 << 24, dtype=np.uint32)
+        b0, b1, b2 = (x & 255), ((x >> 8) & 255), (x >> 16)
+        h = np.uint64((w << 3) & (2 ** 64 - 1)) + (G[b0] << np.uint64(2)) + (G[b1] << np.uint64(1)) + G[b2]
+        hit = np.flatnonzero((h & np.uint64(mask_s)) == 0)
+        for v in hit[:32]:
+            data[p - 2:p + 1] = [v & 255, (v >> 8) & 255, v >> 16]
+            cuts = O.fastcdc(data, mn, avg, mx)
+            if len(cuts) >= 2 and n - (cuts[0][0] + cuts[0][1]) <= 3:
+                return data, cuts
+    raise AssertionError("no tail-cut case found")
+
+
+@pytest.mark.parametrize("tail,back", [(2, 1), (2, 2), (3, 2), (3, 3)], ids=["n2b1", "n2b2", "n3b2", "n3b3"])
+def test_cut_in_last_partial_dword(ca, O, tail, back):
+    """a batch whose length is not a multiple of 4 with a real FastCDC cut in
+    its last 3 bytes.  K1 reads the batch's last rows through a buffer resource; the
+    candidates there must come from the real bytes of the last (partial) dword, on the
+    prefiltered flat kernel (avg 64 KiB) and the dense kernel (avg 4 KiB)."""
+    for params in ((16384, 65536, 262144), (1024, 4096, 16384)):
+        data, cuts = tail_cut_case(O, params, tail + 4 * 200, back, seed=back * 7 + tail + params[1])
+        for algo in (SHA, B3):
+            got = ca.chunking.chunk_descriptors_array(bytes(data), *params, hash=algo)
+            ref = O.chunk_descriptors(data, *params, algo=algo)
+            assert_same(got, ref, f"tail cut back={back} {params}")
+            assert [(int(d["offset"]), int(d["length"])) for d in got] == cuts
+        # the device entry over an exactly-sized device buffer (no slack after the batch)
+        import torch
+
+        d = torch.from_numpy(data.copy()).to("cuda")
+        offs = np.array([0, len(data)], np.uint64)
+        cap = ca.chunking.batch_capacity(offs, params[0])
+        out = torch.empty(cap * 48, dtype=torch.uint8, device="cuda")
+        first = ca.chunk_batch_device(d.data_ptr(), offs, out.data_ptr(), cap, *params, hash=SHA)
+        got = out[: int(first[-1]) * 48].cpu().numpy().view(ca.DESC_DTYPE)
+        assert_same(got, O.chunk_descriptors(data, *params, algo=SHA), "device entry")
+
+
 def test_batch_ragged_unaligned(ca, O, algo):
     rng = np.random.default_rng(99)
     lens = [0, 1, 7, 1023, 1024, 1025, 65_535, 100_001, 0, 333_333, 1_048_577, 2_000_003, 5, 4_194_305]
@@ -624,6 +681,33 @@ def test_scan_paths_agree(ca, O, path):
             assert_same(got, O.chunk_descriptors(dense, *params, algo=algo), f"path={path} dense algo={algo}")
     finally:
         ca.lib.cg_test_scan_path(old)
+
+
+@pytest.mark.parametrize("oneshot", [0, 1], ids=["persistent", "oneshot"])
+def test_scan_kernels_agree(ca, O, oneshot):
+    """K1's persistent form (k_scan_flat32p: resident grid, per-XCD unit queue, halo row
+    per unit) and the one-shot k_scan_flat32 (cg_test_scan_kernel) both give the oracle's
+    descriptors on batches whose NAR and unit seams fall everywhere: units of 8 segments
+    (32 KiB) against NARs of odd lengths, a batch of many tiny NARs, a batch ending inside
+    a unit's first row, one with fewer units than waves, and back-to-back launches (the
+    queue must come back zeroed after each)."""
+    rng = np.random.default_rng(77 + oneshot)
+    params = (16384, 65536, 262144)  # 16 prefilter bits: the flat kernels
+    batches = [
+        [rng.integers(0, 256, n, dtype=np.uint8) for n in (32768 * 3 + 5, 2048, 1, 32767, 65536 + 2049, 500_001)],
+        [rng.integers(0, 256, int(n), dtype=np.uint8) for n in rng.integers(1, 9000, 300)],
+        [rng.integers(0, 256, 32768 * 5 + 100, dtype=np.uint8)],
+        [rng.integers(0, 256, 6_000_011, dtype=np.uint8), rng.integers(0, 256, 2_000_000, dtype=np.uint8)],
+    ]
+    old = ca.lib.cg_test_scan_kernel(oneshot)
+    try:
+        for rep in range(2):
+            for b, nars in enumerate(batches):
+                got = ca.chunk_batch(nars, *params, hash=SHA)
+                for i, nar in enumerate(nars):
+                    assert_same(got[i], O.chunk_descriptors(nar, *params, algo=SHA), f"oneshot={oneshot} b{b} nar{i}")
+    finally:
+        ca.lib.cg_test_scan_kernel(old)
 
 
 @pytest.mark.parametrize("fused,packed", [(1, 1), (1, 0), (0, 0)], ids=["packed_leaves", "assembly_map", "plan_kernel"])

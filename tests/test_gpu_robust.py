@@ -114,6 +114,88 @@ def test_concurrent_device_callers_on_distinct_streams(ca, O):
             assert _same(descs[int(first[i]):int(first[i + 1])], ref), (t, i)
 
 
+def _coalesced_jobs(ca, n_threads, seed):
+    """Per thread: a batch of a few NARs of different shapes (ragged, tiny, one empty,
+    one holding several max-size chunks) on its own stream."""
+    import torch
+
+    rng = np.random.default_rng(seed)
+    jobs = []
+    for t in range(n_threads):
+        lens = [int(x) for x in rng.integers(1, 3 << 20, 3)] + [0, 77, 2 * P[2] + 5]
+        nars = [rng.integers(0, 256, n, dtype=np.uint8) for n in lens]
+        offs = np.zeros(len(nars) + 1, np.uint64)
+        np.cumsum(lens, out=offs[1:])
+        data = np.concatenate(nars)
+        d = torch.from_numpy(np.concatenate([data, np.zeros(16, np.uint8)])).cuda()
+        cap = ca.chunking.batch_capacity(offs, P[0])
+        out = torch.zeros(cap * 48, dtype=torch.uint8, device="cuda")
+        jobs.append((nars, offs, d, out, cap, torch.cuda.Stream()))
+    torch.cuda.synchronize()
+    return jobs
+
+
+def _run_threads(ca, jobs, reps=1):
+    firsts, errors = [None] * len(jobs), []
+    start = threading.Barrier(len(jobs))
+
+    def work(t):
+        try:
+            nars, offs, d, out, cap, s = jobs[t]
+            start.wait()
+            for _ in range(reps):
+                firsts[t] = ca.chunk_batch_device(d.data_ptr(), offs, out.data_ptr(), cap, *P, stream=s.cuda_stream)
+        except Exception as e:  # noqa: BLE001
+            errors.append((t, e))
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(len(jobs))]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=200)
+    return firsts, errors
+
+
+@pytest.mark.parametrize("coalesce", [1, 0], ids=["coalesced", "per_batch"])
+def test_concurrent_sha_callers_share_one_digest(ca, O, coalesce):
+    """Round 4 coalescer: concurrent callers of the synchronous device entry have their
+    SHA-256 digests merged into one launch (runtime.hip coalesced_sha256); every caller
+    still gets exactly its own batch's oracle descriptors (digests scattered back to the
+    right arrays, empty NARs and max-size chunks included), over several rounds of
+    groups; and the same with coalescing off (cg_test_coalesce)."""
+    import torch
+
+    old = ca.lib.cg_test_coalesce(coalesce)
+    try:
+        jobs = _coalesced_jobs(ca, 12, seed=5 + coalesce)
+        firsts, errors = _run_threads(ca, jobs, reps=3)
+    finally:
+        ca.lib.cg_test_coalesce(old)
+    assert not errors, errors
+    torch.cuda.synchronize()
+    for t, (nars, offs, d, out, cap, s) in enumerate(jobs):
+        descs = out.cpu().numpy().view(ca.DESC_DTYPE)
+        first = firsts[t]
+        for i, nar in enumerate(nars):
+            ref = O.chunk_descriptors(nar, *P, algo=1, nthreads=8)
+            assert _same(descs[int(first[i]):int(first[i + 1])], ref), (t, i)
+
+
+def test_coalesced_spin_guard_reaches_every_member(ca):
+    """A spin-guard expiry inside a merged digest fails every member's call with CG_E_IO
+    (the merged launch's error word is copied into each member's), and the next round is
+    exact again."""
+    jobs = _coalesced_jobs(ca, 6, seed=9)
+    old = ca.lib.cg_test_sha_spin_limit(0)
+    try:
+        _, errors = _run_threads(ca, jobs)
+    finally:
+        ca.lib.cg_test_sha_spin_limit(old)
+    assert len(errors) == len(jobs) and all(isinstance(e, ca.IoError) for _, e in errors), errors
+    firsts, errors = _run_threads(ca, jobs)
+    assert not errors, errors
+
+
 def test_sha_spin_guard_timeout_is_an_error(ca, O):
     """With the spin limit forced to 0 every hand-off wait expires at once: the kernel
     finishes (no hang) but flags the launch, and the call fails with CG_E_IO instead of

@@ -103,6 +103,47 @@ def test_chunk_data_async_and_helpers(ca, O, monkeypatch):
     assert ei.value.limit == 64 << 20 and ei.value.attempted > ei.value.limit
 
 
+class FailingAsyncReader(AsyncBytesReader):
+    """Reads `ok` bytes, then raises `exc` on every later read."""
+
+    def __init__(self, data, ok, exc):
+        super().__init__(data, steps=(65536,))
+        self._ok, self._exc = ok, exc
+
+    async def read(self, n=-1):
+        if self._pos >= self._ok:
+            self.reads += 1
+            raise self._exc
+        return await super().read(min(n, self._ok - self._pos) if n >= 0 else self._ok - self._pos)
+
+
+@pytest.mark.parametrize("exc,want", [(ConnectionResetError("peer reset"), "IoError"),
+                                      (asyncio.IncompleteReadError(b"", 10), "IncompleteReadError"),
+                                      (ValueError("bad frame"), "ValueError")],
+                         ids=["oserror", "incomplete_read", "valueerror"])
+def test_chunk_stream_async_first_reader_error_ends_stream(ca, exc, want):
+    """the first reader error of any kind ends ChunkStreamAsync (try_stream!
+    stops at the first Err, src/chunking.rs:987-998): an OSError surfaces as IoError, any
+    other exception as itself; the next iteration ends the stream instead of reading again."""
+    data = rand_bytes(1_000_000, 44)
+    rd = FailingAsyncReader(data, 300_000, exc)
+
+    async def run():
+        s = ca.ChunkStreamAsync(rd, *P)
+        got = []
+        with pytest.raises(Exception) as ei:
+            async for c in s:
+                got.append(c)
+        reads = rd.reads
+        rest = [c async for c in s]
+        return ei.value, got, rest, reads
+
+    err, got, rest, reads = asyncio.run(run())
+    assert type(err).__name__ == want
+    assert rest == [] and rd.reads == reads  # ended: no further read
+    assert sum(c.length for c in got) <= 300_000
+
+
 def test_stream_metrics_recorded_by_streaming_paths_only(ca):
     """chunker.chunks_emitted / bytes_processed / chunk_size are recorded per chunk by
     PushChunker, ChunkStream and ChunkStreamAsync, and not by chunk_data (as in the

@@ -14,7 +14,10 @@ def test_async_buffer_limit_clamp(monkeypatch):
     64 MiB..3 GiB, unparsable -> default."""
     monkeypatch.delenv("CHUNKER_ASYNC_BUFFER_LIMIT_BYTES", raising=False)
     assert chunking.effective_async_buffer_limit() == 2 << 30
-    for v, want in (("1", 64 << 20), (str(100 << 20), 100 << 20), (str(1 << 40), 3 << 30), ("x", 2 << 30)):
+    for v, want in (("1", 64 << 20), (str(100 << 20), 100 << 20), (str(1 << 40), 3 << 30), ("x", 2 << 30),
+                    # usize's parser: '+' accepted; '-', whitespace, '_' and overflow rejected -> default
+                    ("+100000000", 100000000), ("-1", 2 << 30), (" 5 ", 2 << 30), ("1_000", 2 << 30),
+                    (str(1 << 64), 2 << 30), ("\u0665", 2 << 30)):
         monkeypatch.setenv("CHUNKER_ASYNC_BUFFER_LIMIT_BYTES", v)
         assert chunking.effective_async_buffer_limit() == want, v
 
