@@ -137,7 +137,6 @@ def test_piece_walks(ca, O, params):
         assert_same(got[i], O.chunk_descriptors(nar, *params, algo=B3), f"nar{i} len={len(nar)}")
 
 
-@pytest.mark.parametrize("algo", [SHA, B3], ids=["sha256", "blake3"])
 def tail_cut_case(O, params, tail_len, back, seed):
     """Bytes whose FastCDC cut lands `back` bytes before the end of a buffer whose length
     is 2 or 3 (mod 4): the last partial dword's bytes decide the cut.  (cut_gear tests
@@ -195,6 +194,7 @@ def test_cut_in_last_partial_dword(ca, O, tail, back):
         assert_same(got, O.chunk_descriptors(data, *params, algo=SHA), "device entry")
 
 
+@pytest.mark.parametrize("algo", [SHA, B3], ids=["sha256", "blake3"])
 def test_batch_ragged_unaligned(ca, O, algo):
     rng = np.random.default_rng(99)
     lens = [0, 1, 7, 1023, 1024, 1025, 65_535, 100_001, 0, 333_333, 1_048_577, 2_000_003, 5, 4_194_305]
