@@ -51,7 +51,7 @@ EXPORTS = (
 )
 # test hooks the product library exports beyond the header (tier caps, spin-guard limit)
 TEST_HOOKS = ("cg_test_sha_quad_max", "cg_test_sha_split_max", "cg_test_sha_spin_limit", "cg_test_cas_pair_max",
-              "cg_test_fail_alloc", "cg_test_sha_quad_fill", "cg_test_sha_pair_fill", "cg_test_scan_path", "cg_test_scan_kernel", "cg_test_coalesce",
+              "cg_test_fail_alloc", "cg_test_sha_quad_fill", "cg_test_sha_pair_fill", "cg_test_scan_path", "cg_test_scan_kernel", "cg_test_coalesce", "cg_test_scan_grid",
               "cg_test_stream_group_cap", "cg_test_stream_max_lanes", "cg_test_stream_eager",
               "cg_test_b3_fused_plan", "cg_test_b3_packed")
 
@@ -143,6 +143,8 @@ def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
                  "cg_test_sha_pair_fill", "cg_test_scan_path", "cg_test_scan_kernel", "cg_test_coalesce"):
         getattr(L, name).argtypes = [u32]
         getattr(L, name).restype = u32
+    L.cg_test_scan_grid.argtypes = [u64]
+    L.cg_test_scan_grid.restype = u64
     L.cg_test_cas_pair_max.argtypes = [ctypes.c_int64]
     L.cg_test_cas_pair_max.restype = ctypes.c_int64
     if hasattr(L, "cg_test_stream_group_cap"):  # (absent from builds before round 3: A/B runs)

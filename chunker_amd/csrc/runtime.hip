@@ -267,14 +267,16 @@ uint32_t seg_slots(const CdcParams &p) {
 // reference's callers are concurrent: thread-per-connection HTTP,
 // crates/proto/nix/src/lib.rs:153-162; BEAM dirty schedulers, src/nif.rs:188-234) each
 // run their boundary stages on their own stream; their SHA-256 digests are then merged:
-// a caller whose boundary stages are queued submits its chunk list and blocks; when no
-// merged digest is in flight, one waiting caller becomes the leader, lets the callers
-// still launching their boundary stages submit too (at most kCoalWindow), and launches
-// ONE k_sha256 over every pending batch's chunks on the device's coalescer stream, after
-// each member's boundary stages (events).  Each member's stream then waits for that
-// launch's end, so its own tail (NAR index, spin-guard word) and its completion event
-// follow the merged digest.  A group of one runs the ordinary per-batch launch on the
-// member's own stream, so a lone caller's latency is unchanged.
+// a caller whose boundary stages are queued submits its chunk list and blocks; one waiting
+// caller becomes the leader, lets the callers still launching their boundary stages submit
+// too (at most kCoalWindow), and launches ONE k_sha256 over every pending batch's chunks,
+// after each member's boundary stages (events), on a coalescer set (stream + merged
+// buffers) no earlier group still uses.  Groups do not wait for one another: the next
+// leader forms the next group at once, on another set (at most kCoalSets per device; past
+// that, on the set whose digest ends first).  Each member's stream then waits for its
+// group's end, so its own tail (NAR index, spin-guard word) and its completion event follow
+// the merged digest.  A group of one runs the ordinary per-batch launch on the member's own
+// stream, so a lone caller's latency is unchanged.
 // ---------------------------------------------------------------------------
 struct CoalGroup {
     hipEvent_t done = nullptr;
@@ -283,19 +285,26 @@ struct CoalGroup {
     }
 };
 
+struct CoalSet {
+    hipStream_t stream = nullptr;
+    bool leased = false;               // a leader is launching on it
+    std::shared_ptr<CoalGroup> last;   // its latest merged digest
+    DevBuf mdesc, mabs, mtotal, morder, merr;
+};
+
 struct Coalescer {
     std::mutex mu;
     std::condition_variable cv;
     std::deque<CoalEntry *> pending;
-    int active = 0;        // SHA-256 device-entry callers that have not submitted yet
-    bool inflight = false;  // a merged digest is launched and not yet known to be complete
-    hipStream_t stream = nullptr;
-    DevBuf mdesc, mabs, mtotal, morder, merr;
+    int active = 0;         // SHA-256 device-entry callers that have not submitted yet
+    bool leading = false;   // a leader is collecting the next group
+    std::vector<std::unique_ptr<CoalSet>> sets;
 };
 Coalescer g_coal[64];
 thread_local CoalActive *t_coal_active = nullptr;
 std::atomic<uint32_t> g_coalesce{1};  // test hook cg_test_coalesce
 constexpr auto kCoalWindow = std::chrono::microseconds(3000);
+constexpr size_t kCoalSets = 8;
 
 Coalescer &coalescer(int dev) { return g_coal[(dev >= 0 && dev < 64) ? dev : 0]; }
 
@@ -316,11 +325,43 @@ void CoalActive::leave() {
     C.cv.notify_all();
 }
 
-// Launch one group (called by its leader without the lock).  Sets every member's group.
-static int launch_group(Coalescer &C, std::vector<CoalEntry *> &grp, std::shared_ptr<CoalGroup> &G) {
+static bool set_idle(const CoalSet &S) { return !S.last || hipEventQuery(S.last->done) == hipSuccess; }
+
+// Lease a set whose previous merged digest has ended (its buffers may be regrown).
+// Called with the lock held; may release it while waiting for a busy set.
+static CoalSet *lease_set(Coalescer &C, std::unique_lock<std::mutex> &lk) {
+    for (;;) {
+        CoalSet *oldest = nullptr;
+        for (auto &S : C.sets) {
+            if (S->leased) continue;
+            if (set_idle(*S)) {
+                S->leased = true;
+                return S.get();
+            }
+            if (!oldest) oldest = S.get();
+        }
+        if (C.sets.size() < kCoalSets) {
+            C.sets.push_back(std::make_unique<CoalSet>());
+            C.sets.back()->leased = true;
+            return C.sets.back().get();
+        }
+        if (!oldest) {  // every set is leased by another leader
+            C.cv.wait(lk);
+            continue;
+        }
+        std::shared_ptr<CoalGroup> g = oldest->last;
+        lk.unlock();
+        (void)hipEventSynchronize(g->done);
+        lk.lock();
+    }
+}
+
+// Launch one group (called by its leader without the lock).  A group of one runs on its
+// member's stream; a larger group on the leased set S.
+static int launch_group(CoalSet *S, std::vector<CoalEntry *> &grp, std::shared_ptr<CoalGroup> &G) {
     G = std::make_shared<CoalGroup>();
     HIP_TRY(hipEventCreateWithFlags(&G->done, hipEventDisableTiming));
-    if (grp.size() == 1) {  // a group of one: the ordinary launch on the member's stream
+    if (grp.size() == 1) {
         CoalEntry *e = grp[0];
         Workspace *ws = e->ws;
         cg::launch_sha256(e->d_data, e->d_abs, e->d_out, e->d_total, e->bound, e->expected, e->max_len,
@@ -331,7 +372,7 @@ static int launch_group(Coalescer &C, std::vector<CoalEntry *> &grp, std::shared
         return CG_OK;
     }
     int rc;
-    if (!C.stream) HIP_TRY(hipStreamCreateWithFlags(&C.stream, hipStreamNonBlocking));
+    if (!S->stream) HIP_TRY(hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking));
     cg::CoalTable t{};
     uint64_t bound = 0, expected = 0, max_len = 0;
     t.n = (uint32_t)grp.size();
@@ -346,18 +387,18 @@ static int launch_group(Coalescer &C, std::vector<CoalEntry *> &grp, std::shared
         bound += e->bound;
         expected += e->expected;
         max_len = std::max<uint64_t>(max_len, e->max_len);
-        HIP_TRY(hipStreamWaitEvent(C.stream, e->ready, 0));
+        HIP_TRY(hipStreamWaitEvent(S->stream, e->ready, 0));
     }
-    // (growing a buffer frees the old one: only while no merged digest is in flight)
-    if ((rc = C.mdesc.ensure((bound + 1) * sizeof(DescRaw), "coalesced descriptors"))) return rc;
-    if ((rc = C.mabs.ensure((bound + 1) * 8, "coalesced addresses"))) return rc;
-    if ((rc = C.mtotal.ensure(64, "coalesced total"))) return rc;
-    if ((rc = C.morder.ensure(cg::sha256_order_tmp_elems(bound) * 4, "coalesced order"))) return rc;
-    if ((rc = C.merr.ensure(64, "coalesced spin guard"))) return rc;
-    cg::launch_sha256_coalesced(t, bound, expected, max_len, C.mdesc.as<DescRaw>(), C.mabs.as<uint64_t>(),
-                                C.mtotal.as<uint64_t>(), C.morder.as<uint32_t>(), C.merr.as<uint32_t>(), C.stream);
+    // (the set's previous digest has ended, so growing a buffer frees nothing in use)
+    if ((rc = S->mdesc.ensure((bound + 1) * sizeof(DescRaw), "coalesced descriptors"))) return rc;
+    if ((rc = S->mabs.ensure((bound + 1) * 8, "coalesced addresses"))) return rc;
+    if ((rc = S->mtotal.ensure(64, "coalesced total"))) return rc;
+    if ((rc = S->morder.ensure(cg::sha256_order_tmp_elems(bound) * 4, "coalesced order"))) return rc;
+    if ((rc = S->merr.ensure(64, "coalesced spin guard"))) return rc;
+    cg::launch_sha256_coalesced(t, bound, expected, max_len, S->mdesc.as<DescRaw>(), S->mabs.as<uint64_t>(),
+                                S->mtotal.as<uint64_t>(), S->morder.as<uint32_t>(), S->merr.as<uint32_t>(), S->stream);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(G->done, C.stream));
+    HIP_TRY(hipEventRecord(G->done, S->stream));
     return CG_OK;
 }
 
@@ -377,8 +418,8 @@ int coalesced_sha256(CoalEntry *e) {
     }
     C.cv.notify_all();
     while (!e->group && !e->rc) {
-        if (!C.inflight && !C.pending.empty()) {
-            C.inflight = true;  // this thread leads the next group
+        if (!C.leading && !C.pending.empty()) {
+            C.leading = true;  // this thread leads the next group
             const auto t0 = std::chrono::steady_clock::now();
             while (C.active > 0 && C.pending.size() < CG_COAL_MAX && std::chrono::steady_clock::now() - t0 < kCoalWindow)
                 C.cv.wait_for(lk, std::chrono::microseconds(100));
@@ -387,20 +428,23 @@ int coalesced_sha256(CoalEntry *e) {
                 grp.push_back(C.pending.front());
                 C.pending.pop_front();
             }
+            C.leading = false;  // the next group may form while this one launches
+            CoalSet *S = grp.size() > 1 ? lease_set(C, lk) : nullptr;
             lk.unlock();
             std::shared_ptr<CoalGroup> G;
-            const int rc = launch_group(C, grp, G);
+            const int rc = launch_group(S, grp, G);
+            // a failed launch may have left merge work queued that reads the members'
+            // buffers: drain it before they return and release their workspaces
+            if (rc && S && S->stream) (void)hipStreamSynchronize(S->stream);
             lk.lock();
+            if (S) {
+                S->leased = false;
+                if (!rc) S->last = G;
+            }
             for (CoalEntry *m : grp) {
                 if (rc) m->rc = rc;
                 else m->group = G;
             }
-            C.cv.notify_all();
-            lk.unlock();
-            // the next group launches once this one has ended (its merged buffers are reused)
-            if (!rc) (void)hipEventSynchronize(G->done);
-            lk.lock();
-            C.inflight = false;
             C.cv.notify_all();
             continue;
         }

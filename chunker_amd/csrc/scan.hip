@@ -464,7 +464,7 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
                                                            ScanQueue *queue, uint32_t nunits) {
     __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * GEAR_COPIES];
     __shared__ uint32_t s_slots[SCAN2_T / 64][64];  // the open segment's candidate slots, per wave
-    constexpr uint32_t R = SPU * F32_RPS;           // rows per unit (even: the 2-row ring starts each unit at slot 0)
+    constexpr uint32_t R = SPU * F32_RPS;           // rows per unit
     constexpr uint32_t UNIT = SPU * CG_SEG;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -472,39 +472,55 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     xcc &= 7u;
     typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-    // a unit's rows through a buffer resource based at the unit, its size ending at the batch
-    // end rounded up to the 16-byte granule (k_scan_flat32)
-    auto rsrc_of = [&](uint32_t u) {
+    // A unit's rows through a buffer resource based at its halo row (the row before the unit;
+    // at the batch start, the unit itself), its size ending at the batch end rounded up to the
+    // 16-byte granule (k_scan_flat32).  The halo is entry 0 of the unit's stream, data row j
+    // entry j + 1 at byte hoff + j x 2 KiB of the resource.
+    struct UnitRs {
+        __amdgpu_buffer_rsrc_t rs;
+        uint32_t hoff;  // 2 KiB, or 0 for the batch's first unit (no halo: its "halo" is row 0, unused)
+    };
+    auto unit_rs = [&](uint32_t u) {
         const uint64_t r0 = (uint64_t)u * UNIT;
-        const uint64_t avail = r0 < n ? ((n - r0 + 15) & ~15ull) : 0;
-        return __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(data + (r0 < n ? r0 : 0)), (short)0,
-                                                 (int)(avail < UNIT ? avail : UNIT), 0x00027000);
+        const uint64_t base = r0 >= F32_ROW ? r0 - F32_ROW : 0;
+        const uint64_t avail = base < n ? ((n - base + 15) & ~15ull) : 0;
+        const uint64_t span = UNIT + (r0 - base);
+        return UnitRs{__builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(data + (base < n ? base : 0)), (short)0,
+                                                        (int)(avail < span ? avail : span), 0x00027000),
+                      (uint32_t)(r0 - base)};
     };
     const uint32_t lane_off = 32u * lane;
-    auto blk = [&](__amdgpu_buffer_rsrc_t rs, uint32_t row, uint4 (&v)[2]) {
-        const uint32_t so = row * F32_ROW;
+    auto blk = [&](__amdgpu_buffer_rsrc_t rs, uint32_t so, uint4 (&v)[2]) {
         const u32x4_t x0 = __builtin_amdgcn_raw_buffer_load_b128(rs, lane_off, so, 2);  // aux 2: nt
         const u32x4_t x1 = __builtin_amdgcn_raw_buffer_load_b128(rs, lane_off + 16u, so, 2);
         v[0] = uint4{x0.x, x0.y, x0.z, x0.w};
         v[1] = uint4{x1.x, x1.y, x1.z, x1.w};
     };
-    // the row before unit u (its hash carries into the unit's first lanes); unit 0 has none
-    auto halo = [&](uint32_t u, uint4 (&v)[2]) {
-        const uint64_t r0 = (uint64_t)u * UNIT;
-        const uint64_t a = (r0 >= F32_ROW && r0 < n ? r0 - F32_ROW : 0) + lane_off;
-        v[0] = *reinterpret_cast<const uint4 *>(data + a);
-        v[1] = *reinterpret_cast<const uint4 *>(data + a + 16);
+    // One unit index, wave-uniform; nunits when every range is empty.  The add on this XCD's
+    // head is issued at a unit's start and read half a unit later (the compiler's atomic
+    // optimizer is off for this file, so the returning atomic is one instruction and the
+    // wait for it lands at the read); only once this XCD's range is empty are the other
+    // heads tried, one at a time.
+    const uint32_t own_lo = (uint32_t)((uint64_t)nunits * xcc / 8);
+    const uint32_t own_n = (uint32_t)((uint64_t)nunits * (xcc + 1) / 8) - own_lo;
+    uint32_t tick = 0;
+    auto dq_issue = [&]() {
+        if (lane == 0) tick = __hip_atomic_fetch_add(&queue->head[xcc][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
-    // one unit index, wave-uniform; nunits when every range is empty
-    auto dequeue = [&]() -> uint32_t {
-        for (uint32_t k = 0; k < 8; ++k) {
+    // `dep`: a value of the row loop, so the read stays where it is written (without it the
+    // compiler hoists the read out of the row loop, to right after the issue)
+    auto dq_resolve = [&](uint32_t dep) -> uint32_t {
+        asm volatile("" : "+v"(tick) : "v"(dep));
+        const uint32_t i = __builtin_amdgcn_readfirstlane(tick);
+        if (i < own_n) return own_lo + i;
+        for (uint32_t k = 1; k < 8; ++k) {
             const uint32_t x = (xcc + k) & 7u;
             const uint32_t lo = (uint32_t)((uint64_t)nunits * x / 8), hi = (uint32_t)((uint64_t)nunits * (x + 1) / 8);
             if (lo == hi) continue;
-            uint32_t i = 0;
-            if (lane == 0) i = __hip_atomic_fetch_add(&queue->head[x][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            i = __builtin_amdgcn_readfirstlane(i);
-            if (i < hi - lo) return lo + i;
+            uint32_t j = 0;
+            if (lane == 0) j = __hip_atomic_fetch_add(&queue->head[x][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            j = __builtin_amdgcn_readfirstlane(j);
+            if (j < hi - lo) return lo + j;
         }
         return nunits;
     };
@@ -512,13 +528,15 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
     static_assert(SCAN2_T == 2 * 256 && GEAR_COPIES == 32, "two threads per Gear entry, 16 copies each");
     const uint32_t ge = threadIdx.x >> 1;
     const uint64_t gv = gear_g[ge] << SCAN_SHIFT;
-    uint32_t u = dequeue();
+    dq_issue();
+    uint32_t u = dq_resolve(0u);
     const bool any = u < nunits;
-    __amdgpu_buffer_rsrc_t rs = rsrc_of(any ? u : 0);
-    uint4 ring[2][2], pro[2];
-    blk(rs, 0, ring[0]);
-    blk(rs, 1, ring[1]);
-    halo(any ? u : 0, pro);
+    UnitRs ur = unit_rs(any ? u : 0);
+    // the ring: two stream entries in flight; a unit starts with its halo in slot 0 and its
+    // row 0 in slot 1
+    uint4 ring[2][2];
+    blk(ur.rs, 0, ring[0]);
+    blk(ur.rs, ur.hoff, ring[1]);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (uint32_t j = 0; j < 16; ++j) s_gear[ge * GEAR_COPIES + (((threadIdx.x & 1u) * 16u + j + ge) & 31u)] = gv;
@@ -565,45 +583,48 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
         const uint64_t r0 = (uint64_t)u * UNIT;
         const uint64_t seg0 = (uint64_t)u * SPU;
         const uint64_t end_rel = n - r0;  // > 0: units start inside the batch
-        // the next unit: dequeued now, its halo row and first two rows issued as the current
-        // unit's rows free their ring slots
-        const uint32_t un = dequeue();
-        const bool more = un < nunits;
-        const __amdgpu_buffer_rsrc_t rs_next = rsrc_of(more ? un : u);
-        // zero state at the batch start, as the crate's hash restart
+        // the next unit: its head add issued now and read half a unit later, its halo and row
+        // 0 issued as this unit's last two rows free their slots
+        dq_issue();
+        uint32_t un = nunits;
+        bool more = false;
+        UnitRs urn = ur;
+        // halo (slot 0): zero state at the batch start, as the crate's hash restart
         uint64_t R1 = 0;
         uint32_t R2 = 0;
-        if (r0 >= F32_ROW) {
+        {
             uint64_t q[8][4];
-            partials(pro, q);
-            const uint64_t P = block_p(q);
-            R1 = ((uint64_t)wave_ror1((uint32_t)(P >> 32)) << 32) | wave_ror1((uint32_t)P);
-            R2 = wave_ror1((uint32_t)R1);
+            partials(ring[0], q);
+            blk(ur.rs, ur.hoff + F32_ROW, ring[0]);  // row 1
+            if (r0 >= F32_ROW) {
+                const uint64_t P = block_p(q);
+                R1 = ((uint64_t)wave_ror1((uint32_t)(P >> 32)) << 32) | wave_ror1((uint32_t)P);
+                R2 = wave_ror1((uint32_t)R1);
+            }
         }
-        halo(more ? un : u, pro);
         uint32_t segc = 0;
 #pragma unroll 1
         for (uint32_t r = 0; r < R; r += 2) {
+            if (r == ((R / 2) & ~1u)) {  // uniform: read the next unit's index
+                un = dq_resolve((uint32_t)R1);
+                more = un < nunits;
+                urn = unit_rs(more ? un : u);
+            }
 #pragma unroll
             for (uint32_t uu = 0; uu < 2; ++uu) {
                 const uint32_t row = r + uu;
-                const bool nx_here = row + 2 < R;  // uniform: the slot's next row is in this unit
+                const uint32_t slot = uu ^ 1u;  // data row j sits in slot (j + 1) & 1
+                // the entry two ahead: row + 2 of this unit, else the next unit's halo / row 0
+                const uint32_t e = row + 2;
+                const __amdgpu_buffer_rsrc_t nrs = e < R ? ur.rs : urn.rs;
+                const uint32_t nso = e < R ? ur.hoff + e * F32_ROW : (e == R ? 0u : urn.hoff);
+                // (a row past the batch end -- the last unit's -- takes the tail path below with
+                // every position masked: the slot's loads stay on one code path, so the compiler
+                // counts vmcnt exactly)
                 const uint64_t rowb = (uint64_t)row * F32_ROW;
-                if (rowb >= end_rel) {  // a row past the batch end (the last unit only): nothing to hash
-                    blk(nx_here ? rs : rs_next, nx_here ? row + 2 : row + 2 - R, ring[uu]);
-                    if (uu == 1) {
-                        const uint64_t seg = seg0 + row / F32_RPS;
-                        if (seg < nseg) {
-                            if (lane < min(segc, cap)) seg_cand[seg * cap + lane] = slots[lane];
-                            if (lane == 0) seg_count[seg] = segc;
-                        }
-                        segc = 0;
-                    }
-                    continue;
-                }
                 uint64_t q[8][4];
-                partials(ring[uu], q);
-                blk(nx_here ? rs : rs_next, nx_here ? row + 2 : row + 2 - R, ring[uu]);  // re-issue the slot now
+                partials(ring[slot], q);
+                blk(nrs, nso, ring[slot]);  // re-issue the slot now
                 const uint64_t P = block_p(q);
                 const uint32_t a_lo = wave_ror1_add((uint32_t)P, zero), a_hi = wave_ror1_add((uint32_t)(P >> 32), zero);
                 const uint32_t p1_lo = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)R1, a_lo, 0xCA);
@@ -704,8 +725,15 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
             }
         }
         if (!more) break;
+        // the next unit's halo went to slot 1 and its row 0 to slot 0: swap them into place
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const uint4 t = ring[0][k];
+            ring[0][k] = ring[1][k];
+            ring[1][k] = t;
+        }
         u = un;
-        rs = rs_next;
+        ur = urn;
     }
     // leave: the last wave of the grid resets the queue for the next launch
     if (lane == 0) {
@@ -741,6 +769,8 @@ void launch_k_scan_pre(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear
 
 // test hook (cg_test_scan_kernel): 1 = the one-shot k_scan_flat32 instead of the persistent form
 uint32_t g_scan_oneshot = 0;
+// test hook (cg_test_scan_grid): workgroups of the persistent scan (0 = the resident count)
+uint64_t g_scan_grid = 0;
 
 void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint64_t mask_s, uint64_t mask_l,
                  uint32_t cap, uint32_t *d_seg_count, uint32_t *d_seg_cand, uint64_t nseg, hipStream_t st,
@@ -793,7 +823,8 @@ void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint
         const uint64_t nunits = (nseg + CG_SCAN_SPU - 1) / CG_SCAN_SPU;
         const uint64_t resident = scan_resident_wgs();
         const uint64_t want = (nunits + SCAN2_T / 64 - 1) / (SCAN2_T / 64);  // >= one unit per wave
-        const uint64_t grid = std::max<uint64_t>(1, std::min(want, resident));
+        uint64_t grid = std::max<uint64_t>(1, std::min(want, resident));
+        if (g_scan_grid) grid = g_scan_grid;
         hipLaunchKernelGGL(k_scan_flat32p<CG_SCAN_SPU>, dim3((uint32_t)grid), dim3(SCAN2_T), 0, st, d_data, n, d_gear,
                            mask_s, mask_l, cap, d_seg_count, d_seg_cand, nseg, d_queue, (uint32_t)nunits);
         return;
@@ -1034,6 +1065,12 @@ void launch_scan_compact(const uint32_t *d_seg_count, const uint32_t *d_seg_cand
 }
 
 }  // namespace cg
+
+// grid override of the persistent scan (0 = resident workgroups); returns the resident count
+extern "C" uint64_t cg_test_scan_grid(uint64_t v) {
+    cg::g_scan_grid = v;
+    return cg::scan_resident_wgs();
+}
 
 extern "C" uint32_t cg_test_scan_kernel(uint32_t v) {
     const uint32_t old = cg::g_scan_oneshot;

@@ -26,23 +26,26 @@ ap.add_argument("--configs", default="c2,c4,c5")
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--kernels", default="0,1", help="cg_test_scan_kernel values: 0 persistent, 1 one-shot")
 ap.add_argument("--hash", type=int, default=1)
+ap.add_argument("--grids", default="0", help="persistent-scan grid overrides to sweep (cg_test_scan_grid; 0 = resident)")
 args = ap.parse_args()
 torch.cuda.set_device(0)
 lib = ca.lib
 buf = (ctypes.c_double * 5)()
-res = {"lib": os.environ.get("CHUNKER_AMD_LIB", "product")}
+res = {"lib": os.environ.get("CHUNKER_AMD_LIB", "product"), "resident_wgs": int(lib.cg_test_scan_grid(0))}
+grids = [int(g) for g in args.grids.split(",")]
 for cfg in args.configs.split(","):
     n, size, params = SHAPES[cfg]
     d, offs = synth_nars_device(np.full(n, size, np.uint64))
     cap = ca.chunking.batch_capacity(offs, params[0])
     out = torch.empty(cap * 48, dtype=torch.uint8, device="cuda")
     sp = torch.cuda.current_stream().cuda_stream
-    kinds = [int(k) for k in args.kernels.split(",")]
+    kinds = [(int(k), g) for k in args.kernels.split(",") for g in (grids if int(k) == 0 else [0])]
     ms = {k: [] for k in kinds}
     firsts = {}
     for rep in range(args.reps + 1):
         for k in kinds:
-            lib.cg_test_scan_kernel(k)
+            lib.cg_test_scan_kernel(k[0])
+            lib.cg_test_scan_grid(k[1])
             lib.cg_set_profiling(1)
             first = ca.chunk_batch_device(d.data_ptr(), offs, out.data_ptr(), cap, *params, hash=args.hash, stream=sp)
             lib.cg_last_stage_times(buf, 5)
@@ -52,10 +55,11 @@ for cfg in args.configs.split(","):
             assert np.array_equal(first, firsts[kinds[0]]), "kernels disagree on the chunk counts"
     lib.cg_set_profiling(0)
     lib.cg_test_scan_kernel(0)
+    lib.cg_test_scan_grid(0)
     nbytes = int(offs[-1])
     for k in kinds:
         med = float(np.median(ms[k]))
-        res[f"{cfg}_{'persistent' if k == 0 else 'oneshot'}"] = {
+        res[f"{cfg}_{'persistent' if k[0] == 0 else 'oneshot'}" + (f"_grid{k[1]}" if k[1] else "")] = {
             "ms": round(med, 4), "TBps": round(nbytes / (med * 1e-3) / 1e12, 3),
             "frac_8TBps": round(nbytes / (med * 1e-3) / 8e12, 4), "all_ms": [round(x, 4) for x in ms[k]]}
     del d, out
