@@ -271,9 +271,13 @@ uint32_t seg_slots(const CdcParams &p) {
 // caller becomes the leader, lets the callers still launching their boundary stages submit
 // too (at most kCoalWindow), and launches ONE k_sha256 over every pending batch's chunks,
 // after each member's boundary stages (events), on a coalescer set (stream + merged
-// buffers) no earlier group still uses.  Groups do not wait for one another: the next
-// leader forms the next group at once, on another set (at most kCoalSets per device; past
-// that, on the set whose digest ends first).  Each member's stream then waits for its
+// buffers) no earlier group still uses.  A device has coal_sets() sets (2 by default,
+// CHUNKER_AMD_COAL_SETS): the leader first leases a free set -- waiting for the oldest
+// group's end when every set is busy, while later callers join the pending list -- and
+// only then takes the pending callers as its group.  One set serialises the groups (a
+// group that missed the last launch then waits a whole chain before its own starts);
+// two let one group's chain overlap the next group's, and every other caller collects
+// into the group after.  Each member's stream then waits for its
 // group's end, so its own tail (NAR index, spin-guard word) and its completion event follow
 // the merged digest.  A group of one runs the ordinary per-batch launch on the member's own
 // stream, so a lone caller's latency is unchanged.
@@ -304,7 +308,17 @@ Coalescer g_coal[64];
 thread_local CoalActive *t_coal_active = nullptr;
 std::atomic<uint32_t> g_coalesce{1};  // test hook cg_test_coalesce
 constexpr auto kCoalWindow = std::chrono::microseconds(3000);
-constexpr size_t kCoalSets = 8;
+
+// coalescer sets per device (CHUNKER_AMD_COAL_SETS, 1..8; read once)
+static size_t coal_sets() {
+    static const size_t n = [] {
+        const char *e = getenv("CHUNKER_AMD_COAL_SETS");
+        char *end = nullptr;
+        const unsigned long v = e && *e ? strtoul(e, &end, 10) : 0;
+        return (e && *e && end && *end == 0 && v >= 1 && v <= 8) ? (size_t)v : (size_t)2;
+    }();
+    return n;
+}
 
 Coalescer &coalescer(int dev) { return g_coal[(dev >= 0 && dev < 64) ? dev : 0]; }
 
@@ -340,7 +354,7 @@ static CoalSet *lease_set(Coalescer &C, std::unique_lock<std::mutex> &lk) {
             }
             if (!oldest) oldest = S.get();
         }
-        if (C.sets.size() < kCoalSets) {
+        if (C.sets.size() < coal_sets()) {
             C.sets.push_back(std::make_unique<CoalSet>());
             C.sets.back()->leased = true;
             return C.sets.back().get();
@@ -420,6 +434,7 @@ int coalesced_sha256(CoalEntry *e) {
     while (!e->group && !e->rc) {
         if (!C.leading && !C.pending.empty()) {
             C.leading = true;  // this thread leads the next group
+            CoalSet *S = lease_set(C, lk);  // (callers arriving meanwhile join the group)
             const auto t0 = std::chrono::steady_clock::now();
             while (C.active > 0 && C.pending.size() < CG_COAL_MAX && std::chrono::steady_clock::now() - t0 < kCoalWindow)
                 C.cv.wait_for(lk, std::chrono::microseconds(100));
@@ -429,7 +444,10 @@ int coalesced_sha256(CoalEntry *e) {
                 C.pending.pop_front();
             }
             C.leading = false;  // the next group may form while this one launches
-            CoalSet *S = grp.size() > 1 ? lease_set(C, lk) : nullptr;
+            if (grp.size() == 1) {  // a group of one runs on its member's stream
+                S->leased = false;
+                S = nullptr;
+            }
             lk.unlock();
             std::shared_ptr<CoalGroup> G;
             const int rc = launch_group(S, grp, G);

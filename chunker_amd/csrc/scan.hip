@@ -735,14 +735,18 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
         u = un;
         ur = urn;
     }
-    // leave: the last wave of the grid resets the queue for the next launch
+    // leave: the last wave of the grid resets the queue for the next launch.  Relaxed:
+    // a wave counts itself done only after its last dequeue has returned, the counter
+    // guards no data, and the kernel's end publishes the reset.  (An acquire-release
+    // count made every wave write back and invalidate its XCD's L2 on the way out --
+    // buffer_wbl2 / buffer_inv sc1 -- dropping the lines the running waves had fetched.)
     if (lane == 0) {
         const uint32_t waves = gridDim.x * (SCAN2_T / 64);
-        const uint32_t old = __hip_atomic_fetch_add(&queue->done[0], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t old = __hip_atomic_fetch_add(&queue->done[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (old == waves - 1) {
 #pragma unroll
             for (int x = 0; x < 8; ++x) __hip_atomic_store(&queue->head[x][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&queue->done[0], 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&queue->done[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
