@@ -68,34 +68,34 @@ def _device_for(group=None):
 
 
 class GatheredBatch:
-    """A gather queued by gather_batch_async: on rank 0 the per-rank padded buffers
-    (filled when the current stream reaches the collectives); `assemble()` waits for them
+    """A gather queued by gather_batch_async: on rank 0 the per-rank packed buffers
+    (filled when the current stream reaches the collective); `assemble()` waits for them
     and returns (uint8 tensor of every descriptor in global NAR order, global nar_first
     as np.uint64[n_total + 1])."""
 
-    def __init__(self, meta, descs):
-        self.meta, self.descs = meta, descs
+    def __init__(self, parts, meta_bytes):
+        self.parts, self.meta_bytes = parts, meta_bytes
 
     def assemble(self):
-        metas = [m.cpu().numpy() for m in self.meta]  # the one host sync, off the step's path
-        parts, firsts, base = [], [np.zeros(1, np.uint64)], 0
-        for m, d in zip(metas, self.descs):
+        mb = self.meta_bytes
+        metas = [p[:mb].cpu().numpy().view(np.int64) for p in self.parts]  # the one host sync, off the step's path
+        descs, firsts, base = [], [np.zeros(1, np.uint64)], 0
+        for m, p in zip(metas, self.parts):
             n_nars, n_desc = int(m[0]), int(m[1])
             f = m[2:3 + n_nars].astype(np.uint64)
-            parts.append(d[: n_desc * DESC_BYTES])
+            descs.append(p[mb: mb + n_desc * DESC_BYTES])
             firsts.append(f[1:] + np.uint64(base))
             base += n_desc
-        return torch.cat(parts), np.concatenate(firsts)
+        return torch.cat(descs), np.concatenate(firsts)
 
 
 def gather_batch_async(desc: torch.Tensor, nar_first, max_cap: int, max_nars: int, group=None):
     """Queue the gather of this rank's batch to rank 0 on the current stream, with no host
-    sync: two collectives of fixed size (gather_shape), the rank's metadata {n_nars,
-    n_descriptors, nar_first[0..n_nars]} padded to max_nars and its descriptor array
-    padded to max_cap (desc must hold max_cap * 48 bytes, or it is copied into a buffer
-    that does).  Returns a GatheredBatch on rank 0, None elsewhere.  The collectives read
-    `desc` on the process group's stream after the current stream's queued work: record
-    an event after this call before anything overwrites `desc` (bench.py)."""
+    sync: ONE collective of fixed size (gather_shape) over a packed per-rank buffer --
+    metadata {n_nars, n_descriptors, nar_first[0..n_nars]} as int64 padded to max_nars,
+    then the descriptor array padded to max_cap.  Returns a GatheredBatch on rank 0, None
+    elsewhere.  The packing copies `desc` on the current stream, so once this returns
+    (and the stream has reached it) the caller may overwrite `desc`."""
     first = np.asarray(nar_first, dtype=np.uint64)
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
@@ -103,18 +103,16 @@ def gather_batch_async(desc: torch.Tensor, nar_first, max_cap: int, max_nars: in
     meta_h = np.zeros(max_nars + 3, np.int64)
     meta_h[0], meta_h[1] = len(first) - 1, int(first[-1])
     meta_h[2:2 + len(first)] = first.astype(np.int64)
-    meta = torch.from_numpy(meta_h)
-    if dev.type == "cuda":
-        meta = meta.pin_memory().to(dev, non_blocking=True)
+    meta = torch.from_numpy(meta_h.view(np.uint8))
+    mb = meta.numel()
     want = max_cap * DESC_BYTES
-    buf = desc[:want]
-    if buf.numel() < want:
-        buf = torch.cat([buf, torch.zeros(want - buf.numel(), dtype=torch.uint8, device=dev)])
-    gm = [torch.empty_like(meta) for _ in range(world)] if rank == 0 else None
-    gd = [torch.empty(want, dtype=torch.uint8, device=dev) for _ in range(world)] if rank == 0 else None
-    dist.gather(meta, gm, dst=0, group=group)
-    dist.gather(buf.contiguous(), gd, dst=0, group=group)
-    return GatheredBatch(gm, gd) if rank == 0 else None
+    n = min(desc.numel(), want, int(first[-1]) * DESC_BYTES)
+    packed = torch.zeros(mb + want, dtype=torch.uint8, device=dev)
+    packed[:mb].copy_(meta.pin_memory() if dev.type == "cuda" else meta, non_blocking=True)
+    packed[mb: mb + n].copy_(desc[:n], non_blocking=True)
+    gd = [torch.empty(mb + want, dtype=torch.uint8, device=dev) for _ in range(world)] if rank == 0 else None
+    dist.gather(packed, gd, dst=0, group=group)
+    return GatheredBatch(gd, mb) if rank == 0 else None
 
 
 def gather_batch(desc: torch.Tensor, nar_first, group=None):
