@@ -72,6 +72,7 @@ def parse_args():
     ap.add_argument("--no-concurrent", action="store_true", help="skip the K-batches-in-flight measurement")
     ap.add_argument("--concurrent", default="8,32", help="K values of the in-flight measurement")
     ap.add_argument("--concurrent-only", action="store_true", help="only the in-flight measurement (profiling)")
+    ap.add_argument("--concurrent-reps", type=int, default=3, help="batches per thread in the in-flight measurement")
     ap.add_argument("--e2e", default="1,8,16", help="K values of the host-to-host in-flight measurement ('' = skip)")
     ap.add_argument("--hw-queues", type=int, default=16, choices=range(0, 33), metavar="0..32",
                     help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's)")
@@ -352,7 +353,7 @@ def concurrent_rates(ca, torch, args, n_per, nar_bytes, params, algo):
     batch_bytes = int(jobs[0][1][-1])
     coal = bool(ca.lib.cg_test_coalesce(1))
     ca.lib.cg_test_coalesce(int(coal))
-    res = {"unit": "GiB/s", "batch": f"{n_per}x{nar_bytes >> 20}MiB", "reps": 3,
+    res = {"unit": "GiB/s", "batch": f"{n_per}x{nar_bytes >> 20}MiB", "reps": max(1, args.concurrent_reps),
            "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default (4)"),
            "digests": "coalesced (one SHA-256 launch per group of concurrent callers)" if coal and algo == 1
            else "one launch per batch"}

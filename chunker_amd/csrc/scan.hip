@@ -453,6 +453,12 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
 #ifndef CG_SCAN_SPU
 #define CG_SCAN_SPU 8u
 #endif
+#ifndef CG_SCAN_STATIC
+#define CG_SCAN_STATIC 0
+#endif
+#ifndef CG_SCAN_RESOLVE_LATE  // A/B: read the next unit's ticket at the unit's last row pair
+#define CG_SCAN_RESOLVE_LATE 0
+#endif
 static_assert(sizeof(ScanQueue) == 9 * 64, "one 64-B line per counter");
 
 template <uint32_t SPU>
@@ -504,12 +510,27 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
     const uint32_t own_lo = (uint32_t)((uint64_t)nunits * xcc / 8);
     const uint32_t own_n = (uint32_t)((uint64_t)nunits * (xcc + 1) / 8) - own_lo;
     uint32_t tick = 0;
+#if CG_SCAN_STATIC
+    // (A/B form: no queue; wave g of the grid takes units g, g + W, g + 2W, ...)
+    uint32_t snext = blockIdx.x * (SCAN2_T / 64) + wv;
+    const uint32_t sstride = gridDim.x * (SCAN2_T / 64);
+    auto dq_issue = [&]() {};
+#else
     auto dq_issue = [&]() {
         if (lane == 0) tick = __hip_atomic_fetch_add(&queue->head[xcc][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
+#endif
     // `dep`: a value of the row loop, so the read stays where it is written (without it the
     // compiler hoists the read out of the row loop, to right after the issue)
     auto dq_resolve = [&](uint32_t dep) -> uint32_t {
+#if CG_SCAN_STATIC
+        (void)dep;
+        const uint32_t si = snext;
+        snext += sstride;
+        return si < nunits ? si : nunits;
+#else
+        (void)0;
+#endif
         asm volatile("" : "+v"(tick) : "v"(dep));
         const uint32_t i = __builtin_amdgcn_readfirstlane(tick);
         if (i < own_n) return own_lo + i;
@@ -605,7 +626,7 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
         uint32_t segc = 0;
 #pragma unroll 1
         for (uint32_t r = 0; r < R; r += 2) {
-            if (r == ((R / 2) & ~1u)) {  // uniform: read the next unit's index
+            if (r == (CG_SCAN_RESOLVE_LATE ? R - 2 : ((R / 2) & ~1u))) {  // uniform: read the next unit's index
                 un = dq_resolve((uint32_t)R1);
                 more = un < nunits;
                 urn = unit_rs(more ? un : u);
