@@ -266,7 +266,7 @@ def main():
         "note": "digest stage: algorithmic bytes = every NAR byte once, / mean digest-stage duration over the "
                 "timed steps (HIP events around the digest only); scan stage (scan_kernel) from "
                 f"{PROFILE_STEPS} untimed steps with every stage timed",
-        "scan_kernel": {"kernel": scan_kernel_name(ca, params[1]),
+        "scan_kernel": {"kernel": scan_kernel_name(ca, params[1], total_bytes),
                         "achieved": round(total_bytes / (scan_ms * 1e-3) / 1e9, 2),
                         "frac": round(total_bytes / (scan_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                         "traffic": None},
@@ -497,15 +497,18 @@ def sha_chain_floor(ca, descs, dig_ms, clk=None):
     return res
 
 
-def scan_kernel_name(ca, avg):
-    """The K1 kernel launch_scan (scan.hip) picks for these params: k_scan_flat32 when the
-    prefilter sees >= 14 bits of mask_s & mask_l above bit 15, else k_scan."""
+def scan_kernel_name(ca, avg, nbytes):
+    """The K1 kernel launch_scan (scan.hip) picks for these params: k_scan when the
+    prefilter sees fewer than 14 bits of mask_s & mask_l above bit 15, else the persistent
+    k_scan_flat32p from 4 GiB (2^20 segments) on and the one-shot k_scan_flat32 below."""
     import math
 
     _, masks = ca.get_cdc_tables()
     bits = round(math.log2(avg))
     both = int(masks[bits + 1]) & int(masks[bits - 1])
-    return "k_scan_flat32" if bin(both >> 16).count("1") >= 14 else "k_scan"
+    if bin(both >> 16).count("1") < 14:
+        return "k_scan"
+    return "k_scan_flat32p" if (nbytes + 4095) // 4096 >= (1 << 20) else "k_scan_flat32"
 
 
 def pmc_traffic(config, kernels):

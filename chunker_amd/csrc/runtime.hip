@@ -268,19 +268,25 @@ uint32_t seg_slots(const CdcParams &p) {
 // crates/proto/nix/src/lib.rs:153-162; BEAM dirty schedulers, src/nif.rs:188-234) each
 // run their boundary stages on their own stream; their SHA-256 digests are then merged:
 // a caller whose boundary stages are queued submits its chunk list and blocks; one waiting
-// caller becomes the leader, lets the callers still launching their boundary stages submit
-// too (at most kCoalWindow), and launches ONE k_sha256 over every pending batch's chunks,
+// caller becomes the leader and launches ONE k_sha256 over every pending batch's chunks,
 // after each member's boundary stages (events), on a coalescer set (stream + merged
-// buffers) no earlier group still uses.  A device has coal_sets() sets (2 by default,
-// CHUNKER_AMD_COAL_SETS): the leader first leases a free set -- waiting for the oldest
-// group's end when every set is busy, while later callers join the pending list -- and
-// only then takes the pending callers as its group.  One set serialises the groups (a
-// group that missed the last launch then waits a whole chain before its own starts);
-// two let one group's chain overlap the next group's, and every other caller collects
-// into the group after.  Each member's stream then waits for its
-// group's end, so its own tail (NAR index, spin-guard word) and its completion event follow
-// the merged digest.  A group of one runs the ordinary per-batch launch on the member's own
-// stream, so a lone caller's latency is unchanged.
+// buffers) no earlier group still uses.
+//
+// Policy.  A merged launch sizes its tiers for the whole chip and lasts one chain (the
+// longest chunk's) whatever its size, so two merged launches do not overlap on the GPU
+// and the rate is set by how many batches each chain carries (K = 32 concurrent callers:
+// 199 GiB/s with one set, 100 with two sets -- halved groups, same chains --
+// profiles/r04_v4_conc_*).  So a device has ONE set by default (CHUNKER_AMD_COAL_SETS, up
+// to 8, for A/B) and the leader (1) leases it, waiting for the previous group's end while
+// later callers keep joining the pending list, then (2) waits up to kCoalWindow while
+// callers are still launching their boundary stages or fewer are pending than the
+// previous group held -- callers that just got their digests back re-enter within a
+// window, so a group that once split in two merges again instead of alternating (two
+// groups taking turns each carry half the batches per chain: K = 8, 60 vs 110 GiB/s) --
+// and (3) takes every pending caller (at most CG_COAL_MAX).  Each member's stream then
+// waits for its group's end, so its own tail (NAR index, spin-guard word) and its
+// completion event follow the merged digest.  A group of one runs the ordinary per-batch
+// launch on the member's own stream, so a lone caller's latency is unchanged.
 // ---------------------------------------------------------------------------
 struct CoalGroup {
     hipEvent_t done = nullptr;
@@ -302,6 +308,7 @@ struct Coalescer {
     std::deque<CoalEntry *> pending;
     int active = 0;         // SHA-256 device-entry callers that have not submitted yet
     bool leading = false;   // a leader is collecting the next group
+    size_t last_group = 1;  // the previous group's size: the next leader waits for as many
     std::vector<std::unique_ptr<CoalSet>> sets;
 };
 Coalescer g_coal[64];
@@ -315,7 +322,7 @@ static size_t coal_sets() {
         const char *e = getenv("CHUNKER_AMD_COAL_SETS");
         char *end = nullptr;
         const unsigned long v = e && *e ? strtoul(e, &end, 10) : 0;
-        return (e && *e && end && *end == 0 && v >= 1 && v <= 8) ? (size_t)v : (size_t)2;
+        return (e && *e && end && *end == 0 && v >= 1 && v <= 8) ? (size_t)v : (size_t)1;
     }();
     return n;
 }
@@ -436,13 +443,15 @@ int coalesced_sha256(CoalEntry *e) {
             C.leading = true;  // this thread leads the next group
             CoalSet *S = lease_set(C, lk);  // (callers arriving meanwhile join the group)
             const auto t0 = std::chrono::steady_clock::now();
-            while (C.active > 0 && C.pending.size() < CG_COAL_MAX && std::chrono::steady_clock::now() - t0 < kCoalWindow)
+            while ((C.active > 0 || C.pending.size() < C.last_group) && C.pending.size() < CG_COAL_MAX &&
+                   std::chrono::steady_clock::now() - t0 < kCoalWindow)
                 C.cv.wait_for(lk, std::chrono::microseconds(100));
             std::vector<CoalEntry *> grp;
             while (!C.pending.empty() && grp.size() < CG_COAL_MAX) {
                 grp.push_back(C.pending.front());
                 C.pending.pop_front();
             }
+            C.last_group = grp.size();
             C.leading = false;  // the next group may form while this one launches
             if (grp.size() == 1) {  // a group of one runs on its member's stream
                 S->leased = false;

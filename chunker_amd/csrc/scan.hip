@@ -451,13 +451,13 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
 // starts from zero without a memset.
 // ---------------------------------------------------------------------------
 #ifndef CG_SCAN_SPU
-#define CG_SCAN_SPU 8u
+#define CG_SCAN_SPU 16u
 #endif
 #ifndef CG_SCAN_STATIC
 #define CG_SCAN_STATIC 0
 #endif
-#ifndef CG_SCAN_RESOLVE_LATE  // A/B: read the next unit's ticket at the unit's last row pair
-#define CG_SCAN_RESOLVE_LATE 0
+#ifndef CG_SCAN_RESOLVE_LATE  // read the next unit's ticket at the unit's last row pair (else half-way)
+#define CG_SCAN_RESOLVE_LATE 1
 #endif
 static_assert(sizeof(ScanQueue) == 9 * 64, "one 64-B line per counter");
 
@@ -792,8 +792,9 @@ void launch_k_scan_pre(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear
 }
 #endif
 
-// test hook (cg_test_scan_kernel): 1 = the one-shot k_scan_flat32 instead of the persistent form
-uint32_t g_scan_oneshot = 0;
+// test hook (cg_test_scan_kernel): 0 = the product's choice (below), 1 = the one-shot
+// k_scan_flat32, 2 = the persistent k_scan_flat32p at any size
+uint32_t g_scan_kernel = 0;
 // test hook (cg_test_scan_grid): workgroups of the persistent scan (0 = the resident count)
 uint64_t g_scan_grid = 0;
 
@@ -836,15 +837,20 @@ void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint
     spw = spw < 4 ? 4 : (spw > spw_max ? spw_max : (spw + 3) & ~3ull);
     const uint64_t waves = (nseg + spw - 1) / spw;
     const uint64_t wgs = (waves + SCAN2_T / 64 - 1) / (SCAN2_T / 64);
-    // product: the persistent form (k_scan_flat32p) when the caller passes its queue and the
-    // one-shot k_scan_flat32 was not asked for (cg_test_scan_kernel); the 16-byte row forms of
+    // product: the persistent form (k_scan_flat32p) from 4 GiB on when the caller passes its
+    // queue, the one-shot k_scan_flat32 below (cg_test_scan_kernel forces either).  Same-process
+    // A/B, 5 reps each (profiles/r04_v5_scan_ab*.json): 16 GiB of 1 GiB NARs (configs 4 / 5)
+    // 3.36-3.42 / 3.48-3.57 ms persistent against 3.44-3.57 / 3.54-3.70 one-shot; 1 GiB of
+    // 4 MiB NARs (config 2) 0.23-0.27 against 0.203 -- there the one-shot grid is only two
+    // dispatch rounds and the queue's per-unit cost shows.  The 16-byte row forms of
     // k_scan_flat are the diagnostics build's A/B
 #ifdef CG_DIAG
     const bool diag_variant = g_scan_variant == 5;
 #else
     const bool diag_variant = false;
 #endif
-    if (d_queue && !g_scan_oneshot && !diag_variant) {
+    const bool persistent = g_scan_kernel == 2 || (g_scan_kernel == 0 && nseg >= (1ull << 20));
+    if (d_queue && persistent && !diag_variant) {
         const uint64_t nunits = (nseg + CG_SCAN_SPU - 1) / CG_SCAN_SPU;
         const uint64_t resident = scan_resident_wgs();
         const uint64_t want = (nunits + SCAN2_T / 64 - 1) / (SCAN2_T / 64);  // >= one unit per wave
@@ -1098,8 +1104,8 @@ extern "C" uint64_t cg_test_scan_grid(uint64_t v) {
 }
 
 extern "C" uint32_t cg_test_scan_kernel(uint32_t v) {
-    const uint32_t old = cg::g_scan_oneshot;
-    cg::g_scan_oneshot = v ? 1u : 0u;
+    const uint32_t old = cg::g_scan_kernel;
+    cg::g_scan_kernel = v <= 2 ? v : 0u;
     return old;
 }
 

@@ -1,5 +1,5 @@
 """A/B of K1 scan kernels, same process, alternating: the scan stage's HIP-event time
-(cg_set_profiling(1)) for the persistent k_scan_flat32p (product) and the one-shot
+(cg_set_profiling(1)) for the persistent k_scan_flat32p and the one-shot
 k_scan_flat32 (cg_test_scan_kernel(1)), on config-shaped device batches.  With
 CHUNKER_AMD_LIB set, the persistent side is that build (e.g. another CG_SCAN_SPU).
 Prints one JSON object: median ms and TB/s per (config, kernel)."""
@@ -24,7 +24,7 @@ SHAPES = {"c2": (256, 4 << 20, (256 << 10, 1 << 20, 4 << 20)),
 ap = argparse.ArgumentParser()
 ap.add_argument("--configs", default="c2,c4,c5")
 ap.add_argument("--reps", type=int, default=5)
-ap.add_argument("--kernels", default="0,1", help="cg_test_scan_kernel values: 0 persistent, 1 one-shot")
+ap.add_argument("--kernels", default="2,1", help="cg_test_scan_kernel values: 2 persistent, 1 one-shot, 0 product choice")
 ap.add_argument("--hash", type=int, default=1)
 ap.add_argument("--grids", default="0", help="persistent-scan grid overrides to sweep (cg_test_scan_grid; 0 = resident)")
 args = ap.parse_args()
@@ -39,7 +39,7 @@ for cfg in args.configs.split(","):
     cap = ca.chunking.batch_capacity(offs, params[0])
     out = torch.empty(cap * 48, dtype=torch.uint8, device="cuda")
     sp = torch.cuda.current_stream().cuda_stream
-    kinds = [(int(k), g) for k in args.kernels.split(",") for g in (grids if int(k) == 0 else [0])]
+    kinds = [(int(k), g) for k in args.kernels.split(",") for g in (grids if int(k) == 2 else [0])]
     ms = {k: [] for k in kinds}
     firsts = {}
     for rep in range(args.reps + 1):
@@ -59,7 +59,7 @@ for cfg in args.configs.split(","):
     nbytes = int(offs[-1])
     for k in kinds:
         med = float(np.median(ms[k]))
-        res[f"{cfg}_{'persistent' if k[0] == 0 else 'oneshot'}" + (f"_grid{k[1]}" if k[1] else "")] = {
+        res[f"{cfg}_{['product', 'oneshot', 'persistent'][k[0]]}" + (f"_grid{k[1]}" if k[1] else "")] = {
             "ms": round(med, 4), "TBps": round(nbytes / (med * 1e-3) / 1e12, 3),
             "frac_8TBps": round(nbytes / (med * 1e-3) / 8e12, 4), "all_ms": [round(x, 4) for x in ms[k]]}
     del d, out

@@ -683,29 +683,31 @@ def test_scan_paths_agree(ca, O, path):
         ca.lib.cg_test_scan_path(old)
 
 
-@pytest.mark.parametrize("oneshot", [0, 1], ids=["persistent", "oneshot"])
-def test_scan_kernels_agree(ca, O, oneshot):
+@pytest.mark.parametrize("kernel", [2, 1, 0], ids=["persistent", "oneshot", "product"])
+def test_scan_kernels_agree(ca, O, kernel):
     """K1's persistent form (k_scan_flat32p: resident grid, per-XCD unit queue, halo row
-    per unit) and the one-shot k_scan_flat32 (cg_test_scan_kernel) both give the oracle's
-    descriptors on batches whose NAR and unit seams fall everywhere: units of 8 segments
-    (32 KiB) against NARs of odd lengths, a batch of many tiny NARs, a batch ending inside
-    a unit's first row, one with fewer units than waves, and back-to-back launches (the
-    queue must come back zeroed after each)."""
-    rng = np.random.default_rng(77 + oneshot)
+    per unit; the product from 4 GiB on) and the one-shot k_scan_flat32 (the product below),
+    each forced at any size by cg_test_scan_kernel, both give the oracle's descriptors on
+    batches whose NAR and unit seams fall everywhere: units of 16 segments (64 KiB) against
+    NARs of odd lengths, a batch of many tiny NARs, a batch ending inside a unit's first
+    row, one with fewer units than waves, and back-to-back launches (the queue must come
+    back zeroed after each)."""
+    rng = np.random.default_rng(77 + kernel)
     params = (16384, 65536, 262144)  # 16 prefilter bits: the flat kernels
+    unit = 65536
     batches = [
-        [rng.integers(0, 256, n, dtype=np.uint8) for n in (32768 * 3 + 5, 2048, 1, 32767, 65536 + 2049, 500_001)],
+        [rng.integers(0, 256, n, dtype=np.uint8) for n in (unit * 3 + 5, 2048, 1, unit - 1, unit + 2049, 500_001)],
         [rng.integers(0, 256, int(n), dtype=np.uint8) for n in rng.integers(1, 9000, 300)],
-        [rng.integers(0, 256, 32768 * 5 + 100, dtype=np.uint8)],
+        [rng.integers(0, 256, unit * 5 + 100, dtype=np.uint8)],
         [rng.integers(0, 256, 6_000_011, dtype=np.uint8), rng.integers(0, 256, 2_000_000, dtype=np.uint8)],
     ]
-    old = ca.lib.cg_test_scan_kernel(oneshot)
+    old = ca.lib.cg_test_scan_kernel(kernel)
     try:
         for rep in range(2):
             for b, nars in enumerate(batches):
                 got = ca.chunk_batch(nars, *params, hash=SHA)
                 for i, nar in enumerate(nars):
-                    assert_same(got[i], O.chunk_descriptors(nar, *params, algo=SHA), f"oneshot={oneshot} b{b} nar{i}")
+                    assert_same(got[i], O.chunk_descriptors(nar, *params, algo=SHA), f"kernel={kernel} b{b} nar{i}")
     finally:
         ca.lib.cg_test_scan_kernel(old)
 
