@@ -260,9 +260,14 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
     const bool has_pro = active && r0 >= F32_ROW;
     uint4 pro[2];
     {
-        const uint64_t a = has_pro ? r0 - F32_ROW + 32u * lane : 0;
-        pro[0] = *reinterpret_cast<const uint4 *>(data + a);
-        pro[1] = *reinterpret_cast<const uint4 *>(data + a + 16);
+        // only lanes 62 and 63 of the row before the run feed the hash (C_0 and C_1 take
+        // P_63 and P_62), so the other lanes read nothing
+        pro[0] = pro[1] = uint4{0, 0, 0, 0};
+        if (has_pro && lane >= 62) {
+            const uint64_t a = r0 - F32_ROW + 32u * lane;
+            pro[0] = *reinterpret_cast<const uint4 *>(data + a);
+            pro[1] = *reinterpret_cast<const uint4 *>(data + a + 16);
+        }
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -496,9 +501,13 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
                       (uint32_t)(r0 - base)};
     };
     const uint32_t lane_off = 32u * lane;
-    auto blk = [&](__amdgpu_buffer_rsrc_t rs, uint32_t so, uint4 (&v)[2]) {
-        const u32x4_t x0 = __builtin_amdgcn_raw_buffer_load_b128(rs, lane_off, so, 2);  // aux 2: nt
-        const u32x4_t x1 = __builtin_amdgcn_raw_buffer_load_b128(rs, lane_off + 16u, so, 2);
+    // A halo row feeds the hash only through lanes 62 and 63 (C_0 and C_1 take P_63 and
+    // P_62), so its other lanes read at an offset past every resource's size: zeros, no
+    // memory request (PMC: the halo rows were +3 % of the unit bytes in HBM reads).
+    const uint32_t halo_off = lane >= 62 ? lane_off : 0x80000000u;
+    auto blk = [&](__amdgpu_buffer_rsrc_t rs, uint32_t so, uint4 (&v)[2], uint32_t voff) {
+        const u32x4_t x0 = __builtin_amdgcn_raw_buffer_load_b128(rs, voff, so, 2);  // aux 2: nt
+        const u32x4_t x1 = __builtin_amdgcn_raw_buffer_load_b128(rs, voff + 16u, so, 2);
         v[0] = uint4{x0.x, x0.y, x0.z, x0.w};
         v[1] = uint4{x1.x, x1.y, x1.z, x1.w};
     };
@@ -556,8 +565,8 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
     // the ring: two stream entries in flight; a unit starts with its halo in slot 0 and its
     // row 0 in slot 1
     uint4 ring[2][2];
-    blk(ur.rs, 0, ring[0]);
-    blk(ur.rs, ur.hoff, ring[1]);
+    blk(ur.rs, 0, ring[0], halo_off);
+    blk(ur.rs, ur.hoff, ring[1], lane_off);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (uint32_t j = 0; j < 16; ++j) s_gear[ge * GEAR_COPIES + (((threadIdx.x & 1u) * 16u + j + ge) & 31u)] = gv;
@@ -616,7 +625,7 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
         {
             uint64_t q[8][4];
             partials(ring[0], q);
-            blk(ur.rs, ur.hoff + F32_ROW, ring[0]);  // row 1
+            blk(ur.rs, ur.hoff + F32_ROW, ring[0], lane_off);  // row 1
             if (r0 >= F32_ROW) {
                 const uint64_t P = block_p(q);
                 R1 = ((uint64_t)wave_ror1((uint32_t)(P >> 32)) << 32) | wave_ror1((uint32_t)P);
@@ -645,7 +654,7 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
                 const uint64_t rowb = (uint64_t)row * F32_ROW;
                 uint64_t q[8][4];
                 partials(ring[slot], q);
-                blk(nrs, nso, ring[slot]);  // re-issue the slot now
+                blk(nrs, nso, ring[slot], e == R ? halo_off : lane_off);  // re-issue the slot now
                 const uint64_t P = block_p(q);
                 const uint32_t a_lo = wave_ror1_add((uint32_t)P, zero), a_hi = wave_ror1_add((uint32_t)(P >> 32), zero);
                 const uint32_t p1_lo = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)R1, a_lo, 0xCA);
