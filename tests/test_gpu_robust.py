@@ -10,6 +10,7 @@ reporting, and the reference's error variants with their fields.
   CG_E_IO instead of returning digests computed from a stale ring slot.
 * BufferLimitExceeded{attempted, limit} (src/chunking.rs:49-50) carries its fields.
 """
+import os
 import threading
 
 import numpy as np
@@ -179,6 +180,21 @@ def test_concurrent_sha_callers_share_one_digest(ca, O, coalesce):
         for i, nar in enumerate(nars):
             ref = O.chunk_descriptors(nar, *P, algo=1, nthreads=8)
             assert _same(descs[int(first[i]):int(first[i + 1])], ref), (t, i)
+
+
+def test_sixteen_hardware_queues():
+    """The deployment setting DESIGN.md §7 / INTEGRATION.md recommend for concurrent
+    callers, GPU_MAX_HW_QUEUES=16, in a fresh process (HIP reads it once, at start): 8
+    concurrent device callers with and without digest coalescing, and a ChunkStream using
+    all 8 of its digest lanes (one HIP stream each, queues - 2), all oracle-exact
+    (tests/hw16_child.py)."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="16", CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR="1")
+    child = os.path.join(os.path.dirname(os.path.abspath(__file__)), "hw16_child.py")
+    r = subprocess.run([sys.executable, child], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "hw16 ok" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
 
 
 def test_coalesced_spin_guard_reaches_every_member(ca):
