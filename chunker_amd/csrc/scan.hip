@@ -208,6 +208,11 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan(const uint8_t *__restrict__ da
 // VALU per 32 bytes: 32 SDWA addresses, 24 + 7 (partials, P), 32 (hashes), 32 ands +
 // 16 min3 (prefilter), 7 (exchange) ~= 150, against ~186 for two 16-byte blocks.
 // ---------------------------------------------------------------------------
+// A/B (round 4): raise the wave's issue priority from a row's start to its slot re-issue,
+// so a wave that has its row's bytes reaches its next load sooner (more bytes in flight)
+#ifndef CG_SCAN_PRIO
+#define CG_SCAN_PRIO 0
+#endif
 #define F32_ROW 2048u
 #define F32_RPS (CG_SEG / F32_ROW)  // rows per segment
 static_assert(CG_SEG % F32_ROW == 0 && F32_RPS == 2, "two 2 KiB rows per segment");
@@ -331,8 +336,10 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
             const uint64_t row = r + u;
             const uint64_t next = row + RING < nrow ? row + RING : nrow - 1;
             uint64_t q[8][4];
+            if (CG_SCAN_PRIO) __builtin_amdgcn_s_setprio(2);
             partials(ring[u], q);
             blk(next, ring[u]);  // the slot's bytes are in the lookups: re-issue it now
+            if (CG_SCAN_PRIO) __builtin_amdgcn_s_setprio(0);
             const uint64_t P = block_p(q);
             const uint32_t a_lo = wave_ror1_add((uint32_t)P, zero), a_hi = wave_ror1_add((uint32_t)(P >> 32), zero);
             const uint32_t p1_lo = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)R1, a_lo, 0xCA);
@@ -653,8 +660,10 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
                 // counts vmcnt exactly)
                 const uint64_t rowb = (uint64_t)row * F32_ROW;
                 uint64_t q[8][4];
+                if (CG_SCAN_PRIO) __builtin_amdgcn_s_setprio(2);
                 partials(ring[slot], q);
                 blk(nrs, nso, ring[slot], e == R ? halo_off : lane_off);  // re-issue the slot now
+                if (CG_SCAN_PRIO) __builtin_amdgcn_s_setprio(0);
                 const uint64_t P = block_p(q);
                 const uint32_t a_lo = wave_ror1_add((uint32_t)P, zero), a_hi = wave_ror1_add((uint32_t)(P >> 32), zero);
                 const uint32_t p1_lo = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)R1, a_lo, 0xCA);
