@@ -70,7 +70,7 @@ def parse_args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-nars", type=int, default=0, help="0 = whole batch for c2/c3, 1 NAR for c4/c5")
     ap.add_argument("--no-concurrent", action="store_true", help="skip the K-batches-in-flight measurement")
-    ap.add_argument("--concurrent", default="8,32", help="K values of the in-flight measurement")
+    ap.add_argument("--concurrent", default="8,32", help="K values of the in-flight measurement ('' = skip it)")
     ap.add_argument("--concurrent-only", action="store_true", help="only the in-flight measurement (profiling)")
     ap.add_argument("--concurrent-reps", type=int, default=3, help="batches per thread in the in-flight measurement")
     ap.add_argument("--e2e", default="1,8,16", help="K values of the host-to-host in-flight measurement ('' = skip)")
@@ -341,6 +341,8 @@ def concurrent_rates(ca, torch, args, n_per, nar_bytes, params, algo):
     from chunker_amd.nar import synth_nars_device
 
     ks = sorted({int(k) for k in args.concurrent.split(",") if k})
+    if not ks:  # --concurrent '': only the host-to-host leg (e2e)
+        return {"unit": "GiB/s"}
     kmax = max(ks)
     sizes = np.full(n_per, nar_bytes, np.uint64)
     jobs = []
