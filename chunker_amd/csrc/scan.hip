@@ -213,6 +213,18 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan(const uint8_t *__restrict__ da
 #ifndef CG_SCAN_PRIO
 #define CG_SCAN_PRIO 0
 #endif
+// A/B (round 4): touch the row CG_SCAN_PF rows past the ring's (one dword per lane, at the
+// start of each 32-byte lane block: every 128-B line of the 2 KiB row) with a load into an
+// LDS scratch word, so its lines are on their way into L2 / MALL before the ring asks for
+// them -- more bytes in flight than the register ring holds.  Issued after the ring's own
+// loads (vmcnt is in order, so it never holds back a row the wave needs next); past the end
+// the offset is out of the resource's range (no request) so every row has the same path.
+#ifndef CG_SCAN_PF
+#define CG_SCAN_PF 0
+#endif
+__device__ __forceinline__ void scan_touch(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff, uint32_t *lds) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)lds, 4, voff, soff, 0, 0);
+}
 #define F32_ROW 2048u
 #define F32_RPS (CG_SEG / F32_ROW)  // rows per segment
 static_assert(CG_SEG % F32_ROW == 0 && F32_RPS == 2, "two 2 KiB rows per segment");
@@ -225,6 +237,7 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
                                                           uint32_t *__restrict__ seg_cand, uint64_t nseg, uint32_t spw) {
     __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * GEAR_COPIES];
     __shared__ uint32_t s_slots[SCAN2_T / 64][64];  // the open segment's candidate slots, per wave
+    __shared__ uint32_t s_touch[CG_SCAN_PF ? 64 : 1];   // CG_SCAN_PF's landing words (never read)
     const uint32_t lane = threadIdx.x & 63u;
     // the wave index through readfirstlane: the run's base, bounds and buffer resource
     // are then scalar (SGPRs), not per-lane copies
@@ -340,6 +353,10 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
             partials(ring[u], q);
             blk(next, ring[u]);  // the slot's bytes are in the lookups: re-issue it now
             if (CG_SCAN_PRIO) __builtin_amdgcn_s_setprio(0);
+            if (CG_SCAN_PF) {
+                const uint64_t pf = row + RING + CG_SCAN_PF;
+                scan_touch(run_rs, lane_off, pf < nrow ? (uint32_t)(pf * F32_ROW) : 0x80000000u, s_touch);
+            }
             const uint64_t P = block_p(q);
             const uint32_t a_lo = wave_ror1_add((uint32_t)P, zero), a_hi = wave_ror1_add((uint32_t)(P >> 32), zero);
             const uint32_t p1_lo = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)R1, a_lo, 0xCA);
@@ -482,6 +499,7 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
                                                            ScanQueue *queue, uint32_t nunits) {
     __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * GEAR_COPIES];
     __shared__ uint32_t s_slots[SCAN2_T / 64][64];  // the open segment's candidate slots, per wave
+    __shared__ uint32_t s_touch[CG_SCAN_PF ? 64 : 1];   // CG_SCAN_PF's landing words (never read)
     constexpr uint32_t R = SPU * F32_RPS;           // rows per unit
     constexpr uint32_t UNIT = SPU * CG_SEG;
     const uint32_t lane = threadIdx.x & 63u;
@@ -664,6 +682,10 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
                 partials(ring[slot], q);
                 blk(nrs, nso, ring[slot], e == R ? halo_off : lane_off);  // re-issue the slot now
                 if (CG_SCAN_PRIO) __builtin_amdgcn_s_setprio(0);
+                if (CG_SCAN_PF) {  // (within the unit only)
+                    const uint32_t pf = e + CG_SCAN_PF;
+                    scan_touch(ur.rs, lane_off, pf < R ? ur.hoff + pf * F32_ROW : 0x80000000u, s_touch);
+                }
                 const uint64_t P = block_p(q);
                 const uint32_t a_lo = wave_ror1_add((uint32_t)P, zero), a_hi = wave_ror1_add((uint32_t)(P >> 32), zero);
                 const uint32_t p1_lo = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)R1, a_lo, 0xCA);
