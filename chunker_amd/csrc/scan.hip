@@ -349,7 +349,7 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
             const uint64_t row = r + u;
             const uint64_t next = row + RING < nrow ? row + RING : nrow - 1;
             uint64_t q[8][4];
-            if (CG_SCAN_PRIO) __builtin_amdgcn_s_setprio(2);
+            if (CG_SCAN_PRIO) __builtin_amdgcn_s_setprio(CG_SCAN_PRIO);
             partials(ring[u], q);
             blk(next, ring[u]);  // the slot's bytes are in the lookups: re-issue it now
             if (CG_SCAN_PRIO) __builtin_amdgcn_s_setprio(0);
@@ -678,7 +678,7 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
                 // counts vmcnt exactly)
                 const uint64_t rowb = (uint64_t)row * F32_ROW;
                 uint64_t q[8][4];
-                if (CG_SCAN_PRIO) __builtin_amdgcn_s_setprio(2);
+                if (CG_SCAN_PRIO) __builtin_amdgcn_s_setprio(CG_SCAN_PRIO);
                 partials(ring[slot], q);
                 blk(nrs, nso, ring[slot], e == R ? halo_off : lane_off);  // re-issue the slot now
                 if (CG_SCAN_PRIO) __builtin_amdgcn_s_setprio(0);
