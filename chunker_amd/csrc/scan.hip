@@ -208,10 +208,13 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan(const uint8_t *__restrict__ da
 // VALU per 32 bytes: 32 SDWA addresses, 24 + 7 (partials, P), 32 (hashes), 32 ands +
 // 16 min3 (prefilter), 7 (exchange) ~= 150, against ~186 for two 16-byte blocks.
 // ---------------------------------------------------------------------------
-// A/B (round 4): raise the wave's issue priority from a row's start to its slot re-issue,
-// so a wave that has its row's bytes reaches its next load sooner (more bytes in flight)
+// Issue priority from a row's start to its slot re-issue (round 4): a wave that has its row's
+// bytes forms its lookup addresses and re-issues the slot ahead of the waves hashing, so
+// loads go out sooner and more bytes are in flight.  Same-box A/B, 3 alternating rounds
+// (profiles/r04_v12_*): config 2 0.2005-0.2026 -> 0.194-0.196 ms, the 16 GiB shapes
+// 3.24-3.45 / 3.37-3.53 -> 3.15-3.30 / 3.33-3.51 ms; levels 1, 2 and 3 alike.
 #ifndef CG_SCAN_PRIO
-#define CG_SCAN_PRIO 0
+#define CG_SCAN_PRIO 2
 #endif
 // A/B (round 4): touch the row CG_SCAN_PF rows past the ring's (one dword per lane, at the
 // start of each 32-byte lane block: every 128-B line of the 2 KiB row) with a load into an
