@@ -216,24 +216,6 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan(const uint8_t *__restrict__ da
 #ifndef CG_SCAN_PRIO
 #define CG_SCAN_PRIO 2
 #endif
-// A/B (round 4): touch the row CG_SCAN_PF rows past the ring's (one dword per lane, at the
-// start of each 32-byte lane block: every 128-B line of the 2 KiB row) with a load into an
-// LDS scratch word, so its lines are on their way into L2 / MALL before the ring asks for
-// them -- more bytes in flight than the register ring holds.  Issued after the ring's own
-// loads (vmcnt is in order, so it never holds back a row the wave needs next); past the end
-// the offset is out of the resource's range (no request) so every row has the same path.
-#ifndef CG_SCAN_PF
-#define CG_SCAN_PF 0
-#endif
-#ifndef CG_SCAN_LDSRING  // A/B: k_scan_flat32L (ring rows in LDS) in place of the one-shot kernel
-#define CG_SCAN_LDSRING 0
-#endif
-#ifndef CG_SCAN_LDSRING_SPW
-#define CG_SCAN_LDSRING_SPW 24
-#endif
-__device__ __forceinline__ void scan_touch(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t soff, uint32_t *lds) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)lds, 4, voff, soff, 0, 0);
-}
 #define F32_ROW 2048u
 #define F32_RPS (CG_SEG / F32_ROW)  // rows per segment
 static_assert(CG_SEG % F32_ROW == 0 && F32_RPS == 2, "two 2 KiB rows per segment");
@@ -246,7 +228,6 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
                                                           uint32_t *__restrict__ seg_cand, uint64_t nseg, uint32_t spw) {
     __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * GEAR_COPIES];
     __shared__ uint32_t s_slots[SCAN2_T / 64][64];  // the open segment's candidate slots, per wave
-    __shared__ uint32_t s_touch[CG_SCAN_PF ? 64 : 1];   // CG_SCAN_PF's landing words (never read)
     const uint32_t lane = threadIdx.x & 63u;
     // the wave index through readfirstlane: the run's base, bounds and buffer resource
     // are then scalar (SGPRs), not per-lane copies
@@ -362,10 +343,6 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
             partials(ring[u], q);
             blk(next, ring[u]);  // the slot's bytes are in the lookups: re-issue it now
             if (CG_SCAN_PRIO) __builtin_amdgcn_s_setprio(0);
-            if (CG_SCAN_PF) {
-                const uint64_t pf = row + RING + CG_SCAN_PF;
-                scan_touch(run_rs, lane_off, pf < nrow ? (uint32_t)(pf * F32_ROW) : 0x80000000u, s_touch);
-            }
             const uint64_t P = block_p(q);
             const uint32_t a_lo = wave_ror1_add((uint32_t)P, zero), a_hi = wave_ror1_add((uint32_t)(P >> 32), zero);
             const uint32_t p1_lo = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)R1, a_lo, 0xCA);
@@ -467,221 +444,6 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
     }
 }
 
-#if CG_SCAN_LDSRING
-// ---------------------------------------------------------------------------
-// A/B (round 4): k_scan_flat32 with its row ring in LDS.  One 1,024-thread workgroup per CU
-// (16 waves: the Gear table's 64 KiB once per CU instead of twice), three 2 KiB ring rows
-// per wave filled by buffer_load_dwordx4 ... lds (96 KiB), so ~2.5 rows per wave are in
-// flight instead of ~1.5 and no VGPRs hold them.  Candidates go straight to seg_cand (no LDS
-// slot list: all 160 KiB are taken).  spw must be a multiple of 12 (rows in threes).
-// ---------------------------------------------------------------------------
-#define SCANL_T 1024u
-#define SCANL_W (SCANL_T / 64)
-__global__ __launch_bounds__(SCANL_T, 1) void k_scan_flat32L(const uint8_t *data, uint64_t n,
-                                                          const uint64_t *__restrict__ gear_g, uint64_t mask_s,
-                                                          uint64_t mask_l, uint32_t cap,
-                                                          uint32_t *__restrict__ seg_count,
-                                                          uint32_t *__restrict__ seg_cand, uint64_t nseg, uint32_t spw) {
-    __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * GEAR_COPIES];
-    __shared__ __attribute__((aligned(16))) uint32_t s_ring0[SCANL_W][512];
-    __shared__ __attribute__((aligned(16))) uint32_t s_ring1[SCANL_W][512];
-    __shared__ __attribute__((aligned(16))) uint32_t s_ring2[SCANL_W][512];
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t seg0 = ((uint64_t)blockIdx.x * SCANL_W + wv) * spw;
-    const bool active = seg0 < nseg;
-    const uint64_t r0 = seg0 * CG_SEG;
-    const uint64_t nrow = (uint64_t)spw * F32_RPS;  // a multiple of 3
-    const uint64_t run_bytes = nrow * F32_ROW;
-    const uint64_t avail = active ? ((n - r0 + 15) & ~15ull) : 0;
-    const __amdgpu_buffer_rsrc_t run_rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t *>(data + (active ? r0 : 0)), (short)0, (int)(avail < run_bytes ? avail : run_bytes),
-        0x00027000);
-    const uint32_t lane_off = 32u * lane;
-    // row -> a ring array: lane L's 32 bytes land at [16 L] and [1024 + 16 L] (bytes) of the
-    // wave's 2 KiB (a DMA writes lane i's 16 bytes at base + 16 i)
-    auto dma = [&](uint32_t (*ring)[512], uint64_t row) {
-        const uint32_t so = (uint32_t)(row * F32_ROW);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(run_rs, (__attribute__((address_space(3))) void *)&ring[wv][0], 16,
-                                                 lane_off, so, 0, 2);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(run_rs, (__attribute__((address_space(3))) void *)&ring[wv][256], 16,
-                                                 lane_off + 16u, so, 0, 2);
-    };
-    auto fetch = [&](uint32_t (*ring)[512], uint4 (&v)[2]) {
-        v[0] = *reinterpret_cast<const uint4 *>(&ring[wv][4 * lane]);
-        v[1] = *reinterpret_cast<const uint4 *>(&ring[wv][256 + 4 * lane]);
-    };
-    static_assert(GEAR_COPIES == 32, "32 copies");
-    // Gear fill: 1,024 threads, 4 per entry, 8 copies each
-    const uint32_t ge = threadIdx.x >> 2;
-    const uint64_t gv = gear_g[ge] << SCAN_SHIFT;
-    if (active) {
-        dma(s_ring0, 0);
-        dma(s_ring1, 1);
-        dma(s_ring2, 2);
-    }
-    const bool has_pro = active && r0 >= F32_ROW;
-    uint4 pro[2];
-    pro[0] = pro[1] = uint4{0, 0, 0, 0};
-    if (has_pro && lane >= 62) {
-        const uint64_t a = r0 - F32_ROW + 32u * lane;
-        pro[0] = *reinterpret_cast<const uint4 *>(data + a);
-        pro[1] = *reinterpret_cast<const uint4 *>(data + a + 16);
-    }
-#pragma unroll
-    for (uint32_t j = 0; j < 8; ++j) s_gear[ge * GEAR_COPIES + (((threadIdx.x & 3u) * 8u + j + ge) & 31u)] = gv;
-    __syncthreads();
-    if (!active) return;
-    const char *gbase = reinterpret_cast<const char *>(s_gear);
-    const uint32_t lo8 = (threadIdx.x & 31u) * 8u;
-    uint32_t ad[4] = {lo8, lo8, lo8, lo8};
-    const uint64_t ms = mask_s << SCAN_SHIFT, ml = mask_l << SCAN_SHIFT;
-    const uint32_t mh = (uint32_t)((mask_s & mask_l) >> (32 - SCAN_SHIFT));
-    const uint32_t m0 = lane == 0 ? 0xffffffffu : 0u;
-    uint32_t zero = 0;
-    asm volatile("" : "+v"(zero));
-    const uint32_t ms_lo = (uint32_t)ms, ms_hi = (uint32_t)(ms >> 32), ml_lo = (uint32_t)ml, ml_hi = (uint32_t)(ml >> 32);
-    const uint64_t end_rel = n - r0;
-    auto partials = [&](const uint4 (&v)[2], uint64_t (&q)[8][4]) {
-        lookup4(gbase, ad, v[0].x, q[0]);
-        lookup4(gbase, ad, v[0].y, q[1]);
-        lookup4(gbase, ad, v[0].z, q[2]);
-        lookup4(gbase, ad, v[0].w, q[3]);
-        lookup4(gbase, ad, v[1].x, q[4]);
-        lookup4(gbase, ad, v[1].y, q[5]);
-        lookup4(gbase, ad, v[1].z, q[6]);
-        lookup4(gbase, ad, v[1].w, q[7]);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            q[k][1] = shl1_add(q[k][0], q[k][1]);
-            q[k][2] = shl1_add(q[k][1], q[k][2]);
-            q[k][3] = shl1_add(q[k][2], q[k][3]);
-        }
-    };
-    auto block_p = [&](const uint64_t (&q)[8][4]) {
-        uint64_t P = q[0][3];
-#pragma unroll
-        for (int k = 1; k < 8; ++k) P = shl_add<4>(P, q[k][3]);
-        return P;
-    };
-    uint64_t R1 = 0;
-    uint32_t R2 = 0;
-    if (has_pro) {
-        uint64_t q[8][4];
-        partials(pro, q);
-        const uint64_t P = block_p(q);
-        R1 = ((uint64_t)wave_ror1((uint32_t)(P >> 32)) << 32) | wave_ror1((uint32_t)P);
-        R2 = wave_ror1((uint32_t)R1);
-    }
-    uint32_t segc = 0;
-#pragma unroll 1
-    for (uint64_t r = 0; r < nrow; r += 3) {
-#pragma unroll
-        for (uint32_t u = 0; u < 3; ++u) {
-            uint32_t (*ring)[512] = u == 0 ? s_ring0 : (u == 1 ? s_ring1 : s_ring2);
-            const uint64_t row = r + u;
-            const uint64_t next = row + 3;  // past the run: out of the resource's range (no request)
-            uint64_t q[8][4];
-            if (CG_SCAN_PRIO) __builtin_amdgcn_s_setprio(CG_SCAN_PRIO);
-            uint4 v[2];
-            // this slot's DMA is the oldest of the three rows' in flight: wait until only the
-            // other two rows' (4 ops) remain.  Explicit: the compiler does not order LDS reads
-            // after the DMAs into the same array for every slot.
-            __builtin_amdgcn_s_waitcnt(0x0f74);  // vmcnt(4)
-            __builtin_amdgcn_sched_barrier(0);
-            fetch(ring, v);
-            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the slot is read before the DMA refills it
-            dma(ring, next < nrow ? next : 0x7ffffu);
-            partials(v, q);
-            if (CG_SCAN_PRIO) __builtin_amdgcn_s_setprio(0);
-            const uint64_t P = block_p(q);
-            const uint32_t a_lo = wave_ror1_add((uint32_t)P, zero), a_hi = wave_ror1_add((uint32_t)(P >> 32), zero);
-            const uint32_t p1_lo = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)R1, a_lo, 0xCA);
-            const uint32_t p1_hi = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)(R1 >> 32), a_hi, 0xCA);
-            R1 = ((uint64_t)a_hi << 32) | a_lo;
-            const uint32_t b_lo = wave_ror1_add(p1_lo, zero);
-            const uint32_t p2_lo = __builtin_amdgcn_bitop3_b32(m0, R2, b_lo, 0xCA);
-            R2 = b_lo;
-            const uint64_t C = ((uint64_t)(p1_hi + p2_lo) << 32) | p1_lo;
-            uint32_t acc = 0xffffffffu;
-            {
-                uint64_t E = C;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const uint64_t h0 = shl_add<1>(E, q[k][0]), h1 = shl_add<2>(E, q[k][1]);
-                    const uint64_t h2 = shl_add<3>(E, q[k][2]), h3 = shl_add<4>(E, q[k][3]);
-                    acc = min(min(acc, (uint32_t)(h0 >> 32) & mh), (uint32_t)(h1 >> 32) & mh);
-                    acc = min(min(acc, (uint32_t)(h2 >> 32) & mh), (uint32_t)(h3 >> 32) & mh);
-                    E = h3;
-                }
-            }
-            auto step = [&](uint64_t &x, uint32_t j) -> uint64_t {
-                const uint64_t qj = q[j >> 2][j & 3];
-                switch (j & 3) {
-                case 0: return shl_add<1>(x, qj);
-                case 1: return shl_add<2>(x, qj);
-                case 2: return shl_add<3>(x, qj);
-                default: return x = shl_add<4>(x, qj);
-                }
-            };
-            const uint64_t seg = seg0 + row / F32_RPS;
-            const bool tail = (row + 1) * F32_ROW > end_rel;  // uniform
-            if (__builtin_amdgcn_ballot_w64(acc == 0) != 0 || tail) {
-                bool exact = tail;
-                if (!tail) {
-                    uint32_t ex = 0xffffffffu;
-                    uint64_t x = C;
-#pragma unroll
-                    for (uint32_t j = 0; j < 32; ++j) {
-                        const uint64_t hx = step(x, j);
-                        const uint32_t lo = (uint32_t)hx, hi = (uint32_t)(hx >> 32);
-                        ex = min(ex, min((lo & ms_lo) | (hi & ms_hi), (lo & ml_lo) | (hi & ml_hi)));
-                    }
-                    exact = __builtin_amdgcn_ballot_w64(ex == 0) != 0;
-                }
-                if (exact && seg < nseg) {
-                    const uint64_t prel = row * F32_ROW + 32u * lane;
-                    const uint32_t nb = prel < end_rel ? (end_rel - prel < 32 ? (uint32_t)(end_rel - prel) : 32u) : 0u;
-                    uint32_t sm = 0, lm = 0;
-                    uint64_t x = C;
-#pragma unroll
-                    for (uint32_t j = 0; j < 32; ++j) {
-                        const uint64_t hx = step(x, j);
-                        const uint64_t zs = hx & ms, zl = hx & ml;
-                        const uint32_t ts = (uint32_t)zs | (uint32_t)(zs >> 32), tl = (uint32_t)zl | (uint32_t)(zl >> 32);
-                        sm |= (1u - min(ts, 1u)) << j;
-                        lm |= (1u - min(tl, 1u)) << j;
-                    }
-                    const uint32_t vm = nb >= 32 ? 0xffffffffu : (1u << nb) - 1u;
-                    sm &= vm;
-                    lm &= vm;
-                    const uint32_t any = sm | lm, c = (uint32_t)__builtin_popcount(any);
-                    uint32_t incl = c;
-#pragma unroll
-                    for (uint32_t d = 1; d < 64; d <<= 1) {
-                        const uint32_t y = (uint32_t)__shfl_up((int)incl, d, 64);
-                        if (lane >= d) incl += y;
-                    }
-                    const uint32_t excl = incl - c, total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-                    const uint32_t pos0 = (uint32_t)(row % F32_RPS) * F32_ROW + 32u * lane;
-                    uint32_t idx = segc + excl;
-                    for (uint32_t m = any; m; m &= m - 1) {
-                        const uint32_t j = (uint32_t)__builtin_ctz(m);
-                        const uint32_t f = (((sm >> j) & 1u) * CG_FLAG_S) | (((lm >> j) & 1u) * CG_FLAG_L);
-                        if (idx < cap) seg_cand[seg * cap + idx] = ((pos0 + j) << 2) | f;
-                        ++idx;
-                    }
-                    segc += total;
-                }
-            }
-            if (row % F32_RPS == F32_RPS - 1) {  // segment end: its count
-                if (seg < nseg && lane == 0) seg_count[seg] = segc;
-                segc = 0;
-            }
-        }
-    }
-}
-#endif
 
 // ---------------------------------------------------------------------------
 // K1, persistent form (round 4, the product for prefilterable masks): the row work of
@@ -724,7 +486,6 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
                                                            ScanQueue *queue, uint32_t nunits) {
     __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * GEAR_COPIES];
     __shared__ uint32_t s_slots[SCAN2_T / 64][64];  // the open segment's candidate slots, per wave
-    __shared__ uint32_t s_touch[CG_SCAN_PF ? 64 : 1];   // CG_SCAN_PF's landing words (never read)
     constexpr uint32_t R = SPU * F32_RPS;           // rows per unit
     constexpr uint32_t UNIT = SPU * CG_SEG;
     const uint32_t lane = threadIdx.x & 63u;
@@ -907,10 +668,6 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
                 partials(ring[slot], q);
                 blk(nrs, nso, ring[slot], e == R ? halo_off : lane_off);  // re-issue the slot now
                 if (CG_SCAN_PRIO) __builtin_amdgcn_s_setprio(0);
-                if (CG_SCAN_PF) {  // (within the unit only)
-                    const uint32_t pf = e + CG_SCAN_PF;
-                    scan_touch(ur.rs, lane_off, pf < R ? ur.hoff + pf * F32_ROW : 0x80000000u, s_touch);
-                }
                 const uint64_t P = block_p(q);
                 const uint32_t a_lo = wave_ror1_add((uint32_t)P, zero), a_hi = wave_ror1_add((uint32_t)(P >> 32), zero);
                 const uint32_t p1_lo = __builtin_amdgcn_bitop3_b32(m0, (uint32_t)R1, a_lo, 0xCA);
@@ -1125,17 +882,6 @@ void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint
                            mask_s, mask_l, cap, d_seg_count, d_seg_cand, nseg, d_queue, (uint32_t)nunits);
         return;
     }
-#if CG_SCAN_LDSRING
-    {
-        // runs of a multiple of 12 segments (rows in threes)
-        uint64_t spl = (nseg + 4095) / 4096;
-        spl = std::max<uint64_t>(12, std::min<uint64_t>(CG_SCAN_LDSRING_SPW, (spl + 11) / 12 * 12));
-        const uint64_t lwaves = (nseg + spl - 1) / spl;
-        hipLaunchKernelGGL(k_scan_flat32L, dim3((uint32_t)((lwaves + SCANL_W - 1) / SCANL_W)), dim3(SCANL_T), 0, st, d_data,
-                           n, d_gear, mask_s, mask_l, cap, d_seg_count, d_seg_cand, nseg, (uint32_t)spl);
-        return;
-    }
-#endif
     auto k = k_scan_flat32<2, true>;
 #ifdef CG_DIAG
     if (diag_variant) k = scan_flat_diag_kernel(k);
