@@ -185,14 +185,15 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
               uint8_t *d_chunk_ids = nullptr, uint8_t *h_manifest_ids = nullptr, bool digest = true,
               bool coalesce = false);
 
-// Digest coalescer (runtime.hip): a SHA-256 device-entry caller is counted from entry
-// (CoalActive) until it submits its chunk list, so a leader can wait for it to join.
+// Digest coalescer (runtime.hip): a SHA-256 device-entry caller is counted as "active" from
+// entry (CoalActive) until it submits its chunk list, and as "inside" until it returns, so a
+// leader can wait for every caller in the entry to join its group.
 struct CoalActive {
     int dev;
     bool left = false;
     explicit CoalActive(int dev);
     void leave();
-    ~CoalActive() { leave(); }
+    ~CoalActive();
 };
 struct CoalGroup;
 struct CoalEntry {

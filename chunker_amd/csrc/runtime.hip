@@ -278,14 +278,13 @@ uint32_t seg_slots(const CdcParams &p) {
 // 199 GiB/s with one set, 100 with two sets -- halved groups, same chains --
 // profiles/r04_v4_conc_*).  So a device has ONE set by default (CHUNKER_AMD_COAL_SETS, up
 // to 8, for A/B) and the leader (1) leases it, waiting for the previous group's end while
-// later callers keep joining the pending list, then (2) waits up to kCoalWindow while
-// callers are still launching their boundary stages or fewer are pending than those
-// already pending plus the group that just ended (its callers re-enter as soon as their
-// digests are back), capped at the largest recent group -- so two half-groups taking
-// turns (each carrying half the batches per chain: K = 8, 60 vs 110 GiB/s) merge into one
-// -- and (3) takes every pending caller (at most CG_COAL_MAX).  A window that expires short
-// of its target lowers the cap to the group it got, so a caller count that drops costs
-// one window.  Each member's stream then
+// later callers keep joining the pending list, then (2) waits up to kCoalWindow until every
+// caller inside the entry has submitted -- those still launching their boundary stages and
+// those of the group that just ended, which call again as soon as their digests are back --
+// so two half-groups taking turns (each carrying half the batches per chain: K = 8, 60 vs
+// 110 GiB/s) merge into one, and (3) takes every pending caller (at most CG_COAL_MAX).  A
+// caller that does not call again leaves the count when it returns, so a lone caller never
+// waits.  Each member's stream then
 // waits for its group's end, so its own tail (NAR index, spin-guard word) and its
 // completion event follow the merged digest.  A group of one runs the ordinary per-batch
 // launch on the member's own stream, so a lone caller's latency is unchanged.
@@ -309,9 +308,8 @@ struct Coalescer {
     std::condition_variable cv;
     std::deque<CoalEntry *> pending;
     int active = 0;         // SHA-256 device-entry callers that have not submitted yet
+    int inside = 0;         // SHA-256 device-entry callers that have not returned yet
     bool leading = false;   // a leader is collecting the next group
-    size_t last_group = 1;  // the previous group's size
-    size_t max_seen = 1;    // the largest recent group (lowered when a window expires short of it)
     std::vector<std::unique_ptr<CoalSet>> sets;
 };
 Coalescer g_coal[64];
@@ -337,6 +335,16 @@ CoalActive::CoalActive(int dev) : dev(dev) {
     Coalescer &C = coalescer(dev);
     std::lock_guard<std::mutex> g(C.mu);
     ++C.active;
+    ++C.inside;
+}
+CoalActive::~CoalActive() {
+    leave();
+    Coalescer &C = coalescer(dev);
+    {
+        std::lock_guard<std::mutex> g(C.mu);
+        --C.inside;
+    }
+    C.cv.notify_all();
 }
 void CoalActive::leave() {
     if (left) return;
@@ -445,25 +453,19 @@ int coalesced_sha256(CoalEntry *e) {
         if (!C.leading && !C.pending.empty()) {
             C.leading = true;  // this thread leads the next group
             CoalSet *S = lease_set(C, lk);  // (callers arriving meanwhile join the group)
-            // wait for the callers of the group that just ended too (they re-enter as soon as
-            // their digests are back), up to the largest recent group
-            const size_t target = std::min(C.pending.size() + C.last_group, std::max<size_t>(C.max_seen, 1));
+            // wait until every caller in the entry has submitted: those still launching their
+            // boundary stages, and those of the group that just ended, which return and call
+            // again as soon as their digests are back (a caller that does not call again
+            // leaves the count when it returns)
             const auto t0 = std::chrono::steady_clock::now();
-            bool expired = false;
-            while ((C.active > 0 || C.pending.size() < target) && C.pending.size() < CG_COAL_MAX) {
-                if (std::chrono::steady_clock::now() - t0 >= kCoalWindow) {
-                    expired = true;
-                    break;
-                }
+            while ((C.active > 0 || (int)C.pending.size() < C.inside) && C.pending.size() < CG_COAL_MAX &&
+                   std::chrono::steady_clock::now() - t0 < kCoalWindow)
                 C.cv.wait_for(lk, std::chrono::microseconds(100));
-            }
             std::vector<CoalEntry *> grp;
             while (!C.pending.empty() && grp.size() < CG_COAL_MAX) {
                 grp.push_back(C.pending.front());
                 C.pending.pop_front();
             }
-            C.last_group = grp.size();
-            C.max_seen = expired && grp.size() < target ? grp.size() : std::max(C.max_seen, grp.size());
             C.leading = false;  // the next group may form while this one launches
             if (grp.size() == 1) {  // a group of one runs on its member's stream
                 S->leased = false;
