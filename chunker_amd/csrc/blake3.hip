@@ -7,9 +7,6 @@
 // and a second kernel folds the <= 256 subtree values of chunks larger than
 // 64 KiB.  Level-wise pairing with the odd node carried up is exactly BLAKE3's
 // left-complete tree (left subtree = largest power of two < n leaves).
-#include <algorithm>
-#include <atomic>
-
 #include "common.h"
 
 namespace cg {
@@ -439,12 +436,6 @@ __global__ __launch_bounds__(64 * B3_WAVES) void k_b3_groups(const uint8_t *__re
 // lane past that chunk's leaves steps to the next chunk (chunks of fewer than 64 leaves
 // make it several steps).  A one-leaf chunk's lane writes the digest (ROOT); every other
 // leaf value goes to its group's slot in lcv, folded by k_b3_fold as before.
-// CG_B3_PERSIST (A/B, round 4): the grid is only the resident workgroups and every wave
-// walks the 64-leaf slot groups W = g, g + G, ... (g its index, G the grid's waves), so no
-// SIMD waits for the slowest wave of a finished workgroup before the next one is dispatched.
-#ifndef CG_B3_PERSIST
-#define CG_B3_PERSIST 0
-#endif
 __global__ __launch_bounds__(64 * B3_WAVES) void k_b3_leaves(const uint8_t *__restrict__ data,
                                                              const uint64_t *__restrict__ abs,
                                                              const DescRaw *__restrict__ desc,
@@ -457,31 +448,27 @@ __global__ __launch_bounds__(64 * B3_WAVES) void k_b3_leaves(const uint8_t *__re
                                                              uint32_t *__restrict__ lcv) {
     uint64_t total = *total_p;
     if (total > max_chunks) total = max_chunks;
+    const uint64_t W = (uint64_t)blockIdx.x * B3_WAVES + (threadIdx.x >> 6);
     const uint64_t T = leaf_base[total];
+    if (W * 64 >= T) return;  // uniform per wave
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t W0 = (uint64_t)blockIdx.x * B3_WAVES + (threadIdx.x >> 6);
-    const uint64_t WS = CG_B3_PERSIST ? (uint64_t)gridDim.x * B3_WAVES : ~0ull;
-    for (uint64_t W = W0; W * 64 < T; W += WS) {  // uniform per wave
-        const uint64_t s = W * 64 + lane;
-        if (s < T) {  // (all lanes but in the batch's last wave)
-            uint64_t c = lmap[W];
-            while (s >= leaf_base[c + 1]) ++c;
-            const uint64_t len = desc[c].length;
-            const uint64_t leaves = len ? (len + 1023) / 1024 : 1;
-            const uint64_t l = s - leaf_base[c];
-            const uint64_t off = l * 1024;
-            const uint32_t n = len ? (uint32_t)((len - off) < 1024 ? (len - off) : 1024) : 0u;
-            uint32_t cv[8];
-            b3_leaf<false>(data + abs[c] + off, n, l, leaves == 1, cv);
-            if (leaves == 1) {
-                store_digest(hash_base + c * stride, cv);
-            } else {
-                uint4 *o = reinterpret_cast<uint4 *>(lcv + ((group_base[c] + l / 64) * 64 + l % 64) * 8);
-                o[0] = make_uint4(cv[0], cv[1], cv[2], cv[3]);
-                o[1] = make_uint4(cv[4], cv[5], cv[6], cv[7]);
-            }
-        }
-        if (!CG_B3_PERSIST) break;
+    const uint64_t s = W * 64 + lane;
+    if (s >= T) return;  // the batch's last wave
+    uint64_t c = lmap[W];
+    while (s >= leaf_base[c + 1]) ++c;
+    const uint64_t len = desc[c].length;
+    const uint64_t leaves = len ? (len + 1023) / 1024 : 1;
+    const uint64_t l = s - leaf_base[c];
+    const uint64_t off = l * 1024;
+    const uint32_t n = len ? (uint32_t)((len - off) < 1024 ? (len - off) : 1024) : 0u;
+    uint32_t cv[8];
+    b3_leaf<false>(data + abs[c] + off, n, l, leaves == 1, cv);
+    if (leaves == 1) {
+        store_digest(hash_base + c * stride, cv);
+    } else {
+        uint4 *o = reinterpret_cast<uint4 *>(lcv + ((group_base[c] + l / 64) * 64 + l % 64) * 8);
+        o[0] = make_uint4(cv[0], cv[1], cv[2], cv[3]);
+        o[1] = make_uint4(cv[4], cv[5], cv[6], cv[7]);
     }
 }
 
@@ -837,24 +824,7 @@ void launch_blake3(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
     if (plan_ready && d_leaf_base && defer) {
         // packed leaves: at most total_bytes / 1 KiB + one partial leaf per chunk
         const uint64_t wbound = (total_bytes / 1024 + max_chunks + 63) / 64;
-        uint64_t lgrid = (wbound + B3_WAVES - 1) / B3_WAVES;
-        if (CG_B3_PERSIST) {
-            static std::atomic<uint32_t> resident{0};
-            uint32_t rw = resident.load(std::memory_order_relaxed);
-            if (!rw) {
-                int dev = 0, cus = 0, per_cu = 0;
-                if (hipGetDevice(&dev) != hipSuccess ||
-                    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-                    cus = 256;
-                if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_b3_leaves, 64 * B3_WAVES, 0) != hipSuccess ||
-                    per_cu <= 0)
-                    per_cu = 4;
-                rw = (uint32_t)(cus * per_cu);
-                resident.store(rw, std::memory_order_relaxed);
-            }
-            lgrid = std::min<uint64_t>(lgrid, rw);
-        }
-        hipLaunchKernelGGL(k_b3_leaves, dim3((uint32_t)std::max<uint64_t>(lgrid, 1)), dim3(64 * B3_WAVES), 0, st,
+        hipLaunchKernelGGL(k_b3_leaves, dim3((uint32_t)((wbound + B3_WAVES - 1) / B3_WAVES)), dim3(64 * B3_WAVES), 0, st,
                            d_data, d_abs, desc, d_total, max_chunks, d_group_base, d_leaf_base, d_lmap, d_hash_base,
                            hash_stride, d_lcv);
     } else {

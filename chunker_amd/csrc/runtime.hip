@@ -315,7 +315,10 @@ struct Coalescer {
 Coalescer g_coal[64];
 thread_local CoalActive *t_coal_active = nullptr;
 std::atomic<uint32_t> g_coalesce{1};  // test hook cg_test_coalesce
-constexpr auto kCoalWindow = std::chrono::microseconds(3000);
+#ifndef CG_COAL_WINDOW_US
+#define CG_COAL_WINDOW_US 3000
+#endif
+constexpr auto kCoalWindow = std::chrono::microseconds(CG_COAL_WINDOW_US);
 
 // coalescer sets per device (CHUNKER_AMD_COAL_SETS, 1..8; read once)
 static size_t coal_sets() {
