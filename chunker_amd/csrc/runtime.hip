@@ -280,11 +280,12 @@ uint32_t seg_slots(const CdcParams &p) {
 // to 8, for A/B) and the leader (1) leases it, waiting for the previous group's end while
 // later callers keep joining the pending list, then (2) waits up to kCoalWindow until every
 // caller inside the entry has submitted -- those still launching their boundary stages and
-// those of the group that just ended, which call again as soon as their digests are back --
+// those of the group that just ended -- and every caller that returned within the last
+// window has called again (a server thread calls again as soon as its digests are back),
 // so two half-groups taking turns (each carrying half the batches per chain: K = 8, 60 vs
 // 110 GiB/s) merge into one, and (3) takes every pending caller (at most CG_COAL_MAX).  A
-// caller that does not call again leaves the count when it returns, so a lone caller never
-// waits.  Each member's stream then
+// caller that does not call again stops being expected one window after it returned, so
+// a lone caller never waits.  Each member's stream then
 // waits for its group's end, so its own tail (NAR index, spin-guard word) and its
 // completion event follow the merged digest.  A group of one runs the ordinary per-batch
 // launch on the member's own stream, so a lone caller's latency is unchanged.
@@ -309,6 +310,9 @@ struct Coalescer {
     std::deque<CoalEntry *> pending;
     int active = 0;         // SHA-256 device-entry callers that have not submitted yet
     int inside = 0;         // SHA-256 device-entry callers that have not returned yet
+    // when callers returned, newest last (at most the last kCoalWindow's; a caller entering
+    // again takes one off): callers between two calls, expected back shortly
+    std::deque<std::chrono::steady_clock::time_point> returned;
     bool leading = false;   // a leader is collecting the next group
     std::vector<std::unique_ptr<CoalSet>> sets;
 };
@@ -339,6 +343,7 @@ CoalActive::CoalActive(int dev) : dev(dev) {
     std::lock_guard<std::mutex> g(C.mu);
     ++C.active;
     ++C.inside;
+    if (!C.returned.empty()) C.returned.pop_front();
 }
 CoalActive::~CoalActive() {
     leave();
@@ -346,6 +351,9 @@ CoalActive::~CoalActive() {
     {
         std::lock_guard<std::mutex> g(C.mu);
         --C.inside;
+        const auto now = std::chrono::steady_clock::now();
+        while (!C.returned.empty() && now - C.returned.front() > kCoalWindow) C.returned.pop_front();
+        C.returned.push_back(now);
     }
     C.cv.notify_all();
 }
@@ -461,9 +469,13 @@ int coalesced_sha256(CoalEntry *e) {
             // again as soon as their digests are back (a caller that does not call again
             // leaves the count when it returns)
             const auto t0 = std::chrono::steady_clock::now();
-            while ((C.active > 0 || (int)C.pending.size() < C.inside) && C.pending.size() < CG_COAL_MAX &&
-                   std::chrono::steady_clock::now() - t0 < kCoalWindow)
+            for (;;) {
+                const auto now = std::chrono::steady_clock::now();
+                while (!C.returned.empty() && now - C.returned.front() > kCoalWindow) C.returned.pop_front();
+                const bool more = C.active > 0 || C.pending.size() < (size_t)C.inside + C.returned.size();
+                if (!more || C.pending.size() >= CG_COAL_MAX || now - t0 >= kCoalWindow) break;
                 C.cv.wait_for(lk, std::chrono::microseconds(100));
+            }
             std::vector<CoalEntry *> grp;
             while (!C.pending.empty() && grp.size() < CG_COAL_MAX) {
                 grp.push_back(C.pending.front());
