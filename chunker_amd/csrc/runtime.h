@@ -210,5 +210,6 @@ struct CoalEntry {
     int rc = 0;
 };
 int coalesced_sha256(CoalEntry *e);
+bool coalesce_worth(int dev);
 
 }  // namespace cgrt

@@ -445,6 +445,22 @@ static int launch_group(CoalSet *S, std::vector<CoalEntry *> &grp, std::shared_p
     return CG_OK;
 }
 
+// Merge only when more callers are in flight than per-batch launches run side by side:
+// up to CG_COAL_MIN callers (8) each batch's own launch overlaps the others' on their own
+// hardware queues as well as one merged launch would (K = 8: 105-110 GiB/s per batch
+// against 89-110 merged, profiles/r04_v17_*), and past them the per-batch launches queue
+// behind one another (K = 32: 114-143 against 272-361 merged).
+#ifndef CG_COAL_MIN
+#define CG_COAL_MIN 8
+#endif
+bool coalesce_worth(int dev) {
+    Coalescer &C = coalescer(dev);
+    std::lock_guard<std::mutex> g(C.mu);
+    const auto now = std::chrono::steady_clock::now();
+    while (!C.returned.empty() && now - C.returned.front() > kCoalWindow) C.returned.pop_front();
+    return (size_t)C.inside + C.returned.size() > CG_COAL_MIN;  // (pending callers are inside)
+}
+
 int coalesced_sha256(CoalEntry *e) {
     Coalescer &C = coalescer(e->ws->device);
     HIP_TRY(hipEventCreateWithFlags(&e->ready, hipEventDisableTiming));
@@ -766,7 +782,7 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
         const uint64_t expected = std::min<uint64_t>(chunk_bound, total_len / (o.min + o.avg) + n_nars);
         if ((rc = sha_err_arm(ws, st))) return rc;
         sha_armed = true;
-        if (coalesce && chunk_bound) {
+        if (coalesce && chunk_bound && coalesce_worth(ws->device)) {
             CoalEntry e{ws, d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, expected, o.max, st};
             e.active = t_coal_active;
             if ((rc = coalesced_sha256(&e))) return rc;

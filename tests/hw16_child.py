@@ -3,7 +3,8 @@
 Runs with GPU_MAX_HW_QUEUES=16 set by the parent before anything in this process touches
 HIP (HIP reads the variable once, at initialisation; the library sizes its stream lanes
 from the value it saw at load, stream.hip g_hw_queues_at_load): 8 concurrent callers of
-the synchronous device entry, coalesced and per-batch, and a ChunkStream whose 8 digest
+the synchronous device entry (12 merged, 8 per-batch, 12 with coalescing off), and a
+ChunkStream whose 8 digest
 lanes (queues - 2) each hold a HIP stream of their own -- every result checked against
 the oracle.  Prints one line "hw16 ok ..." on success; any mismatch raises."""
 import io
@@ -83,7 +84,8 @@ def stream_with_all_lanes():
 if __name__ == "__main__":
     assert os.environ.get("GPU_MAX_HW_QUEUES") == "16", "the parent sets GPU_MAX_HW_QUEUES=16"
     torch.cuda.set_device(0)
-    concurrent_callers(8, 1, seed=21)
-    concurrent_callers(8, 0, seed=22)
+    concurrent_callers(12, 1, seed=21)  # more than CG_COAL_MIN (8) callers: merged digests
+    concurrent_callers(8, 1, seed=23)   # per-batch launches (coalescing on, too few callers)
+    concurrent_callers(12, 0, seed=22)
     n = stream_with_all_lanes()
-    print(f"hw16 ok: 8 callers coalesced + per-batch, ChunkStream {n} chunks")
+    print(f"hw16 ok: 12 / 8 callers coalesced + per-batch, ChunkStream {n} chunks")

@@ -184,8 +184,9 @@ def test_concurrent_sha_callers_share_one_digest(ca, O, coalesce):
 
 def test_sixteen_hardware_queues():
     """The deployment setting DESIGN.md §7 / INTEGRATION.md recommend for concurrent
-    callers, GPU_MAX_HW_QUEUES=16, in a fresh process (HIP reads it once, at start): 8
-    concurrent device callers with and without digest coalescing, and a ChunkStream using
+    callers, GPU_MAX_HW_QUEUES=16, in a fresh process (HIP reads it once, at start): 12
+    concurrent device callers with merged digests, 8 with per-batch launches, 12 with
+    coalescing off, and a ChunkStream using
     all 8 of its digest lanes (one HIP stream each, queues - 2), all oracle-exact
     (tests/hw16_child.py)."""
     import subprocess
@@ -201,7 +202,7 @@ def test_coalesced_spin_guard_reaches_every_member(ca):
     """A spin-guard expiry inside a merged digest fails every member's call with CG_E_IO
     (the merged launch's error word is copied into each member's), and the next round is
     exact again."""
-    jobs = _coalesced_jobs(ca, 6, seed=9)
+    jobs = _coalesced_jobs(ca, 12, seed=9)  # more than CG_COAL_MIN (8): the merged path
     old = ca.lib.cg_test_sha_spin_limit(0)
     try:
         _, errors = _run_threads(ca, jobs)
