@@ -281,11 +281,11 @@ uint32_t seg_slots(const CdcParams &p) {
 // later callers keep joining the pending list, then (2) waits up to kCoalWindow until every
 // caller inside the entry has submitted -- those still launching their boundary stages and
 // those of the group that just ended -- and every caller that returned within the last
-// window has called again (a server thread calls again as soon as its digests are back),
+// kCoalRecent has called again (a server thread calls again as soon as its digests are back),
 // so two half-groups taking turns (each carrying half the batches per chain: K = 8, 60 vs
 // 110 GiB/s) merge into one, and (3) takes every pending caller (at most CG_COAL_MAX).  A
-// caller that does not call again stops being expected one window after it returned, so
-// a lone caller never waits.  Each member's stream then
+// caller that does not call again stops being expected kCoalRecent after it returned, so
+// a lone caller never waits (its own return is taken off when it calls again).  Each member's stream then
 // waits for its group's end, so its own tail (NAR index, spin-guard word) and its
 // completion event follow the merged digest.  A group of one runs the ordinary per-batch
 // launch on the member's own stream, so a lone caller's latency is unchanged.
@@ -310,7 +310,7 @@ struct Coalescer {
     std::deque<CoalEntry *> pending;
     int active = 0;         // SHA-256 device-entry callers that have not submitted yet
     int inside = 0;         // SHA-256 device-entry callers that have not returned yet
-    // when callers returned, newest last (at most the last kCoalWindow's; a caller entering
+    // when callers returned, newest last (at most the last kCoalRecent's; a caller entering
     // again takes one off): callers between two calls, expected back shortly
     std::deque<std::chrono::steady_clock::time_point> returned;
     bool leading = false;   // a leader is collecting the next group
@@ -320,9 +320,13 @@ Coalescer g_coal[64];
 thread_local CoalActive *t_coal_active = nullptr;
 std::atomic<uint32_t> g_coalesce{1};  // test hook cg_test_coalesce
 #ifndef CG_COAL_WINDOW_US
-#define CG_COAL_WINDOW_US 3000
+#define CG_COAL_WINDOW_US 10000
 #endif
-constexpr auto kCoalWindow = std::chrono::microseconds(CG_COAL_WINDOW_US);
+#ifndef CG_COAL_RECENT_US
+#define CG_COAL_RECENT_US 50000
+#endif
+constexpr auto kCoalWindow = std::chrono::microseconds(CG_COAL_WINDOW_US);  // longest a leader waits
+constexpr auto kCoalRecent = std::chrono::microseconds(CG_COAL_RECENT_US);  // how long a returned caller is expected back
 
 // coalescer sets per device (CHUNKER_AMD_COAL_SETS, 1..8; read once)
 static size_t coal_sets() {
@@ -352,7 +356,7 @@ CoalActive::~CoalActive() {
         std::lock_guard<std::mutex> g(C.mu);
         --C.inside;
         const auto now = std::chrono::steady_clock::now();
-        while (!C.returned.empty() && now - C.returned.front() > kCoalWindow) C.returned.pop_front();
+        while (!C.returned.empty() && now - C.returned.front() > kCoalRecent) C.returned.pop_front();
         C.returned.push_back(now);
     }
     C.cv.notify_all();
@@ -457,7 +461,7 @@ bool coalesce_worth(int dev) {
     Coalescer &C = coalescer(dev);
     std::lock_guard<std::mutex> g(C.mu);
     const auto now = std::chrono::steady_clock::now();
-    while (!C.returned.empty() && now - C.returned.front() > kCoalWindow) C.returned.pop_front();
+    while (!C.returned.empty() && now - C.returned.front() > kCoalRecent) C.returned.pop_front();
     return (size_t)C.inside + C.returned.size() > CG_COAL_MIN;  // (pending callers are inside)
 }
 
@@ -487,7 +491,7 @@ int coalesced_sha256(CoalEntry *e) {
             const auto t0 = std::chrono::steady_clock::now();
             for (;;) {
                 const auto now = std::chrono::steady_clock::now();
-                while (!C.returned.empty() && now - C.returned.front() > kCoalWindow) C.returned.pop_front();
+                while (!C.returned.empty() && now - C.returned.front() > kCoalRecent) C.returned.pop_front();
                 const bool more = C.active > 0 || C.pending.size() < (size_t)C.inside + C.returned.size();
                 if (!more || C.pending.size() >= CG_COAL_MAX || now - t0 >= kCoalWindow) break;
                 C.cv.wait_for(lk, std::chrono::microseconds(100));
