@@ -320,7 +320,7 @@ Coalescer g_coal[64];
 thread_local CoalActive *t_coal_active = nullptr;
 std::atomic<uint32_t> g_coalesce{1};  // test hook cg_test_coalesce
 #ifndef CG_COAL_WINDOW_US
-#define CG_COAL_WINDOW_US 10000
+#define CG_COAL_WINDOW_US 3000
 #endif
 #ifndef CG_COAL_RECENT_US
 #define CG_COAL_RECENT_US 50000
@@ -452,8 +452,9 @@ static int launch_group(CoalSet *S, std::vector<CoalEntry *> &grp, std::shared_p
 // Merge only when more callers are in flight than per-batch launches run side by side:
 // up to CG_COAL_MIN callers (8) each batch's own launch overlaps the others' on their own
 // hardware queues as well as one merged launch would (K = 8: 105-110 GiB/s per batch
-// against 89-110 merged, profiles/r04_v17_*), and past them the per-batch launches queue
-// behind one another (K = 32: 114-143 against 272-361 merged).
+// against 87-111 always merged, profiles/r04_v18_*, r04_v19_*), and past them the per-batch
+// launches queue behind one another (K = 16 / 32: 110-118 / 114-175 per batch against
+// 155 / 286-305 merged).  Leader window 3 ms: 10 ms gave K = 32 220-279.
 #ifndef CG_COAL_MIN
 #define CG_COAL_MIN 8
 #endif
