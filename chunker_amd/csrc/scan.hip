@@ -472,6 +472,9 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
 #ifndef CG_SCAN_STATIC
 #define CG_SCAN_STATIC 0
 #endif
+#ifndef CG_SCAN_LOADS_ONLY  // diagnostics A/B: the persistent schedule's loads without the hashing
+#define CG_SCAN_LOADS_ONLY 0
+#endif
 #ifndef CG_SCAN_RESOLVE_LATE  // read the next unit's ticket at the unit's last row pair (else half-way)
 #define CG_SCAN_RESOLVE_LATE 1
 #endif
@@ -620,6 +623,9 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
         return P;
     };
 
+#if CG_SCAN_LOADS_ONLY
+    uint32_t sink = 0;
+#endif
     while (any) {
         const uint64_t r0 = (uint64_t)u * UNIT;
         const uint64_t seg0 = (uint64_t)u * SPU;
@@ -663,6 +669,18 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
                 // every position masked: the slot's loads stay on one code path, so the compiler
                 // counts vmcnt exactly)
                 const uint64_t rowb = (uint64_t)row * F32_ROW;
+#if CG_SCAN_LOADS_ONLY
+                // diagnostics form: the same schedule with the hashing removed (no candidates)
+                sink ^= ring[slot][0].x ^ ring[slot][0].y ^ ring[slot][0].z ^ ring[slot][0].w ^ ring[slot][1].x ^
+                        ring[slot][1].y ^ ring[slot][1].z ^ ring[slot][1].w;
+                blk(nrs, nso, ring[slot], e == R ? halo_off : lane_off);
+                (void)rowb;
+                if (uu == 1) {
+                    const uint64_t seg = seg0 + row / F32_RPS;
+                    if (seg < nseg && lane == 0) seg_count[seg] = 0;
+                }
+                continue;
+#endif
                 uint64_t q[8][4];
                 if (CG_SCAN_PRIO) __builtin_amdgcn_s_setprio(CG_SCAN_PRIO);
                 partials(ring[slot], q);
@@ -778,6 +796,9 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
         u = un;
         ur = urn;
     }
+#if CG_SCAN_LOADS_ONLY
+    if (sink == 0x9e3779b9u && nseg == 0) seg_count[0] = sink;  // keeps the loads alive
+#endif
     // leave: the last wave of the grid resets the queue for the next launch.  Relaxed:
     // a wave counts itself done only after its last dequeue has returned, the counter
     // guards no data, and the kernel's end publishes the reset.  (An acquire-release
