@@ -694,8 +694,16 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
 #endif
                 uint64_t q[8][4];
                 if (CG_SCAN_PRIO) __builtin_amdgcn_s_setprio(CG_SCAN_PRIO);
+#if CG_SCAN_EARLY
+                {
+                    const uint4 cur[2] = {ring[slot][0], ring[slot][1]};
+                    blk(nrs, nso, ring[slot], e == R ? halo_off : lane_off);
+                    partials(cur, q);
+                }
+#else
                 partials(ring[slot], q);
                 blk(nrs, nso, ring[slot], e == R ? halo_off : lane_off);  // re-issue the slot now
+#endif
                 if (CG_SCAN_PRIO) __builtin_amdgcn_s_setprio(0);
                 const uint64_t P = block_p(q);
                 const uint32_t a_lo = wave_ror1_add((uint32_t)P, zero), a_hi = wave_ror1_add((uint32_t)(P >> 32), zero);
