@@ -340,16 +340,8 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
             const uint64_t next = row + RING < nrow ? row + RING : nrow - 1;
             uint64_t q[8][4];
             if (CG_SCAN_PRIO) __builtin_amdgcn_s_setprio(CG_SCAN_PRIO);
-#if CG_SCAN_EARLY  // A/B: re-issue the slot before its bytes are used (8 more live VGPRs)
-            {
-                const uint4 cur[2] = {ring[u][0], ring[u][1]};
-                blk(next, ring[u]);
-                partials(cur, q);
-            }
-#else
             partials(ring[u], q);
             blk(next, ring[u]);  // the slot's bytes are in the lookups: re-issue it now
-#endif
             if (CG_SCAN_PRIO) __builtin_amdgcn_s_setprio(0);
             const uint64_t P = block_p(q);
             const uint32_t a_lo = wave_ror1_add((uint32_t)P, zero), a_hi = wave_ror1_add((uint32_t)(P >> 32), zero);
@@ -479,9 +471,6 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
 #endif
 #ifndef CG_SCAN_STATIC
 #define CG_SCAN_STATIC 0
-#endif
-#ifndef CG_SCAN_EARLY
-#define CG_SCAN_EARLY 0
 #endif
 #ifndef CG_SCAN_LOADS_ONLY  // diagnostics A/B: the persistent schedule's loads without the hashing
 #define CG_SCAN_LOADS_ONLY 0
@@ -694,16 +683,8 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
 #endif
                 uint64_t q[8][4];
                 if (CG_SCAN_PRIO) __builtin_amdgcn_s_setprio(CG_SCAN_PRIO);
-#if CG_SCAN_EARLY
-                {
-                    const uint4 cur[2] = {ring[slot][0], ring[slot][1]};
-                    blk(nrs, nso, ring[slot], e == R ? halo_off : lane_off);
-                    partials(cur, q);
-                }
-#else
                 partials(ring[slot], q);
                 blk(nrs, nso, ring[slot], e == R ? halo_off : lane_off);  // re-issue the slot now
-#endif
                 if (CG_SCAN_PRIO) __builtin_amdgcn_s_setprio(0);
                 const uint64_t P = block_p(q);
                 const uint32_t a_lo = wave_ror1_add((uint32_t)P, zero), a_hi = wave_ror1_add((uint32_t)(P >> 32), zero);
