@@ -332,12 +332,18 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
         R2 = wave_ror1((uint32_t)R1);
     }
     uint32_t segc = 0;
+    // row limits as 32-bit scalars (a run has at most 128 rows): the first row that reaches
+    // past the batch end (tail path) and the run's segments inside the batch, so the per-row
+    // tests are SALU compares rather than 64-bit VALU ones
+    const uint32_t nrow32 = (uint32_t)nrow;
+    const uint32_t tail_row = (uint32_t)std::min<uint64_t>(end_rel / F32_ROW, 0x7fffffffu);
+    const uint32_t seg_lim = (uint32_t)std::min<uint64_t>(nseg - seg0, 0x7fffffffu);
 #pragma unroll 1
-    for (uint64_t r = 0; r < nrow; r += RING) {
+    for (uint32_t r = 0; r < nrow32; r += RING) {
 #pragma unroll
         for (uint32_t u = 0; u < RING; ++u) {
-            const uint64_t row = r + u;
-            const uint64_t next = row + RING < nrow ? row + RING : nrow - 1;
+            const uint32_t row = r + u;
+            const uint32_t next = row + RING < nrow32 ? row + RING : nrow32 - 1;
             uint64_t q[8][4];
             if (CG_SCAN_PRIO) __builtin_amdgcn_s_setprio(CG_SCAN_PRIO);
             partials(ring[u], q);
@@ -374,7 +380,7 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
                 default: return x = shl_add<4>(x, qj);
                 }
             };
-            const bool tail = (row + 1) * F32_ROW > end_rel;  // uniform
+            const bool tail = row >= tail_row;  // (row + 1) x 2 KiB > end_rel; uniform
             if (__builtin_amdgcn_ballot_w64(acc == 0) != 0 || tail) {
                 bool exact = tail;
                 if (!tail) {
@@ -389,7 +395,7 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
                     exact = __builtin_amdgcn_ballot_w64(ex == 0) != 0;
                 }
                 if (exact) {
-                    const uint64_t prel = row * F32_ROW + 32u * lane;
+                    const uint64_t prel = (uint64_t)row * F32_ROW + 32u * lane;
                     const uint32_t nb = prel < end_rel ? (end_rel - prel < 32 ? (uint32_t)(end_rel - prel) : 32u) : 0u;
                     uint32_t sm = 0, lm = 0;
                     uint64_t x = C;
@@ -434,7 +440,7 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
             }
             if (u % F32_RPS == F32_RPS - 1) {  // segment end: flush its slots and count
                 const uint64_t seg = seg0 + row / F32_RPS;
-                if (seg < nseg) {
+                if (row / F32_RPS < seg_lim) {
                     if (lane < min(segc, cap)) seg_cand[seg * cap + lane] = slots[lane];
                     if (lane == 0) seg_count[seg] = segc;
                 }
@@ -630,6 +636,10 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
         const uint64_t r0 = (uint64_t)u * UNIT;
         const uint64_t seg0 = (uint64_t)u * SPU;
         const uint64_t end_rel = n - r0;  // > 0: units start inside the batch
+        // 32-bit scalar row limits (SALU compares in the row loop): the first row reaching past
+        // the batch end, and the unit's segments inside the batch
+        const uint32_t tail_row = (uint32_t)std::min<uint64_t>(end_rel / F32_ROW, 0x7fffffffu);
+        const uint32_t seg_lim = (uint32_t)std::min<uint64_t>(nseg - seg0, 0x7fffffffu);
         // the next unit: its head add issued now and read half a unit later, its halo and row
         // 0 issued as this unit's last two rows free their slots
         dq_issue();
@@ -717,7 +727,7 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
                     default: return x = shl_add<4>(x, qj);
                     }
                 };
-                const bool tail = rowb + F32_ROW > end_rel;  // uniform
+                const bool tail = row >= tail_row;  // rowb + 2 KiB > end_rel; uniform
                 if (__builtin_amdgcn_ballot_w64(acc == 0) != 0 || tail) {
                     bool exact = tail;
                     if (!tail) {
@@ -777,7 +787,7 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
                 }
                 if (uu == 1) {  // segment end: flush its slots and count
                     const uint64_t seg = seg0 + row / F32_RPS;
-                    if (seg < nseg) {
+                    if (row / F32_RPS < seg_lim) {
                         if (lane < min(segc, cap)) seg_cand[seg * cap + lane] = slots[lane];
                         if (lane == 0) seg_count[seg] = segc;
                     }
