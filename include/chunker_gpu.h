@@ -91,7 +91,10 @@ int cg_chunk_batch(const uint8_t *data, const uint64_t *nar_offsets, size_t n_na
 /* Device-resident batch: `d_data` and `d_out` are device pointers on the current
  * HIP device, `nar_offsets`/`nar_first` are host arrays, `stream` is a hipStream_t
  * (NULL = the null stream).  Returns after the descriptors are in HBM (the call
- * synchronises `stream` once to learn the count). */
+ * synchronises `stream` once to learn the count).  When more than 8 threads are in this
+ * entry at once (SHA-256), their digests may be computed by one shared launch on a
+ * library stream that `stream` waits for; the results and the return point are the
+ * same as for a lone call. */
 int cg_chunk_batch_device(const uint8_t *d_data, const uint64_t *nar_offsets, size_t n_nars,
                           uint64_t min_size, uint64_t avg_size, uint64_t max_size, int algo,
                           cg_desc *d_out, size_t out_cap, uint64_t *nar_first, void *stream);
