@@ -20,7 +20,9 @@ from chunker_amd.nar import synth_nars_device  # noqa: E402
 SHAPES = {"c2": (256, 4 << 20, (256 << 10, 1 << 20, 4 << 20)),
           "c4": (16, 1 << 30, (64 << 10, 256 << 10, 1 << 20)),
           "c5": (16, 1 << 30, (256 << 10, 1 << 20, 4 << 20)),
-          "c4q": (4, 1 << 30, (64 << 10, 256 << 10, 1 << 20))}
+          "c4q": (4, 1 << 30, (64 << 10, 256 << 10, 1 << 20)),
+          "c2x": (300, 4 << 20, (256 << 10, 1 << 20, 4 << 20)),   # 1.17 GiB: not a whole number of rounds
+          "c2h": (400, 4 << 20, (256 << 10, 1 << 20, 4 << 20))}   # 1.56 GiB
 ap = argparse.ArgumentParser()
 ap.add_argument("--configs", default="c2,c4,c5")
 ap.add_argument("--reps", type=int, default=5)
