@@ -888,30 +888,6 @@ void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint
     if (g_scan_spw_max) spw_max = g_scan_spw_max;
 #endif
     spw = spw < 4 ? 4 : (spw > spw_max ? spw_max : (spw + 3) & ~3ull);
-    // Whole dispatch rounds (round 4): a wave's time grows with its run length (plus a start-up
-    // of ~2 segments' worth: LDS table fill, first loads) and the launch lasts as many rounds
-    // as the resident waves need to cover the grid, so pick the run (a multiple of 4
-    // segments up to spw_max) that minimises rounds x (run + 2); on ties the one nearest 32.
-    // Config 2 (2^18 segments, 4,096 resident waves): runs of 32 (two whole rounds)
-    // 0.194-0.199 ms, 24 / 28 / 40 (fractional last rounds) 0.208-0.225, 16 (four rounds)
-    // 0.201-0.203 (profiles/r04_v13_*, r04_v30_*), as the model orders them (68 vs 78 / 90 /
-    // 84 / 72).
-#ifndef CG_SCAN_ROUND_PICK
-#define CG_SCAN_ROUND_PICK 1
-#endif
-    if (CG_SCAN_ROUND_PICK) {
-        const uint64_t rw = scan_resident_wgs() * (SCAN2_T / 64);
-        uint64_t best = spw, best_t = ~0ull;
-        auto far32 = [](uint64_t c) { return c > 32 ? c - 32 : 32 - c; };
-        for (uint64_t c = 4; c <= spw_max; c += 4) {
-            const uint64_t t = (((nseg + c - 1) / c + rw - 1) / rw) * (c + 2);
-            if (t < best_t || (t == best_t && far32(c) < far32(best))) {
-                best = c;
-                best_t = t;
-            }
-        }
-        spw = best;
-    }
     const uint64_t waves = (nseg + spw - 1) / spw;
     const uint64_t wgs = (waves + SCAN2_T / 64 - 1) / (SCAN2_T / 64);
     // product: the persistent form (k_scan_flat32p) from 4 GiB on when the caller passes its
