@@ -969,20 +969,11 @@ int batch_host(const uint8_t *data, const uint64_t *nar_offsets, size_t n_nars, 
     if ((rc = ws->out.ensure((total_cap + 1) * sizeof(cg_desc), "descriptors"))) return rc;
     if (bytes) HIP_TRY(hipMemcpyAsync(ws->in.p, data + lo, bytes, hipMemcpyHostToDevice, ws->stream));
     std::vector<uint64_t> first(n_nars + 1);
-#ifndef CG_COAL_HOST  // A/B: the host entry's SHA-256 digests join the coalescer too
-#define CG_COAL_HOST 0
-#endif
-    if (CG_COAL_HOST && algo == CG_SHA256 && g_coalesce.load(std::memory_order_relaxed)) {
-        CoalActive active(ws->device);
-        t_coal_active = &active;
-        rc = run_batch(ws, ws->in.as<uint8_t>(), off.data(), n_nars, o, algo, ws->out.as<cg_desc>(), total_cap,
-                       first.data(), ws->stream, nullptr, nullptr, true, true);
-        t_coal_active = nullptr;
-        active.leave();
-    } else {
-        rc = run_batch(ws, ws->in.as<uint8_t>(), off.data(), n_nars, o, algo, ws->out.as<cg_desc>(), total_cap,
-                       first.data(), ws->stream);
-    }
+    // (the host entry does not join the coalescer: its callers are bound by the host link,
+    // and merged digests make them take turns on it -- K = 16 41.7-43.3 GiB/s against
+    // 48.2-48.4 per batch, profiles/r04_v33_*)
+    rc = run_batch(ws, ws->in.as<uint8_t>(), off.data(), n_nars, o, algo, ws->out.as<cg_desc>(), total_cap,
+                   first.data(), ws->stream);
     if (rc) return rc;
     const uint64_t total = first[n_nars];
     if (nar_first) memcpy(nar_first, first.data(), (n_nars + 1) * 8);
