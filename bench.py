@@ -74,9 +74,20 @@ def parse_args():
     ap.add_argument("--concurrent-only", action="store_true", help="only the in-flight measurement (profiling)")
     ap.add_argument("--concurrent-reps", type=int, default=3, help="batches per thread in the in-flight measurement")
     ap.add_argument("--e2e", default="1,8,16", help="K values of the host-to-host in-flight measurement ('' = skip)")
+    ap.add_argument("--drop-in", default="1,8,32",
+                    help="K values of the drop-in leg: BASELINE config 1 (10 MiB, 256K/1M/4M) through the host "
+                         "entry cg_chunk_descriptors from K threads, SHA-256 and BLAKE3, against the CPU port on the "
+                         "same threads ('' = skip)")
+    ap.add_argument("--drop-in-only", action="store_true", help="only the drop-in leg (profiling)")
     ap.add_argument("--hw-queues", type=int, default=16, choices=range(0, 33), metavar="0..32",
                     help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's)")
     ap.add_argument("--no-clock", action="store_true", help="skip the digest clock measurement (scripts/sha_clock.py)")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="queue each batch after everything on the stream (cg_chunk_batch_device_async): its "
+                         "boundary stages wait for the previous batch's digest (A/B of the overlap)")
+    ap.add_argument("--bound-priority", action="store_true",
+                    help="boundary stages of overlapped batches on a highest-priority stream "
+                         "(CHUNKER_AMD_BOUND_PRIORITY=1; A/B)")
     ap.add_argument("--no-coalesce", action="store_true",
                     help="concurrent callers digest their batches alone (cg_test_coalesce(0)); A/B of the coalescer")
     ap.add_argument("--dist-force", action="store_true",
@@ -113,6 +124,8 @@ def main():
     # --hw-queues 0 keeps the environment's value.
     if args.hw_queues:
         os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
+    if args.bound_priority:
+        os.environ["CHUNKER_AMD_BOUND_PRIORITY"] = "1"
 
     import torch
     import torch.distributed as dist
@@ -143,6 +156,9 @@ def main():
     if args.concurrent_only:
         print(json.dumps({"concurrent": concurrent_rates(ca, torch, args, n_per, nar_bytes, params, algo)}))
         return
+    if args.drop_in_only:
+        print(json.dumps({"drop_in": drop_in_rates(ca, args)}))
+        return
     mine = shard_nars(n_per * world, world, rank)
     sizes = np.full(len(mine), nar_bytes, np.uint64)
     d_data, offs = synth_nars_device(sizes, zeros=args.zeros, first_index=mine.start)
@@ -162,13 +178,21 @@ def main():
     sptr = bstream.cuda_stream
     gathered_ev = [None, None]
     gathered = [None]
+    # Inputs-ready events (cg_chunk_batch_device_async_after): a batch's boundary stages
+    # (scan, walk, assembly) wait only for its input and output array to be free -- the NARs
+    # were written once, before the timed region; an output array is free once its previous
+    # gather has run -- so they run under the previous batch's digest on bstream, and only
+    # the digests follow one another there.  --no-overlap: after everything on bstream.
+    synth_ev = torch.cuda.Event()
+    synth_ev.record()
 
     def issue(k):
         ev = gathered_ev[k % 2]
         if ev is not None:
-            bstream.wait_event(ev)
+            bstream.wait_event(ev)  # (the digest writes the output array's hashes)
+        ready = 0 if args.no_overlap else (ev or synth_ev).cuda_event
         return ca.chunk_batch_device_async(d_data.data_ptr(), offs, d_outs[k % 2].data_ptr(), gcap, *params,
-                                           hash=algo, stream=sptr)
+                                           hash=algo, stream=sptr, inputs_ready=ready)
 
     def complete(k, batch):
         first = batch.wait()
@@ -227,6 +251,17 @@ def main():
         step(last)
         ca.lib.cg_last_stage_times(buf, 5)
         prof[k] = list(buf)
+    # The scan stage right after a 2 GiB write (the 256 MB MALL holds none of the batch): the
+    # cold-HBM rate, reported beside the warm pipeline's (the digest just read the batch)
+    cold = np.zeros(PROFILE_STEPS)
+    scratch = torch.empty(2 * GIB, dtype=torch.uint8, device="cuda")
+    for k in range(PROFILE_STEPS):
+        scratch.fill_(k)
+        torch.cuda.synchronize()
+        step(last)
+        ca.lib.cg_last_stage_times(buf, 5)
+        cold[k] = buf[0]
+    del scratch
     ca.lib.cg_set_profiling(0)
     if multi:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if nccl else "cpu")
@@ -269,7 +304,13 @@ def main():
         "scan_kernel": {"kernel": scan_kernel_name(ca, params[1], total_bytes),
                         "achieved": round(total_bytes / (scan_ms * 1e-3) / 1e9, 2),
                         "frac": round(total_bytes / (scan_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                        "traffic": None},
+                        "traffic": None,
+                        "cold_hbm": {"ms": round(float(np.median(cold)), 4),
+                                     "achieved": round(total_bytes / (float(np.median(cold)) * 1e-3) / 1e9, 2),
+                                     "frac": round(total_bytes / (float(np.median(cold)) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                     "note": "scan stage after a 2 GiB write evicted the batch from the MALL "
+                                             f"(median of {PROFILE_STEPS}); the warm figure above follows the "
+                                             "previous step's digest, which just read the batch"}},
     }
     if algo == 1:
         clk = sha_clock(args) if world == 1 and not args.no_clock else None
@@ -285,6 +326,7 @@ def main():
 
     cpu = None
     conc = None
+    drop = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, n_per, nar_bytes, params, algo)
     if world == 1 and not args.no_concurrent:
@@ -293,6 +335,8 @@ def main():
         conc = concurrent_rates(ca, torch, args, n_per, nar_bytes, params, algo)
         if args.e2e:
             conc["e2e"] = e2e_rates(ca, torch, args, n_per, nar_bytes, params, algo, descs)
+    if world == 1 and args.drop_in:
+        drop = drop_in_rates(ca, args)
 
     if rank == 0:
         gear = "placeholder" if ca.lib.cg_gear_is_placeholder() else (
@@ -305,6 +349,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "steps_queued": 2,
+            "boundary_overlap": not args.no_overlap,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
@@ -321,6 +366,7 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
             "concurrent": conc,
+            "drop_in": drop,
         }
         if gather_check is not None:
             line["gather_check"] = gather_check
@@ -454,6 +500,91 @@ def e2e_rates(ca, torch, args, n_per, nar_bytes, params, algo, want):
             assert n == len(want) and np.array_equal(out[:n].view(np.uint8), want.view(np.uint8)), \
                 f"e2e batch {k}: descriptors differ from the device-resident run"
         res[f"K{K}"] = round(K * reps * nbytes / dt / GIB, 3)
+    return res
+
+
+def drop_in_rates(ca, args):
+    """The reference's own call shape: one chunk_data call per NAR --
+    Node::put per HTTP PUT (crates/node/src/lib.rs:114-116, one thread per connection,
+    crates/proto/nix/src/lib.rs:153-162), the NIF per binary (src/nif.rs:188-196), and the
+    published bench, 10 MiB per call (benches/throughput.rs:39-43) -- through the drop-in
+    host entry cg_chunk_descriptors (pageable host bytes in, descriptors out), from K
+    threads at once, each calling `reps` times on its own 10 MiB xorshift64 buffer (BASELINE
+    config 1, 256K/1M/4M).  Per algorithm and K: aggregate GiB/s (K x reps x 10 MiB / wall
+    time), per-call latency p50 / p99 (ms), and the CPU port (the oracle's
+    chunk_descriptors: serial FastCDC + per-chunk digests on max(1, cores / K) threads, as
+    K callers share rayon's pool) on the same K threads over the same buffers.  Every GPU
+    call's descriptors are checked against the CPU port's."""
+    import ctypes
+
+    from chunker_amd.nar import synth_nars
+    from oracle import oracle as O
+
+    ks = sorted({int(k) for k in args.drop_in.split(",") if k})
+    nt, _, _ = host_cpus()
+    ten = 10 << 20
+    P = (256 << 10, 1 << 20, 4 << 20)
+    kmax = max(ks)
+    bufs = [synth_nars([ten], first_index=7 + k)[0] for k in range(kmax)]
+    cap = int(ca.lib.cg_capacity(ten, P[0]))
+    outs = [np.zeros(cap, ca.DESC_DTYPE) for _ in range(kmax)]
+    coal = bool(ca.lib.cg_test_coalesce(1))
+    ca.lib.cg_test_coalesce(int(coal))
+    res = {"unit": "GiB/s", "call": "cg_chunk_descriptors, 10 MiB xorshift64 per call, 256K/1M/4M (BASELINE config 1)",
+           "latency_unit": "ms per call", "cpu_threads_per_call": f"max(1, {nt} // K)",
+           "coalesced_host_calls": coal}
+    for algo, name in ((1, "sha256"), (0, "blake3")):
+        want = [O.chunk_descriptors(b, *P, algo=algo, nthreads=nt) for b in bufs]
+        leg = {}
+        for K in ks:
+            reps = max(3, min(12, 96 // K))
+
+            def run(fn):
+                bar = threading.Barrier(K + 1)
+                lat, errs = [[] for _ in range(K)], []
+
+                def work(k):
+                    bar.wait()
+                    try:
+                        for _ in range(reps):
+                            t = time.perf_counter()
+                            fn(k)
+                            lat[k].append(time.perf_counter() - t)
+                    except Exception as e:  # noqa: BLE001
+                        errs.append(repr(e))
+
+                th = [threading.Thread(target=work, args=(k,)) for k in range(K)]
+                for x in th:
+                    x.start()
+                bar.wait()
+                t0 = time.perf_counter()
+                for x in th:
+                    x.join()
+                dt = time.perf_counter() - t0
+                if errs:
+                    raise RuntimeError(errs[0])
+                ms = np.array([v for row in lat for v in row]) * 1e3
+                return {"GiBps": round(K * reps * ten / dt / GIB, 3), "p50": round(float(np.percentile(ms, 50)), 3),
+                        "p99": round(float(np.percentile(ms, 99)), 3)}
+
+            n_out = [ctypes.c_size_t(0) for _ in range(K)]
+
+            def gpu(k):
+                st = ca.lib.cg_chunk_descriptors(bufs[k].ctypes.data, ten, *P, algo, outs[k].ctypes.data, cap,
+                                                 ctypes.byref(n_out[k]))
+                if st:
+                    raise RuntimeError(f"status {st}: {ca._lib.last_error()}")
+
+            cpu_nt = max(1, nt // K)
+            run(gpu)  # untimed round: every workspace sized
+            g = run(gpu)
+            for k in range(K):
+                n = n_out[k].value
+                assert n == len(want[k]) and np.array_equal(outs[k][:n].view(np.uint8), want[k].view(np.uint8)), \
+                    f"drop-in {name} K={K} caller {k}: descriptors differ from the CPU port"
+            c = run(lambda k: O.chunk_descriptors(bufs[k], *P, algo=algo, nthreads=cpu_nt))
+            leg[f"K{K}"] = {"gpu": g, "cpu_port": c, "reps": reps}
+        res[name] = leg
     return res
 
 

@@ -47,13 +47,13 @@ EXPORTS = (
     "cg_selftest", "cg_tables_verified", "cg_set_profiling", "cg_last_stage_times", "cg_synth_nars", "cg_hash",
     "cg_cas_ids_device", "cg_cas_id", "cg_node_put_batch_device", "cg_node_put", "cg_stream_new", "cg_stream_push",
     "cg_stream_finish", "cg_stream_take", "cg_stream_pending", "cg_stream_bytes_consumed", "cg_stream_free",
-    "cg_last_sha_tiers", "cg_chunk_batch_device_async", "cg_batch_wait",
+    "cg_last_sha_tiers", "cg_chunk_batch_device_async", "cg_batch_wait", "cg_chunk_batch_device_async_after",
 )
 # test hooks the product library exports beyond the header (tier caps, spin-guard limit)
 TEST_HOOKS = ("cg_test_sha_quad_max", "cg_test_sha_split_max", "cg_test_sha_spin_limit", "cg_test_cas_pair_max",
               "cg_test_fail_alloc", "cg_test_sha_quad_fill", "cg_test_sha_pair_fill", "cg_test_scan_path", "cg_test_scan_kernel", "cg_test_coalesce", "cg_test_scan_grid",
               "cg_test_stream_group_cap", "cg_test_stream_max_lanes", "cg_test_stream_eager",
-              "cg_test_b3_fused_plan", "cg_test_b3_packed")
+              "cg_test_b3_fused_plan", "cg_test_b3_packed", "cg_coalesce_stats")
 
 
 def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
@@ -87,6 +87,8 @@ def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
     L.cg_chunk_batch_device.restype = i
     L.cg_chunk_batch_device_async.argtypes = [p, p, sz, u64, u64, u64, i, p, sz, p, ctypes.POINTER(p)]
     L.cg_chunk_batch_device_async.restype = i
+    L.cg_chunk_batch_device_async_after.argtypes = [p, p, sz, u64, u64, u64, i, p, sz, p, p, ctypes.POINTER(p)]
+    L.cg_chunk_batch_device_async_after.restype = i
     L.cg_batch_wait.argtypes = [p, p]
     L.cg_batch_wait.restype = i
     L.cg_push_new.argtypes = [u64, u64, u64, i, ctypes.POINTER(i)]
@@ -157,6 +159,8 @@ def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
         if hasattr(L, name):
             getattr(L, name).argtypes = [i]
             getattr(L, name).restype = i
+    L.cg_coalesce_stats.argtypes = [p]
+    L.cg_coalesce_stats.restype = None
     L.cg_test_fail_alloc.argtypes = [ctypes.c_uint32]
     L.cg_test_fail_alloc.restype = ctypes.c_uint32
     L.cg_set_profiling.argtypes = [i]

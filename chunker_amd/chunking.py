@@ -374,18 +374,24 @@ class BatchInFlight:
 
 def chunk_batch_device_async(d_data_ptr: int, nar_offsets: np.ndarray, d_out_ptr: int, out_cap: int,
                              min_size=None, avg_size=None, max_size=None,
-                             hash: HashAlgorithm = HashAlgorithm.Sha256, stream: int = 0) -> BatchInFlight:
+                             hash: HashAlgorithm = HashAlgorithm.Sha256, stream: int = 0,
+                             inputs_ready: int = 0) -> BatchInFlight:
     """chunk_batch_device without the wait (cg_chunk_batch_device_async): the pipeline is
     queued on `stream` and the call returns; BatchInFlight.wait() gives nar_first.  Keeping
     the next batch queued while waiting for the current one hides the host side of every
-    call behind the GPU's work."""
+    call behind the GPU's work.  `inputs_ready` (a hipEvent_t handle, e.g.
+    torch.cuda.Event().cuda_event, recorded after the last write to the input and the last
+    use of the output array) orders the boundary stages after that event only
+    (cg_chunk_batch_device_async_after), so they run under the digest of the batch queued
+    before on `stream`; 0 = after everything queued on `stream`."""
     o = ChunkingOptions.resolve(min_size, avg_size, max_size)
     offs = np.ascontiguousarray(nar_offsets, dtype=np.uint64)
     n = len(offs) - 1
     h = ctypes.c_void_p()
-    _check(lib.cg_chunk_batch_device_async(ctypes.c_void_p(d_data_ptr), offs.ctypes.data, n, o.min_size,
-                                           o.avg_size, o.max_size, int(hash), ctypes.c_void_p(d_out_ptr), out_cap,
-                                           ctypes.c_void_p(stream or None), ctypes.byref(h)))
+    _check(lib.cg_chunk_batch_device_async_after(ctypes.c_void_p(d_data_ptr), offs.ctypes.data, n, o.min_size,
+                                                 o.avg_size, o.max_size, int(hash), ctypes.c_void_p(d_out_ptr),
+                                                 out_cap, ctypes.c_void_p(stream or None),
+                                                 ctypes.c_void_p(inputs_ready or None), ctypes.byref(h)))
     return BatchInFlight(h.value, n)
 
 

@@ -113,6 +113,7 @@ struct Workspace {
         chunk_abs, b3_gcount, b3_gbase, b3_gcv, b3_gmap, in, out, span_off, span_len, order, cas_order, ids,
         man_abs, man_desc, sha_err, pc_first, pc_count, pc_exit, pc_starts, nar_ngroups, b3_lbase, b3_lmap,
         scanq;  // scanq: the persistent scan's work queue (cg::ScanQueue), zeroed once
+    bool scanq_zeroed = false;  // the zeroing memset of scanq has been queued
     PinBuf stage, err_stage, first_host;  // first_host: mapped, the assembly writes the NAR index there
     hipEvent_t ev[EV_N] = {};
     // CAS ids run on side_stream, concurrently with the digest: both stages are bound by
@@ -122,12 +123,20 @@ struct Workspace {
     // end of a launched batch: its wait syncs this event, not the stream (a batch queued
     // behind it on the same stream must not be waited for too)
     hipEvent_t ev_done = nullptr;
+    // Boundary stages of a batch queued with an inputs-ready event
+    // (cg_chunk_batch_device_async_after): they run on bound_stream, ordered after that
+    // event only, so they overlap the digest of the batch queued before on the caller's
+    // stream; ev_bdone (recorded on bound_stream after the assembly) holds the digest back,
+    // ev_dstart (on the caller's stream after that wait) opens the digest stage's timing.
+    hipStream_t bound_stream = nullptr;
+    hipEvent_t ev_bdone = nullptr, ev_dstart = nullptr;
     // Streams map onto the process's few hardware queues (GPU_MAX_HW_QUEUES, 4 by default)
     // and two streams on one queue serialise: the side stream exists only where used.
     int ensure_side_stream() {
         if (!side_stream) HIP_TRY(hipStreamCreateWithFlags(&side_stream, hipStreamNonBlocking));
         return CG_OK;
     }
+    int ensure_bound_stream();
     int init(int dev) {
         device = dev;
         HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -136,6 +145,8 @@ struct Workspace {
         HIP_TRY(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
         HIP_TRY(hipEventCreate(&ev_cas));
         HIP_TRY(hipEventCreateWithFlags(&ev_done, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&ev_bdone, hipEventDisableTiming));
+        HIP_TRY(hipEventCreate(&ev_dstart));
         return CG_OK;
     }
 };
@@ -173,10 +184,12 @@ struct BatchLaunch {
     bool sha_armed = false, node_put = false;
     int pmode = 0;  // profiling mode at launch (stage events recorded)
     hipEvent_t done = nullptr;  // recorded after the batch's last queued operation
+    hipEvent_t dstart = nullptr;  // opens the digest stage's timing (profiling)
 };
 int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, size_t n_nars, const Opts &o,
                  int algo, cg_desc *d_out, size_t out_cap, hipStream_t st, uint8_t *d_chunk_ids,
-                 uint8_t *h_manifest_ids, bool digest, BatchLaunch *bl, bool coalesce = false);
+                 uint8_t *h_manifest_ids, bool digest, BatchLaunch *bl, bool coalesce = false,
+                 hipEvent_t inputs_ready = nullptr);
 int finish_batch(Workspace *ws, hipStream_t st, const BatchLaunch &bl, uint64_t *h_nar_first);
 
 // The device pipeline for one batch (scan -> compact -> walk -> assemble -> digest).
@@ -190,9 +203,11 @@ int run_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, s
 // leader can wait for every caller in the entry to join its group.
 struct CoalActive {
     int dev;
-    bool left = false;
+    bool left = false;  // submitted, or digesting alone
+    bool solo = false;  // digesting alone (counted in Coalescer::solo until it returns)
     explicit CoalActive(int dev);
     void leave();
+    void go_solo();
     ~CoalActive();
 };
 struct CoalGroup;

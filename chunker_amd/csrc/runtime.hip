@@ -310,10 +310,13 @@ struct Coalescer {
     std::deque<CoalEntry *> pending;
     int active = 0;         // SHA-256 device-entry callers that have not submitted yet
     int inside = 0;         // SHA-256 device-entry callers that have not returned yet
+    int solo = 0;           // of those, callers digesting alone (per-batch launch): never submit
     // when callers returned, newest last (at most the last kCoalRecent's; a caller entering
     // again takes one off): callers between two calls, expected back shortly
     std::deque<std::chrono::steady_clock::time_point> returned;
     bool leading = false;   // a leader is collecting the next group
+    // counters (cg_coalesce_stats): groups led, their members, leader waits, windows run out
+    uint64_t groups = 0, members = 0, wait_us = 0, window_expired = 0;
     std::vector<std::unique_ptr<CoalSet>> sets;
 };
 Coalescer g_coal[64];
@@ -355,6 +358,7 @@ CoalActive::~CoalActive() {
     {
         std::lock_guard<std::mutex> g(C.mu);
         --C.inside;
+        if (solo) --C.solo;
         const auto now = std::chrono::steady_clock::now();
         while (!C.returned.empty() && now - C.returned.front() > kCoalRecent) C.returned.pop_front();
         C.returned.push_back(now);
@@ -368,6 +372,18 @@ void CoalActive::leave() {
     {
         std::lock_guard<std::mutex> g(C.mu);
         --C.active;
+    }
+    C.cv.notify_all();
+}
+// the caller digests its batch alone: a leader stops expecting it until it returns
+void CoalActive::go_solo() {
+    Coalescer &C = coalescer(dev);
+    {
+        std::lock_guard<std::mutex> g(C.mu);
+        if (!left) --C.active;
+        left = true;
+        if (!solo) ++C.solo;
+        solo = true;
     }
     C.cv.notify_all();
 }
@@ -493,15 +509,25 @@ int coalesced_sha256(CoalEntry *e) {
             for (;;) {
                 const auto now = std::chrono::steady_clock::now();
                 while (!C.returned.empty() && now - C.returned.front() > kCoalRecent) C.returned.pop_front();
-                const bool more = C.active > 0 || C.pending.size() < (size_t)C.inside + C.returned.size();
-                if (!more || C.pending.size() >= CG_COAL_MAX || now - t0 >= kCoalWindow) break;
+                // (callers digesting alone are inside but will not submit)
+                const bool more =
+                    C.active > 0 || C.pending.size() < (size_t)(C.inside - C.solo) + C.returned.size();
+                if (!more || C.pending.size() >= CG_COAL_MAX) break;
+                if (now - t0 >= kCoalWindow) {
+                    ++C.window_expired;
+                    break;
+                }
                 C.cv.wait_for(lk, std::chrono::microseconds(100));
             }
+            C.wait_us += (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(
+                             std::chrono::steady_clock::now() - t0).count();
             std::vector<CoalEntry *> grp;
             while (!C.pending.empty() && grp.size() < CG_COAL_MAX) {
                 grp.push_back(C.pending.front());
                 C.pending.pop_front();
             }
+            ++C.groups;
+            C.members += grp.size();
             C.leading = false;  // the next group may form while this one launches
             if (grp.size() == 1) {  // a group of one runs on its member's stream
                 S->leased = false;
@@ -573,18 +599,46 @@ int ensure_pass_buffers(Workspace *ws, uint64_t total_len, size_t n_nars, uint64
     return CG_OK;
 }
 
-// The persistent scan's queue: allocated and zeroed (on the batch's stream, ahead of its
-// first scan) once per workspace; every scan launch leaves it zeroed again.
-int ensure_scan_queue(Workspace *ws, hipStream_t st) {
-    if (ws->scanq.p) return CG_OK;
-    int rc;
-    if ((rc = ws->scanq.ensure(sizeof(cg::ScanQueue), "scan queue"))) return rc;
-    HIP_TRY(hipMemsetAsync(ws->scanq.p, 0, ws->scanq.cap, st));
+// The boundary stages' stream of a split batch.  CHUNKER_AMD_BOUND_PRIORITY=1 (read once)
+// creates it at the device's highest stream priority, so its workgroups are dispatched ahead
+// of the digest's as CU slots free up (A/B: a chip-filling digest leaves the scan few slots).
+int Workspace::ensure_bound_stream() {
+    if (bound_stream) return CG_OK;
+    static const bool high = [] {
+        const char *e = getenv("CHUNKER_AMD_BOUND_PRIORITY");
+        return e && e[0] == '1';
+    }();
+    if (high) {
+        int least = 0, greatest = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIP_TRY(hipStreamCreateWithPriority(&bound_stream, hipStreamNonBlocking, greatest));
+    } else {
+        HIP_TRY(hipStreamCreateWithFlags(&bound_stream, hipStreamNonBlocking));
+    }
     return CG_OK;
 }
 
-// One NAR of len bytes, boundaries only: every buffer launch_batch would grow for it
-// (its staging blocks and the descriptor array included), allocated now.
+// The persistent scan's queue: allocated and zeroed (on the batch's stream, ahead of its
+// first scan) once per workspace; every scan launch leaves it zeroed again.
+int ensure_scan_queue(Workspace *ws, hipStream_t st) {
+    if (ws->scanq_zeroed) return CG_OK;
+    int rc;
+    if ((rc = ws->scanq.ensure(sizeof(cg::ScanQueue), "scan queue"))) return rc;
+    // (marked zeroed only once the memset is queued: a failed memset leaves it to the next call)
+    HIP_TRY(hipMemsetAsync(ws->scanq.p, 0, ws->scanq.cap, st));
+    ws->scanq_zeroed = true;
+    return CG_OK;
+}
+
+// Walk pieces (walk.hip k_walk_pieces): NARs of at least two piece lengths are also
+// walked piece by piece in parallel; a piece is long enough (32 max-size chunks, at
+// least 8 MiB) for a walk started at its first byte to meet the NAR's own cut
+// sequence within a few chunks.
+uint64_t walk_piece_bytes(const Opts &o) { return std::max<uint64_t>(32 * o.max, 8ull << 20); }
+
+// One NAR of len bytes, boundaries only, and a digest of its chunks: every buffer
+// launch_batch grows for it (staging blocks, walk pieces, the descriptor array, the
+// BLAKE3 map, the persistent scan's queue) allocated now, with launch_batch's own sizes.
 int reserve_pass(Workspace *ws, uint64_t len, const Opts &o, int algo) {
     int rc;
     const std::shared_ptr<const Tables> tab = tables();
@@ -592,9 +646,29 @@ int reserve_pass(Workspace *ws, uint64_t len, const Opts &o, int algo) {
     const uint64_t cap = capacity_of(len, o.min);
     if ((rc = ensure_gear(ws, *tab))) return rc;
     if ((rc = ws->out.ensure((cap + 1) * sizeof(cg_desc), "descriptors"))) return rc;
-    if ((rc = ws->stage.ensure(8 * sizeof(uint64_t), /*mapped=*/true))) return rc;
+    const uint64_t pb = walk_piece_bytes(o), k = cg::walk_is_speculative(P) ? len / pb : 0;
+    const uint64_t np = k >= 2 ? k : 0;
+    if ((rc = ws->stage.ensure((4 * 2 + np + (np + 1) / 2) * sizeof(uint64_t), /*mapped=*/true))) return rc;
+    if (np) {
+        uint64_t lb = 0;
+        for (uint64_t j = 0; j < np; ++j) lb += capacity_of(j + 1 < np ? pb : len - j * pb, o.min) + 2;
+        if ((rc = ws->pc_first.ensure(2 * 8 + np * 12, "walk pieces"))) return rc;
+        if ((rc = ws->pc_count.ensure(np * 4, "walk pieces"))) return rc;
+        if ((rc = ws->pc_exit.ensure(np * 8, "walk pieces"))) return rc;
+        if ((rc = ws->pc_starts.ensure(std::max<uint64_t>(lb, cap + 2 * np) * 8, "walk pieces"))) return rc;
+    }
     if ((rc = ws->first_host.ensure(2 * 8, /*mapped=*/true))) return rc;
-    return ensure_pass_buffers(ws, len, 1, cap, cap, seg_slots(P), algo);
+    if ((rc = ensure_pass_buffers(ws, len, 1, cap, cap, seg_slots(P), algo))) return rc;
+    if (algo == CG_BLAKE3) {
+        if ((rc = ws->nar_ngroups.ensure(2 * 2 * 4, "nar_ngroups"))) return rc;
+        if ((rc = ws->b3_lbase.ensure((cap + 1) * 8, "b3_lbase"))) return rc;
+        if ((rc = ws->b3_lmap.ensure(cg::blake3_leaf_wave_bound(len, cap) * 4, "b3_lmap"))) return rc;
+    }
+    if (algo == CG_SHA256 && (rc = ws->order.ensure(cg::sha256_order_tmp_elems(cap) * 4, "order"))) return rc;
+    // the queue's zeroing must be complete before a scan on any stream reads it
+    if ((rc = ensure_scan_queue(ws, ws->stream))) return rc;
+    HIP_TRY(hipStreamSynchronize(ws->stream));
+    return CG_OK;
 }
 
 // The whole device pipeline for one batch.  d_out receives descriptors; the
@@ -609,7 +683,7 @@ int reserve_pass(Workspace *ws, uint64_t len, const Opts &o, int algo) {
 // finish_batch waits for `st` and checks the results.
 int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off, size_t n_nars, const Opts &o,
                  int algo, cg_desc *d_out, size_t out_cap, hipStream_t st, uint8_t *d_chunk_ids,
-                 uint8_t *h_manifest_ids, bool digest, BatchLaunch *bl, bool coalesce) {
+                 uint8_t *h_manifest_ids, bool digest, BatchLaunch *bl, bool coalesce, hipEvent_t inputs_ready) {
     if (algo != CG_BLAKE3 && algo != CG_SHA256) return fail(CG_E_INVALID_OPTIONS, "unknown hash algorithm");
     if (((uintptr_t)d_data & 15u) != 0) return fail(CG_E_IO, "device input must be 16-byte aligned");
     int rc;
@@ -624,11 +698,8 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
     const std::shared_ptr<const Tables> tab = tables();
     const CdcParams P = cdc_params(o, *tab);
 
-    // Walk pieces (walk.hip k_walk_pieces): NARs of at least two piece lengths are also
-    // walked piece by piece in parallel; a piece is long enough (32 max-size chunks, at
-    // least 8 MiB) for a walk started at its first byte to meet the NAR's own cut
-    // sequence within a few chunks.
-    const uint64_t pb = std::max<uint64_t>(32 * o.max, 8ull << 20);
+    // walk pieces (walk_piece_bytes)
+    const uint64_t pb = walk_piece_bytes(o);
     uint64_t np = 0, pcap = 0;
     if (cg::walk_is_speculative(P))
         for (size_t i = 0; i < n_nars; ++i) {
@@ -701,7 +772,17 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
     const uint64_t chunk_bound = std::min<uint64_t>(total_cap, out_cap);
     if ((rc = ensure_gear(ws, *tab))) return rc;
     if ((rc = ensure_pass_buffers(ws, total_len, n_nars, total_cap, chunk_bound, slots, algo))) return rc;
-    if ((rc = ensure_scan_queue(ws, st))) return rc;
+    // The boundary stages' stream: `st` itself, or -- with an inputs-ready event -- the
+    // workspace's bound_stream, ordered after that event only, so the stages run under the
+    // digest of the batch queued before on `st` (which reads another workspace); the digest
+    // waits for them below.
+    hipStream_t bs = st;
+    if (inputs_ready) {
+        if ((rc = ws->ensure_bound_stream())) return rc;
+        bs = ws->bound_stream;
+        HIP_TRY(hipStreamWaitEvent(bs, inputs_ready, 0));
+    }
+    if ((rc = ensure_scan_queue(ws, bs))) return rc;
     // nar_off (n+1) then cap_base (n+1): one block, one copy (s_cap follows s_off in staging)
     const uint64_t *d_nar_off = ws->nar_off.as<uint64_t>(), *d_cap_base = d_nar_off + (n_nars + 1);
 
@@ -712,15 +793,15 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
     const bool prof_all = pmode == 1;
     stage_in.add(s_off, ws->nar_off.p, 2 * (n_nars + 1) * 8);
     for (int k = 0; k < stage_in.n; ++k) stage_in.src[k] = dev_of(stage_in.src[k]);
-    if (prof_all) HIP_TRY(hipEventRecord(ws->ev[EV_START], st));  // scan stage = the scan kernel alone
+    if (prof_all) HIP_TRY(hipEventRecord(ws->ev[EV_START], bs));  // scan stage = the scan kernel alone
 
     cg::launch_scan(d_data, total_len, ws->gear.as<uint64_t>(), P.mask_s, P.mask_l, slots,
-                    ws->seg_count.as<uint32_t>(), ws->seg_cand.as<uint32_t>(), nseg, st, ws->scanq.as<cg::ScanQueue>());
-    if (prof_all) HIP_TRY(hipEventRecord(ws->ev[EV_SCAN], st));
+                    ws->seg_count.as<uint32_t>(), ws->seg_cand.as<uint32_t>(), nseg, bs, ws->scanq.as<cg::ScanQueue>());
+    if (prof_all) HIP_TRY(hipEventRecord(ws->ev[EV_SCAN], bs));
     // (the host tables ride along the compaction's first launch: the scan needs none of them)
     cg::launch_scan_compact(ws->seg_count.as<uint32_t>(), ws->seg_cand.as<uint32_t>(), ws->eoff.as<uint64_t>(), slots,
-                            nseg, ws->entries.as<uint64_t>(), ws->scan_tmp.as<uint64_t>(), st, stage_in);
-    if (prof_all) HIP_TRY(hipEventRecord(ws->ev[EV_COMPACT], st));
+                            nseg, ws->entries.as<uint64_t>(), ws->scan_tmp.as<uint64_t>(), bs, stage_in);
+    if (prof_all) HIP_TRY(hipEventRecord(ws->ev[EV_COMPACT], bs));
     // BLAKE3: the walk counts each NAR's 64-leaf groups and the assembly builds the group
     // map from them, so launch_blake3 needs no planning kernel of its own
     const bool b3_fuse = algo == CG_BLAKE3 && digest && g_b3_fused_plan.load(std::memory_order_relaxed);
@@ -741,8 +822,8 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
     }
     cg::launch_walk(d_data, ws->gear.as<uint64_t>(), ws->entries.as<uint64_t>(), ws->eoff.as<uint64_t>(), nseg,
                     d_nar_off, d_cap_base, n_nars, P, ws->wchunk.as<uint64_t>(),
-                    ws->nar_nchunks.as<uint32_t>(), pieces, st, b3_fuse ? ws->nar_ngroups.as<uint32_t>() : nullptr);
-    if (prof_all) HIP_TRY(hipEventRecord(ws->ev[EV_WALK], st));
+                    ws->nar_nchunks.as<uint32_t>(), pieces, bs, b3_fuse ? ws->nar_ngroups.as<uint32_t>() : nullptr);
+    if (prof_all) HIP_TRY(hipEventRecord(ws->ev[EV_WALK], bs));
     // the NAR index goes straight into mapped host memory from the assembly kernel: a D2H
     // copy after the digest cost ~40 us of idle GPU per call (blit + the runtime's gap
     // before the next call's first copy, profiles/r03_v16_c3_async_kernel_trace.csv)
@@ -751,9 +832,18 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
     const bool b3_planned =
         cg::launch_assemble(d_nar_off, d_cap_base, ws->wchunk.as<uint64_t>(), ws->nar_nchunks.as<uint32_t>(),
                             ws->nar_first.as<uint64_t>(), n_nars, d_out, out_cap, ws->chunk_abs.as<uint64_t>(),
-                            ws->scan_tmp.as<uint64_t>(), st, b3_fuse ? &b3plan : nullptr,
+                            ws->scan_tmp.as<uint64_t>(), bs, b3_fuse ? &b3plan : nullptr,
                             static_cast<uint64_t *>(ws->first_host.dev), &first_on_host);
-    if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_ASSEMBLE], st));
+    if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_ASSEMBLE], bs));
+    bl->dstart = ws->ev[EV_ASSEMBLE];
+    if (bs != st) {  // join: the digest (and everything after it) follows the boundary stages
+        HIP_TRY(hipEventRecord(ws->ev_bdone, bs));
+        HIP_TRY(hipStreamWaitEvent(st, ws->ev_bdone, 0));
+        if (prof) {
+            HIP_TRY(hipEventRecord(ws->ev_dstart, st));
+            bl->dstart = ws->ev_dstart;
+        }
+    }
     const uint64_t *d_total = ws->nar_first.as<uint64_t>() + n_nars;
     uint8_t *d_man = nullptr;
     if (d_chunk_ids) {
@@ -764,7 +854,7 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
         d_man = ws->ids.as<uint8_t>();
         if ((rc = ws->ensure_side_stream())) return rc;
         hipStream_t side = ws->side_stream;
-        HIP_TRY(hipEventRecord(ws->ev_fork, st));
+        HIP_TRY(hipEventRecord(ws->ev_fork, bs));
         HIP_TRY(hipStreamWaitEvent(side, ws->ev_fork, 0));
         const uint32_t *ord = cg::launch_len_order(d_out, d_total, chunk_bound, o.max, ws->cas_order.as<uint32_t>(), side);
         cg::launch_cas_ids(d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, ord, CG_KIND_CHUNK,
@@ -792,7 +882,7 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
             e.active = t_coal_active;
             if ((rc = coalesced_sha256(&e))) return rc;
         } else {
-            if (t_coal_active) t_coal_active->leave();  // nothing to merge: do not hold a leader back
+            if (t_coal_active) t_coal_active->go_solo();  // nothing to merge: do not hold a leader back
             cg::launch_sha256(d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, expected, o.max,
                               ws->order.as<uint32_t>(), hash_base, sizeof(cg_desc), ws->sha_err.as<uint32_t>(), st);
         }
@@ -842,7 +932,9 @@ int finish_batch(Workspace *ws, hipStream_t st, const BatchLaunch &bl, uint64_t 
         t_stage_ms.assign(EV_N - 1 + (bl.node_put ? 1 : 0), prof_all ? 0.0 : std::nan(""));
         for (int k = prof_all ? 1 : EV_DIGEST; k < EV_N; ++k) {
             float ms = 0;
-            HIP_TRY(hipEventElapsedTime(&ms, ws->ev[k - 1], ws->ev[k]));
+            // (the digest stage opens at bl.dstart: the assembly's event, or after a split
+            // batch's join on the caller's stream)
+            HIP_TRY(hipEventElapsedTime(&ms, k == EV_DIGEST ? bl.dstart : ws->ev[k - 1], ws->ev[k]));
             t_stage_ms[k - 1] = ms;
         }
         if (bl.node_put) {  // CAS stage: from descriptor assembly to the last id
@@ -969,9 +1061,11 @@ int batch_host(const uint8_t *data, const uint64_t *nar_offsets, size_t n_nars, 
     if ((rc = ws->out.ensure((total_cap + 1) * sizeof(cg_desc), "descriptors"))) return rc;
     if (bytes) HIP_TRY(hipMemcpyAsync(ws->in.p, data + lo, bytes, hipMemcpyHostToDevice, ws->stream));
     std::vector<uint64_t> first(n_nars + 1);
-    // (the host entry does not join the coalescer: its callers are bound by the host link,
-    // and merged digests make them take turns on it -- K = 16 41.7-43.3 GiB/s against
-    // 48.2-48.4 per batch, profiles/r04_v33_*)
+    // (the host entry does not join the coalescer: bound by the host link, 1 GiB batches
+    // take turns on it when their digests merge -- K = 16 41.7-43.3 GiB/s against 48.2-48.4
+    // per batch, profiles/r04_v33_*; and the reference's own call shape, 10 MiB per call,
+    // gains nothing in rate and loses in latency -- K = 32 2.08 vs 2.13 GiB/s, p50 127 vs
+    // 100 ms, profiles/r05_v2_dropin*)
     rc = run_batch(ws, ws->in.as<uint8_t>(), off.data(), n_nars, o, algo, ws->out.as<cg_desc>(), total_cap,
                    first.data(), ws->stream);
     if (rc) return rc;
@@ -1215,6 +1309,19 @@ extern "C" uint32_t cg_test_coalesce(uint32_t v) {  // 0 = every device-entry ca
     return cgrt::g_coalesce.exchange(v ? 1u : 0u);
 }
 
+// Coalescer counters of the current device since the process started: out = {groups led,
+// batches in them, total leader wait (us), groups launched because the window ran out}.
+extern "C" void cg_coalesce_stats(uint64_t out[4]) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+    cgrt::Coalescer &C = cgrt::coalescer(dev);
+    std::lock_guard<std::mutex> g(C.mu);
+    out[0] = C.groups;
+    out[1] = C.members;
+    out[2] = C.wait_us;
+    out[3] = C.window_expired;
+}
+
 extern "C" {
 
 uint32_t cg_abi_version(void) { return CG_ABI_VERSION; }
@@ -1287,6 +1394,14 @@ int cg_chunk_batch_device(const uint8_t *d_data, const uint64_t *nar_offsets, si
 int cg_chunk_batch_device_async(const uint8_t *d_data, const uint64_t *nar_offsets, size_t n_nars, uint64_t min_size,
                                 uint64_t avg_size, uint64_t max_size, int algo, cg_desc *d_out, size_t out_cap,
                                 void *stream, cg_batch **batch) {
+    return cg_chunk_batch_device_async_after(d_data, nar_offsets, n_nars, min_size, avg_size, max_size, algo, d_out,
+                                             out_cap, stream, nullptr, batch);
+}
+
+int cg_chunk_batch_device_async_after(const uint8_t *d_data, const uint64_t *nar_offsets, size_t n_nars,
+                                      uint64_t min_size, uint64_t avg_size, uint64_t max_size, int algo,
+                                      cg_desc *d_out, size_t out_cap, void *stream, void *inputs_ready,
+                                      cg_batch **batch) {
     clear_error();
     if (!batch) return fail(CG_E_IO, "null batch handle pointer");
     *batch = nullptr;
@@ -1300,9 +1415,11 @@ int cg_chunk_batch_device_async(const uint8_t *d_data, const uint64_t *nar_offse
     if ((rc = acquire(&ws))) return rc;
     hipStream_t st = static_cast<hipStream_t>(stream);
     BatchLaunch bl;
-    rc = launch_batch(ws, d_data, nar_offsets, n_nars, o, algo, d_out, out_cap, st, nullptr, nullptr, true, &bl);
+    rc = launch_batch(ws, d_data, nar_offsets, n_nars, o, algo, d_out, out_cap, st, nullptr, nullptr, true, &bl,
+                      false, static_cast<hipEvent_t>(inputs_ready));
     if (rc) {
         (void)hipStreamSynchronize(st);
+        if (ws->bound_stream) (void)hipStreamSynchronize(ws->bound_stream);
         release(ws);
         return rc;
     }

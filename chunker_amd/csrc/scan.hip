@@ -15,6 +15,10 @@
 
 #include "scan_common.h"
 
+#ifndef CG_SCAN_FLUSH_OLD
+#define CG_SCAN_FLUSH_OLD 0
+#endif
+
 namespace cg {
 
 template <bool PRE, int RING = 4>
@@ -441,7 +445,11 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
             if (u % F32_RPS == F32_RPS - 1) {  // segment end: flush its slots and count
                 const uint64_t seg = seg0 + row / F32_RPS;
                 if (row / F32_RPS < seg_lim) {
+#if CG_SCAN_FLUSH_OLD  // (A/B: the round-4 flush, whose addresses the compiler hoisted and spilled)
                     if (lane < min(segc, cap)) seg_cand[seg * cap + lane] = slots[lane];
+#else
+                    flush_slots(seg_cand + seg * cap, slots, min(segc, cap));
+#endif
                     if (lane == 0) seg_count[seg] = segc;
                 }
                 segc = 0;
@@ -788,7 +796,11 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
                 if (uu == 1) {  // segment end: flush its slots and count
                     const uint64_t seg = seg0 + row / F32_RPS;
                     if (row / F32_RPS < seg_lim) {
+#if CG_SCAN_FLUSH_OLD  // (A/B: the round-4 flush, whose addresses the compiler hoisted and spilled)
                         if (lane < min(segc, cap)) seg_cand[seg * cap + lane] = slots[lane];
+#else
+                        flush_slots(seg_cand + seg * cap, slots, min(segc, cap));
+#endif
                         if (lane == 0) seg_count[seg] = segc;
                     }
                     segc = 0;

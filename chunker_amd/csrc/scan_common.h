@@ -96,4 +96,17 @@ __device__ __forceinline__ uint64_t shl_add(uint64_t a, uint64_t b) {
     return r;
 }
 
+// Segment flush of the flat scans: the first n of the wave's LDS slots (`slots`, wave-uniform
+// base) to `dst` (the segment's row of seg_cand, wave-uniform).  The lane index is made here
+// by an opaque v_mbcnt pair, so the slot and store addresses cannot be hoisted out of the
+// row loop: left to itself the compiler formed both once per kernel, kept them live across
+// the row loop and, at 128 VGPRs, spilled them to scratch -- and each reload's
+// `s_waitcnt vmcnt` drained the row ring on every segment holding a candidate.  The store
+// takes the uniform base in SGPRs plus a 32-bit lane offset (global_store ... saddr).
+__device__ __forceinline__ void flush_slots(uint32_t *__restrict__ dst, const uint32_t *slots, uint32_t n) {
+    uint32_t l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    if (l < n) dst[l] = slots[l];
+}
+
 }  // namespace cg

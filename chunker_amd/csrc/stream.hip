@@ -130,7 +130,7 @@ struct cg_stream {
     Workspace *ws = nullptr;  // boundary pipeline, held for the handle's lifetime
     Arena arena;
     std::vector<Arena> retired;  // the first, two-slot arena once grown (freed with the handle)
-    uint64_t slot_bytes = 0, max_slots = 0, group_bytes = 0;
+    uint64_t slot_bytes = 0, max_slots = 0, group_bytes = 0, group_hard = 0;
     size_t max_lanes = 0;
     int poisoned = CG_OK;  // first failure of push / finish / take, returned by every later call
     std::string poison_msg;
@@ -357,8 +357,21 @@ int stream_drain(cg_stream *h, uint64_t len, bool eof) {
     }
     h->position += consumed;
     h->tail = rest;
-    if (h->open.bytes >= h->group_bytes) return launch_open(h);
-    if (g_stream_eager && !h->open.desc.empty()) {  // launch now if a lane is idle
+    if (h->open.bytes >= h->group_bytes) {
+        // accumulate mode (cg_test_stream_eager(2)): while every lane is busy the group keeps
+        // growing -- a SHA-256 group costs one chain (its longest chunk) whatever its size, up
+        // to what one launch can spread over the chip -- instead of the push waiting for a lane
+        if (g_stream_eager != 2 || h->open.bytes >= h->group_hard) return launch_open(h);
+        bool idle = h->lanes.size() < h->max_lanes;
+        for (const Lane &l : h->lanes) idle = idle || !l.busy;
+        if (!idle && !h->inflight.empty() && hipEventQuery(h->lanes[h->inflight.front().lane].done) == hipSuccess) {
+            if ((rc = complete_oldest(h))) return rc;
+            idle = true;
+        }
+        if (idle) return launch_open(h);
+        return CG_OK;
+    }
+    if (g_stream_eager == 1 && !h->open.desc.empty()) {  // launch now if a lane is idle
         bool idle = h->lanes.size() < h->max_lanes;
         for (const Lane &l : h->lanes) idle = idle || !l.busy;
         if (!idle && !h->inflight.empty() && hipEventQuery(h->lanes[h->inflight.front().lane].done) == hipSuccess) {
@@ -427,6 +440,8 @@ cg_stream *cg_stream_new(uint64_t min_size, uint64_t avg_size, uint64_t max_size
                                                   : (2048 / (uint64_t)h->max_lanes) * (o.min + o.avg);
     h->group_bytes = std::max<uint64_t>(
         std::min<uint64_t>(h->max_slots * h->slot_bytes / (uint64_t)(h->max_lanes + 1), group_cap), slice);
+    // the largest group one launch spreads over the chip (quad workgroups for 2048 chunks)
+    h->group_hard = std::max<uint64_t>(2048 * (o.min + o.avg), h->group_bytes);
     if (!(rc = acquire(&h->ws))) {
         const hipError_t e = hipEventCreateWithFlags(&h->ev_bytes, hipEventDisableTiming);
         if (e != hipSuccess) rc = hip_fail(e, "hipEventCreate");

@@ -97,6 +97,14 @@ def gather_batch_async(desc: torch.Tensor, nar_first, max_cap: int, max_nars: in
     elsewhere.  The packing copies `desc` on the current stream, so once this returns
     (and the stream has reached it) the caller may overwrite `desc`."""
     first = np.asarray(nar_first, dtype=np.uint64)
+    # the shapes agreed by gather_shape bound every rank's buffer: a batch past them would be
+    # truncated and mis-assembled on rank 0, so it is an error, never clamped
+    if len(first) - 1 > max_nars:
+        raise ValueError(f"gather_batch_async: {len(first) - 1} NARs exceed the agreed max_nars {max_nars}")
+    if int(first[-1]) > max_cap:
+        raise ValueError(f"gather_batch_async: {int(first[-1])} descriptors exceed the agreed max_cap {max_cap}")
+    if desc.numel() < int(first[-1]) * DESC_BYTES:
+        raise ValueError("gather_batch_async: desc holds fewer bytes than nar_first[-1] descriptors")
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = desc.device
@@ -106,7 +114,7 @@ def gather_batch_async(desc: torch.Tensor, nar_first, max_cap: int, max_nars: in
     meta = torch.from_numpy(meta_h.view(np.uint8))
     mb = meta.numel()
     want = max_cap * DESC_BYTES
-    n = min(desc.numel(), want, int(first[-1]) * DESC_BYTES)
+    n = int(first[-1]) * DESC_BYTES
     packed = torch.zeros(mb + want, dtype=torch.uint8, device=dev)
     packed[:mb].copy_(meta.pin_memory() if dev.type == "cuda" else meta, non_blocking=True)
     packed[mb: mb + n].copy_(desc[:n], non_blocking=True)

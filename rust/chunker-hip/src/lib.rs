@@ -57,6 +57,10 @@ extern "C" {
     fn cg_chunk_batch_device_async(d_data: *const u8, nar_offsets: *const u64, n: usize, min: u64, avg: u64,
                                    max: u64, algo: c_int, d_out: *mut CgDesc, cap: usize, stream: *mut c_void,
                                    batch: *mut *mut CgBatch) -> c_int;
+    fn cg_chunk_batch_device_async_after(d_data: *const u8, nar_offsets: *const u64, n: usize, min: u64, avg: u64,
+                                         max: u64, algo: c_int, d_out: *mut CgDesc, cap: usize,
+                                         stream: *mut c_void, inputs_ready: *mut c_void,
+                                         batch: *mut *mut CgBatch) -> c_int;
     fn cg_batch_wait(batch: *mut CgBatch, nar_first: *mut u64) -> c_int;
     fn cg_push_new(min: u64, avg: u64, max: u64, algo: c_int, status: *mut c_int) -> *mut CgPush;
     fn cg_push_push(h: *mut CgPush, data: *const u8, len: u64, out: *mut CgDesc, cap: usize,
@@ -156,7 +160,27 @@ pub fn chunk_descriptors(data: &[u8], min: usize, avg: usize, max: usize, algo: 
 pub fn chunk_batch(data: &[u8], offs: &[u64], min: usize, avg: usize, max: usize, algo: i32)
     -> Result<(Vec<CgDesc>, Vec<u64>), CgError> {
     let n = offs.len().saturating_sub(1);
-    let cap: usize = (0..n).map(|i| unsafe { cg_capacity(offs[i + 1] - offs[i], min as u64) }).sum::<usize>().max(1);
+    // cg_chunk_batch takes no length: it copies data[offs[0]..offs[n]], so the offsets are
+    // checked against `data` here, before any arithmetic on them or the FFI call
+    let bounds = |offset: u64, length: u64| CgError::Bounds {
+        data_len: data.len(),
+        offset: offset as usize,
+        length: length as usize,
+    };
+    for i in 0..n {
+        if offs[i + 1] < offs[i] {
+            return Err(bounds(offs[i], 0));
+        }
+    }
+    if n > 0 && offs[n] > data.len() as u64 {
+        return Err(bounds(offs[0], offs[n] - offs[0]));
+    }
+    let mut cap = 0usize;
+    for i in 0..n {
+        let c = unsafe { cg_capacity(offs[i + 1] - offs[i], min as u64) };
+        cap = cap.checked_add(c).ok_or(CgError::Capacity)?;
+    }
+    let cap = cap.max(1);
     let mut out = Vec::<CgDesc>::with_capacity(cap);
     let mut first = vec![0u64; n + 1];
     check(unsafe {
@@ -185,6 +209,21 @@ impl BatchInFlight {
         let mut h = std::ptr::null_mut();
         check(cg_chunk_batch_device_async(d_data, offs.as_ptr(), n, min as u64, avg as u64, max as u64, algo, d_out,
                                           cap, stream, &mut h))?;
+        Ok(BatchInFlight { h, n })
+    }
+    /// The same, with the boundary stages ordered after `inputs_ready` (a hipEvent_t recorded
+    /// after the last write to `d_data` and the last use of `d_out`) instead of after
+    /// everything on `stream`: they run under the digest of the batch queued before.
+    ///
+    /// # Safety
+    /// As `queue`; `inputs_ready` is a hipEvent_t (or null).
+    pub unsafe fn queue_after(d_data: *const u8, offs: &[u64], min: usize, avg: usize, max: usize, algo: i32,
+                              d_out: *mut CgDesc, cap: usize, stream: *mut c_void, inputs_ready: *mut c_void)
+        -> Result<Self, CgError> {
+        let n = offs.len().saturating_sub(1);
+        let mut h = std::ptr::null_mut();
+        check(cg_chunk_batch_device_async_after(d_data, offs.as_ptr(), n, min as u64, avg as u64, max as u64, algo,
+                                                d_out, cap, stream, inputs_ready, &mut h))?;
         Ok(BatchInFlight { h, n })
     }
     pub fn wait(mut self) -> Result<Vec<u64>, CgError> {

@@ -31,12 +31,12 @@ for s in $STEPS; do
          cut -c1-300 ${o}_bench_c2.json ;;
   configs)
          for c in c3 c4 c5; do
-           timeout -k 10 600 python bench.py --config $c --steps 20 --warmup 3 --no-concurrent --e2e '' > ${o}_bench_$c.json 2> ${o}_bench_$c.err || fail "bench $c" ${o}_bench_$c.err
+           timeout -k 10 600 python bench.py --config $c --steps 20 --warmup 3 --no-concurrent --e2e '' --drop-in '' > ${o}_bench_$c.json 2> ${o}_bench_$c.err || fail "bench $c" ${o}_bench_$c.err
            cut -c1-300 ${o}_bench_$c.json
          done ;;
   trace)
          for c in c2 c3 c4 c5; do
-           timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/${o}_trace_$c" -o run --output-format csv -- python3 "$R/bench.py" --config $c --steps 5 --warmup 2 --no-cpu-baseline --no-concurrent --no-clock --e2e '' > ${o}_trace_$c.log 2>&1 || fail "trace $c" ${o}_trace_$c.log
+           timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/${o}_trace_$c" -o run --output-format csv -- python3 "$R/bench.py" --config $c --steps 5 --warmup 2 --no-cpu-baseline --no-concurrent --no-clock --e2e '' --drop-in '' > ${o}_trace_$c.log 2>&1 || fail "trace $c" ${o}_trace_$c.log
            echo "trace $c ok"
          done ;;
   conc)  timeout -k 10 400 python bench.py --concurrent-only --concurrent-reps 6 > ${o}_conc_coal.json 2> ${o}_conc_coal.err || fail conc ${o}_conc_coal.err

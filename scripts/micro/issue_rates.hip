@@ -312,6 +312,100 @@ __device__ __forceinline__ void b3_var(uint32_t (*st)[16], const uint32_t (&m)[1
     }
 }
 
+// Kinds 104-106 (round 5): the G4 stream in an order pinned by one
+// asm volatile per instruction (the compiler keeps volatile asm in program order), so the
+// first-class ops (v_add_u32, v_xor_b32) come in runs between the second-class ones
+// (v_alignbit_b32 rotations, v_add3_u32).  104: two compressions interleaved, add3 split into
+// two v_add_u32 -- per step of 8 G's: 24 F, 8 H, 16 F, 8 H, 24 F, 8 H, 16 F, 8 H (10 F + 4 H
+// per G, 784 VALU per compression); 105: the same with one compression (runs of 12 / 8);
+// 106: two compressions, add3 kept (6 F + 6 H per G, 672 VALU per compression).
+#define A_ADD(d, x, y) asm volatile("v_add_u32 %0, %1, %2" : "=v"(d) : "v"(x), "v"(y))
+#define A_ADD3(d, x, y, z) asm volatile("v_add3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(x), "v"(y), "v"(z))
+#define A_XOR(d, x, y) asm volatile("v_xor_b32 %0, %1, %2" : "=v"(d) : "v"(x), "v"(y))
+#define A_ROT(d, x, n) asm volatile("v_alignbit_b32 %0, %1, %1, " #n : "=v"(d) : "v"(x))
+template <bool SPLIT, int NS>
+__device__ __forceinline__ void g4p(uint32_t (*st)[16], const uint32_t (&m)[16], const int (&ix)[4][4], int mo) {
+    // a += b + m0
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint32_t &a = st[s][ix[j][0]];
+            if constexpr (SPLIT) A_ADD(a, a, st[s][ix[j][1]]);
+            else A_ADD3(a, a, st[s][ix[j][1]], m[(mo + 2 * j) & 15]);
+        }
+    if constexpr (SPLIT) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) A_ADD(st[s][ix[j][0]], st[s][ix[j][0]], m[(mo + 2 * j) & 15]);
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) A_XOR(st[s][ix[j][3]], st[s][ix[j][3]], st[s][ix[j][0]]);
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) A_ROT(st[s][ix[j][3]], st[s][ix[j][3]], 16);
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) A_ADD(st[s][ix[j][2]], st[s][ix[j][2]], st[s][ix[j][3]]);
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) A_XOR(st[s][ix[j][1]], st[s][ix[j][1]], st[s][ix[j][2]]);
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) A_ROT(st[s][ix[j][1]], st[s][ix[j][1]], 12);
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint32_t &a = st[s][ix[j][0]];
+            if constexpr (SPLIT) A_ADD(a, a, st[s][ix[j][1]]);
+            else A_ADD3(a, a, st[s][ix[j][1]], m[(mo + 2 * j + 1) & 15]);
+        }
+    if constexpr (SPLIT) {
+#pragma unroll
+        for (int s = 0; s < NS; ++s)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) A_ADD(st[s][ix[j][0]], st[s][ix[j][0]], m[(mo + 2 * j + 1) & 15]);
+    }
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) A_XOR(st[s][ix[j][3]], st[s][ix[j][3]], st[s][ix[j][0]]);
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) A_ROT(st[s][ix[j][3]], st[s][ix[j][3]], 8);
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) A_ADD(st[s][ix[j][2]], st[s][ix[j][2]], st[s][ix[j][3]]);
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) A_XOR(st[s][ix[j][1]], st[s][ix[j][1]], st[s][ix[j][2]]);
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) A_ROT(st[s][ix[j][1]], st[s][ix[j][1]], 7);
+}
+template <bool SPLIT, int NS>
+__device__ __forceinline__ void b3_pinned(uint32_t (*st)[16], const uint32_t (&m)[16]) {
+    constexpr int col[4][4] = {{0, 4, 8, 12}, {1, 5, 9, 13}, {2, 6, 10, 14}, {3, 7, 11, 15}};
+    constexpr int dia[4][4] = {{0, 5, 10, 15}, {1, 6, 11, 12}, {2, 7, 8, 13}, {3, 4, 9, 14}};
+#pragma unroll
+    for (int rr = 0; rr < 7; ++rr) {
+        g4p<SPLIT, NS>(st, m, col, 0);
+        g4p<SPLIT, NS>(st, m, dia, 8);
+    }
+}
+
 template <int K>
 __global__ __launch_bounds__(256) void k_issue(uint32_t iters, uint32_t *out, unsigned long long *stamps) {
     extern __shared__ uint32_t lds_pad[];
@@ -362,6 +456,24 @@ __global__ __launch_bounds__(256) void k_issue(uint32_t iters, uint32_t *out, un
         for (uint32_t it = 0; it < iters; ++it) body_x<K>();
         t1 = __builtin_amdgcn_s_memtime();
         rt1 = __builtin_amdgcn_s_memrealtime();
+    } else if constexpr (K >= 104 && K <= 106) {
+        constexpr int NS = K == 105 ? 1 : 2;
+        uint32_t st[NS][16], m[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            m[i] = tid ^ (i * 0x01010101u);
+#pragma unroll
+            for (int k = 0; k < NS; ++k) st[k][i] = tid * 0x9E3779B9u + i + 77 * k;
+        }
+        t0 = __builtin_amdgcn_s_memtime();
+        rt0 = __builtin_amdgcn_s_memrealtime();
+        for (uint32_t it = 0; it < iters; ++it) b3_pinned<K != 106, NS>(st, m);
+        t1 = __builtin_amdgcn_s_memtime();
+        rt1 = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+#pragma unroll
+            for (int k = 0; k < NS; ++k) x ^= st[k][i];
     } else if constexpr (K >= 101 && K <= 103) {
         constexpr int NS = K == 101 ? 1 : 2;
         uint32_t st[NS][16], m[16];
@@ -482,6 +594,9 @@ static const char *kind_name(int k) {
     case 101: return "BLAKE3, add3 as two v_add_u32 (784 VALU)";
     case 102: return "BLAKE3, two compressions interleaved (1344 VALU)";
     case 103: return "BLAKE3, two interleaved + add3 split (1568 VALU)";
+    case 104: return "BLAKE3 pinned order, two interleaved + add3 split: F runs of 16-24 (1568 VALU)";
+    case 105: return "BLAKE3 pinned order, one compression + add3 split: F runs of 8-12 (784 VALU)";
+    case 106: return "BLAKE3 pinned order, two interleaved, add3 kept (1344 VALU)";
     case 110: return "mix HF HF (add3 / add alternating)";
     case 111: return "mix 8H 8F";
     case 112: return "mix H FFF";
@@ -505,7 +620,7 @@ int main(int argc, char **argv) {
     reg<32>(ks); reg<33>(ks); reg<34>(ks); reg<35>(ks); reg<36>(ks); reg<37>(ks); reg<38>(ks); reg<39>(ks);
     reg<40>(ks); reg<41>(ks); reg<42>(ks); reg<43>(ks); reg<44>(ks); reg<45>(ks); reg<46>(ks); reg<47>(ks);
     reg<60>(ks); reg<61>(ks); reg<62>(ks); reg<63>(ks); reg<64>(ks); reg<65>(ks); reg<66>(ks); reg<67>(ks);
-    reg<68>(ks); reg<100>(ks); reg<101>(ks); reg<102>(ks); reg<103>(ks);
+    reg<68>(ks); reg<100>(ks); reg<101>(ks); reg<102>(ks); reg<103>(ks); reg<104>(ks); reg<105>(ks); reg<106>(ks);
     reg<110>(ks); reg<111>(ks); reg<112>(ks); reg<113>(ks); reg<114>(ks); reg<115>(ks); reg<116>(ks);
     reg<117>(ks); reg<118>(ks); reg<119>(ks);
     std::vector<int> want;
@@ -530,7 +645,8 @@ int main(int argc, char **argv) {
     for (auto &kf : ks) {
         if (!want.empty() && std::find(want.begin(), want.end(), kf.first) == want.end()) continue;
         const int K = kf.first;
-        const uint32_t per_iter = K == 100 ? 672u : K == 101 ? 784u : K == 102 ? 1344u : K == 103 ? 1568u : 256u;
+        const uint32_t per_iter = K == 100 ? 672u : K == 101 || K == 105 ? 784u : K == 102 || K == 106 ? 1344u
+                                : K == 103 || K == 104 ? 1568u : 256u;
         CHK(hipFuncSetAttribute((const void *)kf.second, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max));
         printf("%s{\"kind\": %d, \"name\": \"%s\"", first ? "" : ",\n", K, kind_name(K));
         first = false;

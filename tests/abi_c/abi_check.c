@@ -110,6 +110,11 @@ static int nodevice(void) {
     CHECK(cg_chunk_batch_device_async(data, boffs, 1, 0, 0, 0, CG_SHA256, out, 64, NULL, &b) == CG_E_NO_DEVICE &&
               b == NULL,
           "async batch");
+    b = NULL;
+    CHECK(cg_chunk_batch_device_async_after(data, boffs, 1, 0, 0, 0, CG_SHA256, out, 64, NULL, NULL, &b) ==
+                  CG_E_NO_DEVICE &&
+              b == NULL,
+          "async batch after an event");
     cg_push *p = cg_push_new(0, 0, 0, CG_SHA256, &st);
     if (p) {
         CHECK(cg_push_push(p, data, sizeof data, out, 64, &n) == CG_E_NO_DEVICE, "push");

@@ -204,3 +204,18 @@ def test_check_gathered_batch():
     bad["offset"][2] = 1  # NAR 2 does not start at 0
     with pytest.raises(AssertionError, match="NAR 2"):
         check_gathered_batch(bad, first, sizes)
+
+
+def test_gather_batch_async_refuses_batches_past_the_agreed_shape():
+    """A rank whose batch exceeds the shapes gather_shape agreed must fail, not be truncated
+    (the descriptors past max_cap would be dropped and rank 0 would mis-assemble the batch).
+    The checks run before any collective, so no process group is needed."""
+    from chunker_amd.dist import gather_batch_async
+
+    desc = torch.zeros(5 * DESC_BYTES, dtype=torch.uint8)
+    with pytest.raises(ValueError, match="max_cap"):
+        gather_batch_async(desc, np.array([0, 5], np.uint64), max_cap=4, max_nars=1)
+    with pytest.raises(ValueError, match="max_nars"):
+        gather_batch_async(desc, np.array([0, 2, 5], np.uint64), max_cap=8, max_nars=1)
+    with pytest.raises(ValueError, match="fewer bytes"):
+        gather_batch_async(desc[:48], np.array([0, 5], np.uint64), max_cap=8, max_nars=1)

@@ -813,3 +813,50 @@ def test_async_batches_match_sync(ca, O):
     first = ca.chunk_batch_device_async(b[0].data_ptr(), b[1], outs[0].data_ptr(), b[2], 4096, 16384, 65536,
                                         hash=SHA, stream=stream).wait()
     assert np.array_equal(first, b[5])
+
+
+def test_async_after_inputs_ready_matches_sync(ca, O):
+    """cg_chunk_batch_device_async_after: each batch's input is written on ANOTHER stream
+    (a pinned H2D copy) and its boundary stages wait only for that copy's event, not for the
+    batch queued before on the digest stream -- so they run under that batch's digest.
+    Every batch (SHA-256 and BLAKE3, all five queued before the first wait) equals the
+    synchronous entry's descriptors and index, and the oracle on a sampled NAR."""
+    import torch
+
+    from chunker_amd.nar import synth_nars
+
+    stream = torch.cuda.Stream()
+    copy = torch.cuda.Stream()
+    batches = []
+    for seed, algo in ((11, SHA), (12, B3), (13, SHA), (14, SHA), (15, B3)):
+        sizes = [4 << 20] * 12 + [8 * seed + 4096, 300_008]
+        data, offs = synth_nars(sizes, first_index=1000 * seed)
+        cap = ca.chunking.batch_capacity(offs, 16384)
+        ref = torch.from_numpy(data).cuda()
+        ref_out = torch.zeros(cap * 48, dtype=torch.uint8, device="cuda")
+        ref_first = ca.chunk_batch_device(ref.data_ptr(), offs, ref_out.data_ptr(), cap, 16384, 65536, 262144,
+                                          hash=algo, stream=torch.cuda.current_stream().cuda_stream)
+        del ref
+        batches.append((torch.from_numpy(data).pin_memory(), offs, cap, algo, ref_out.cpu().numpy(), ref_first, data))
+    torch.cuda.synchronize()
+    devs = [torch.empty(len(b[6]) + 256, dtype=torch.uint8, device="cuda") for b in batches]
+    outs = [torch.full((b[2] * 48,), 0xAB, dtype=torch.uint8, device="cuda") for b in batches]
+    inflight = []
+    for k, b in enumerate(batches):
+        with torch.cuda.stream(copy):  # the input arrives on the copy stream
+            devs[k][: len(b[6])].copy_(b[0], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        inflight.append(ca.chunk_batch_device_async(devs[k].data_ptr(), b[1], outs[k].data_ptr(), b[2], 16384, 65536,
+                                                    262144, hash=b[3], stream=stream.cuda_stream,
+                                                    inputs_ready=ev.cuda_event))
+    for k, h in enumerate(inflight):
+        first = h.wait()
+        _, offs, cap, algo, ref_out, ref_first, data = batches[k]
+        assert np.array_equal(first, ref_first), k
+        n = int(first[-1])
+        got = outs[k].cpu().numpy()
+        assert np.array_equal(got[: n * 48], ref_out[: n * 48]), k
+        descs = got.view(ca.DESC_DTYPE)
+        want = O.chunk_descriptors(data[offs[12]:offs[13]], 16384, 65536, 262144, algo=algo)
+        assert_same(descs[int(first[12]):int(first[13])], want, f"batch{k} nar12")

@@ -10,8 +10,10 @@ reporting, and the reference's error variants with their fields.
   CG_E_IO instead of returning digests computed from a stale ring slot.
 * BufferLimitExceeded{attempted, limit} (src/chunking.rs:49-50) carries its fields.
 """
+import ctypes
 import os
 import threading
+import time
 
 import numpy as np
 import pytest
@@ -173,6 +175,48 @@ def test_concurrent_sha_callers_share_one_digest(ca, O, coalesce):
     finally:
         ca.lib.cg_test_coalesce(old)
     assert not errors, errors
+    torch.cuda.synchronize()
+    for t, (nars, offs, d, out, cap, s) in enumerate(jobs):
+        descs = out.cpu().numpy().view(ca.DESC_DTYPE)
+        first = firsts[t]
+        for i, nar in enumerate(nars):
+            ref = O.chunk_descriptors(nar, *P, algo=1, nthreads=8)
+            assert _same(descs[int(first[i]):int(first[i + 1])], ref), (t, i)
+
+
+def _coal_stats(ca):
+    out = (ctypes.c_uint64 * 4)()
+    ca.lib.cg_coalesce_stats(out)
+    return [int(x) for x in out]  # groups, members, leader wait us, windows run out
+
+
+def test_lone_and_few_callers_never_wait_for_the_window(ca, O):
+    """The coalescer's latency cost: a lone SHA-256 caller, calling
+    back to back, and up to CG_COAL_MIN (8) concurrent callers never enter a merged group,
+    so no leader window delays them (cg_coalesce_stats: no group formed, no window run
+    out); more than 8 callers do form groups, and every result is oracle-exact."""
+    import torch
+
+    old = ca.lib.cg_test_coalesce(1)
+    try:
+        jobs = _coalesced_jobs(ca, 12, seed=21)
+        time.sleep(0.1)  # (callers that returned within the last 50 ms count as expected back)
+        s0 = _coal_stats(ca)
+        _, errors = _run_threads(ca, jobs[:1], reps=4)  # a lone caller
+        assert not errors, errors
+        s1 = _coal_stats(ca)
+        assert s1 == s0, (s0, s1)
+        time.sleep(0.1)
+        _, errors = _run_threads(ca, jobs[:4], reps=2)  # a few callers
+        assert not errors, errors
+        s2 = _coal_stats(ca)
+        assert s2 == s1, (s1, s2)
+        firsts, errors = _run_threads(ca, jobs, reps=2)  # 12 callers: merged groups
+        assert not errors, errors
+        s3 = _coal_stats(ca)
+        assert s3[0] > s2[0] and 2 <= s3[1] - s2[1] <= 24, (s2, s3)
+    finally:
+        ca.lib.cg_test_coalesce(old)
     torch.cuda.synchronize()
     for t, (nars, offs, d, out, cap, s) in enumerate(jobs):
         descs = out.cpu().numpy().view(ca.DESC_DTYPE)
