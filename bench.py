@@ -70,7 +70,7 @@ def parse_args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-nars", type=int, default=0, help="0 = whole batch for c2/c3, 1 NAR for c4/c5")
     ap.add_argument("--no-concurrent", action="store_true", help="skip the K-batches-in-flight measurement")
-    ap.add_argument("--concurrent", default="8,32", help="K values of the in-flight measurement ('' = skip it)")
+    ap.add_argument("--concurrent", default="8,16,32", help="K values of the in-flight measurement ('' = skip it)")
     ap.add_argument("--concurrent-only", action="store_true", help="only the in-flight measurement (profiling)")
     ap.add_argument("--concurrent-reps", type=int, default=3, help="batches per thread in the in-flight measurement")
     ap.add_argument("--e2e", default="1,8,16", help="K values of the host-to-host in-flight measurement ('' = skip)")
@@ -79,12 +79,17 @@ def parse_args():
                          "entry cg_chunk_descriptors from K threads, SHA-256 and BLAKE3, against the CPU port on the "
                          "same threads ('' = skip)")
     ap.add_argument("--drop-in-only", action="store_true", help="only the drop-in leg (profiling)")
+    ap.add_argument("--drop-in-sizes", default="10,64,256,1024",
+                    help="MiB per call of the drop-in leg's one-caller size sweep ('' = skip)")
     ap.add_argument("--hw-queues", type=int, default=16, choices=range(0, 33), metavar="0..32",
                     help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's)")
     ap.add_argument("--no-clock", action="store_true", help="skip the digest clock measurement (scripts/sha_clock.py)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="queue each batch after everything on the stream (cg_chunk_batch_device_async): its "
                          "boundary stages wait for the previous batch's digest (A/B of the overlap)")
+    ap.add_argument("--split-mode", type=int, default=2, choices=(1, 2),
+                    help="overlapped batches: 1 = boundary stages on the library stream, digests in stream order; "
+                         "2 = the whole batch on the library stream (digests of consecutive batches overlap too)")
     ap.add_argument("--bound-priority", action="store_true",
                     help="boundary stages of overlapped batches on a highest-priority stream "
                          "(CHUNKER_AMD_BOUND_PRIORITY=1; A/B)")
@@ -153,6 +158,7 @@ def main():
     n_per, nar_bytes, params, algo, desc = CONFIGS[args.config]
     if args.no_coalesce:
         ca.lib.cg_test_coalesce(0)
+    ca.lib.cg_test_split_mode(args.split_mode)
     if args.concurrent_only:
         print(json.dumps({"concurrent": concurrent_rates(ca, torch, args, n_per, nar_bytes, params, algo)}))
         return
@@ -349,7 +355,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "steps_queued": 2,
-            "boundary_overlap": not args.no_overlap,
+            "overlap": "none" if args.no_overlap else ("boundary stages" if args.split_mode == 1 else "whole batch"),
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True,
@@ -383,7 +389,14 @@ def concurrent_rates(ca, torch, args, n_per, nar_bytes, params, algo):
     """K independent config batches in flight: K host threads, each with its own input
     batch, output array and HIP stream, calling cg_chunk_batch_device `reps` times.
     Aggregate GiB/s = K x reps x batch bytes / wall time (after one untimed round that
-    sizes every workspace).  The headline `value` stays the single-batch rate."""
+    sizes every workspace), and what a caller waits per call (p50 / p99 ms).  For SHA-256
+    both coalescer settings run, one after the other in this process: `merged` (digests
+    of more than 8 concurrent callers share one launch, the product) and `per_batch`
+    (cg_test_coalesce(0)), so the merged rate and its latency cost sit side by side; the
+    coalescer's own counters (groups, members, leader wait, windows run out) are reported
+    for the merged runs.  The headline `value` stays the single-batch rate."""
+    import ctypes
+
     from chunker_amd.nar import synth_nars_device
 
     ks = sorted({int(k) for k in args.concurrent.split(",") if k})
@@ -401,37 +414,63 @@ def concurrent_rates(ca, torch, args, n_per, nar_bytes, params, algo):
     batch_bytes = int(jobs[0][1][-1])
     coal = bool(ca.lib.cg_test_coalesce(1))
     ca.lib.cg_test_coalesce(int(coal))
-    res = {"unit": "GiB/s", "batch": f"{n_per}x{nar_bytes >> 20}MiB", "reps": max(1, args.concurrent_reps),
-           "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default (4)"),
-           "digests": "coalesced (one SHA-256 launch per group of concurrent callers)" if coal and algo == 1
-           else "one launch per batch"}
-    for K in ks:
-        for timed in (False, True):
-            reps = res["reps"] if timed else 1
-            bar = threading.Barrier(K + 1)
-            errs = []
+    res = {"unit": "GiB/s", "latency_unit": "ms per call", "batch": f"{n_per}x{nar_bytes >> 20}MiB",
+           "reps": max(1, args.concurrent_reps), "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default (4)"),
+           "digests": "coalesced (one SHA-256 launch per group of more than 8 concurrent callers)"
+           if coal and algo == 1 else "one launch per batch"}
+    modes = [("merged", 1), ("per_batch", 0)] if coal and algo == 1 else [("per_batch", int(coal))]
+    stats = (ctypes.c_uint64 * 4)()
 
-            def work(k):
-                d, offs, out, cap, s = jobs[k]
-                bar.wait()
-                try:
-                    for _ in range(reps):
-                        ca.chunk_batch_device(d.data_ptr(), offs, out.data_ptr(), cap, *params, hash=algo,
-                                              stream=s.cuda_stream)
-                except Exception as e:  # noqa: BLE001
-                    errs.append(repr(e))
+    def measure(K, reps):
+        bar = threading.Barrier(K + 1)
+        errs, lat = [], [[] for _ in range(K)]
 
-            th = [threading.Thread(target=work, args=(k,)) for k in range(K)]
-            for x in th:
-                x.start()
+        def work(k):
+            d, offs, out, cap, s = jobs[k]
             bar.wait()
-            t0 = time.perf_counter()
-            for x in th:
-                x.join()
-            dt = time.perf_counter() - t0
-            if errs:
-                raise RuntimeError(errs[0])
-        res[f"K{K}"] = round(K * reps * batch_bytes / dt / GIB, 3)
+            try:
+                for _ in range(reps):
+                    t = time.perf_counter()
+                    ca.chunk_batch_device(d.data_ptr(), offs, out.data_ptr(), cap, *params, hash=algo,
+                                          stream=s.cuda_stream)
+                    lat[k].append(time.perf_counter() - t)
+            except Exception as e:  # noqa: BLE001
+                errs.append(repr(e))
+
+        th = [threading.Thread(target=work, args=(k,)) for k in range(K)]
+        for x in th:
+            x.start()
+        bar.wait()
+        t0 = time.perf_counter()
+        for x in th:
+            x.join()
+        dt = time.perf_counter() - t0
+        if errs:
+            raise RuntimeError(errs[0])
+        ms = np.array([v for row in lat for v in row]) * 1e3
+        return dt, ms
+
+    for K in ks:
+        row = {}
+        for name, on in modes:
+            ca.lib.cg_test_coalesce(on)
+            measure(K, 1)  # untimed: sizes every workspace
+            time.sleep(0.1)  # (callers that returned within 50 ms count as expected back)
+            ca.lib.cg_coalesce_stats(stats)
+            s0 = [int(x) for x in stats]
+            dt, ms = measure(K, res["reps"])
+            ca.lib.cg_coalesce_stats(stats)
+            s1 = [int(x) for x in stats]
+            row[name] = {"GiBps": round(K * res["reps"] * batch_bytes / dt / GIB, 3),
+                         "p50": round(float(np.percentile(ms, 50)), 2), "p99": round(float(np.percentile(ms, 99)), 2)}
+            if on and algo == 1:
+                g = s1[0] - s0[0]
+                row[name]["coalescer"] = {"groups": g, "batches": s1[1] - s0[1],
+                                          "leader_wait_ms_mean": round((s1[2] - s0[2]) / 1e3 / g, 3) if g else 0.0,
+                                          "windows_run_out": s1[3] - s0[3]}
+        ca.lib.cg_test_coalesce(int(coal))
+        res[f"K{K}"] = row[modes[0][0]]["GiBps"]
+        res[f"K{K}_detail"] = row
     return res
 
 
@@ -585,6 +624,39 @@ def drop_in_rates(ca, args):
             c = run(lambda k: O.chunk_descriptors(bufs[k], *P, algo=algo, nthreads=cpu_nt))
             leg[f"K{K}"] = {"gpu": g, "cpu_port": c, "reps": reps}
         res[name] = leg
+    # one caller, larger inputs: where a single call starts to pay on the GPU (the SHA-256
+    # chain of the longest chunk is a fixed ~50-70 ms; the CPU port's serial FastCDC ~3 GiB/s)
+    sweep = {}
+    for mib in sorted({int(v) for v in args.drop_in_sizes.split(",") if v}):
+        nb = mib << 20
+        buf = synth_nars([nb], first_index=99)[0]
+        cap_s = int(ca.lib.cg_capacity(nb, P[0]))
+        out = np.zeros(cap_s, ca.DESC_DTYPE)
+        n = ctypes.c_size_t(0)
+        row = {}
+        for algo, name in ((1, "sha256"), (0, "blake3")):
+            want = O.chunk_descriptors(buf, *P, algo=algo, nthreads=nt)
+            reps = 3 if mib >= 256 else 6
+            gt, ct = [], []
+            for r in range(reps + 1):
+                t = time.perf_counter()
+                st = ca.lib.cg_chunk_descriptors(buf.ctypes.data, nb, *P, algo, out.ctypes.data, cap_s, ctypes.byref(n))
+                if r:
+                    gt.append(time.perf_counter() - t)
+                assert st == 0, ca._lib.last_error()
+            assert n.value == len(want) and np.array_equal(out[: n.value].view(np.uint8), want.view(np.uint8)), \
+                f"drop-in sweep {name} {mib} MiB: descriptors differ from the CPU port"
+            for _ in range(reps):
+                t = time.perf_counter()
+                O.chunk_descriptors(buf, *P, algo=algo, nthreads=nt)
+                ct.append(time.perf_counter() - t)
+            g, c = float(np.median(gt)), float(np.median(ct))
+            row[name] = {"gpu_GiBps": round(nb / g / GIB, 3), "gpu_ms": round(g * 1e3, 2),
+                         "cpu_port_GiBps": round(nb / c / GIB, 3), "cpu_port_ms": round(c * 1e3, 2)}
+        sweep[f"{mib}MiB"] = row
+        del buf, out
+    if sweep:
+        res["one_caller_sizes"] = {"note": f"K = 1, median of 3-6 calls; CPU port on {nt} threads", **sweep}
     return res
 
 

@@ -53,7 +53,8 @@ EXPORTS = (
 TEST_HOOKS = ("cg_test_sha_quad_max", "cg_test_sha_split_max", "cg_test_sha_spin_limit", "cg_test_cas_pair_max",
               "cg_test_fail_alloc", "cg_test_sha_quad_fill", "cg_test_sha_pair_fill", "cg_test_scan_path", "cg_test_scan_kernel", "cg_test_coalesce", "cg_test_scan_grid",
               "cg_test_stream_group_cap", "cg_test_stream_max_lanes", "cg_test_stream_eager",
-              "cg_test_b3_fused_plan", "cg_test_b3_packed", "cg_coalesce_stats")
+              "cg_test_b3_fused_plan", "cg_test_b3_packed", "cg_coalesce_stats",
+              "cg_test_split_mode")
 
 
 def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
@@ -159,6 +160,8 @@ def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
         if hasattr(L, name):
             getattr(L, name).argtypes = [i]
             getattr(L, name).restype = i
+    L.cg_test_split_mode.argtypes = [i]
+    L.cg_test_split_mode.restype = i
     L.cg_coalesce_stats.argtypes = [p]
     L.cg_coalesce_stats.restype = None
     L.cg_test_fail_alloc.argtypes = [ctypes.c_uint32]

@@ -381,9 +381,9 @@ def chunk_batch_device_async(d_data_ptr: int, nar_offsets: np.ndarray, d_out_ptr
     the next batch queued while waiting for the current one hides the host side of every
     call behind the GPU's work.  `inputs_ready` (a hipEvent_t handle, e.g.
     torch.cuda.Event().cuda_event, recorded after the last write to the input and the last
-    use of the output array) orders the boundary stages after that event only
-    (cg_chunk_batch_device_async_after), so they run under the digest of the batch queued
-    before on `stream`; 0 = after everything queued on `stream`."""
+    use of the output array) orders the batch after that event only
+    (cg_chunk_batch_device_async_after): it runs on a library stream beside the batch queued
+    before it, and `stream` waits for its end; 0 = after everything queued on `stream`."""
     o = ChunkingOptions.resolve(min_size, avg_size, max_size)
     offs = np.ascontiguousarray(nar_offsets, dtype=np.uint64)
     n = len(offs) - 1

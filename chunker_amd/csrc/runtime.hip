@@ -289,6 +289,15 @@ uint32_t seg_slots(const CdcParams &p) {
 // waits for its group's end, so its own tail (NAR index, spin-guard word) and its
 // completion event follow the merged digest.  A group of one runs the ordinary per-batch
 // launch on the member's own stream, so a lone caller's latency is unchanged.
+//
+// What a member can wait for, beyond its own digest's chain: callers only merge past
+// CG_COAL_MIN (8) in the entry, so a lone caller and up to 8 concurrent ones never enter a
+// group (they go solo and no leader counts them: test_lone_and_few_callers_never_wait_for_the
+// _window); a merged member waits at most kCoalWindow (3 ms) for its group to form plus the
+// previous group's remaining chain on the one set (lease_set: <= one longest-chunk chain,
+// ~55-75 ms at the default 4 MiB max), i.e. its call returns within window + 2 chains + its
+// boundary stages.  bench.py's `concurrent` leg reports the measured per-call p50 / p99 of
+// merged and per-batch digests side by side, and the leader's mean wait (cg_coalesce_stats).
 // ---------------------------------------------------------------------------
 struct CoalGroup {
     hipEvent_t done = nullptr;
@@ -322,6 +331,13 @@ struct Coalescer {
 Coalescer g_coal[64];
 thread_local CoalActive *t_coal_active = nullptr;
 std::atomic<uint32_t> g_coalesce{1};  // test hook cg_test_coalesce
+// cg_chunk_batch_device_async_after: 2 (the product) = the whole batch runs on the library
+// stream, ordered after inputs_ready only, and the caller's stream waits for its end, so
+// the digests of consecutive batches overlap as well (config 2 18.1 -> 35.9 GiB/s, config 5
+// 225 -> 360, config 4 695 -> 722; BLAKE3 config 3 equal: its digest fills the chip,
+// profiles/r05_v3_split_ab.txt); 1 = only the boundary stages do and the digest joins the
+// caller's stream (test hook cg_test_split_mode)
+std::atomic<int> g_split_mode{2};
 #ifndef CG_COAL_WINDOW_US
 #define CG_COAL_WINDOW_US 3000
 #endif
@@ -836,7 +852,14 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
                             static_cast<uint64_t *>(ws->first_host.dev), &first_on_host);
     if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_ASSEMBLE], bs));
     bl->dstart = ws->ev[EV_ASSEMBLE];
-    if (bs != st) {  // join: the digest (and everything after it) follows the boundary stages
+    // The digest's stream: `st`, joined after the boundary stages (split mode 1), or -- split
+    // mode 2 -- the library stream itself, so the whole batch is ordered after inputs_ready
+    // only and `st` waits for its end (below): a batch's digest then runs beside the digest of
+    // the batch queued before it.
+    hipStream_t ds = st;
+    if (bs != st && g_split_mode.load(std::memory_order_relaxed) == 2) {
+        ds = bs;
+    } else if (bs != st) {  // join: the digest (and everything after it) follows the boundary stages
         HIP_TRY(hipEventRecord(ws->ev_bdone, bs));
         HIP_TRY(hipStreamWaitEvent(st, ws->ev_bdone, 0));
         if (prof) {
@@ -875,43 +898,44 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
         if ((rc = ws->order.ensure(cg::sha256_order_tmp_elems(chunk_bound) * 4, "order"))) return rc;
         // expected chunk count: FastCDC's mean chunk is about min + avg on random data
         const uint64_t expected = std::min<uint64_t>(chunk_bound, total_len / (o.min + o.avg) + n_nars);
-        if ((rc = sha_err_arm(ws, st))) return rc;
+        if ((rc = sha_err_arm(ws, ds))) return rc;
         sha_armed = true;
         if (coalesce && chunk_bound && coalesce_worth(ws->device)) {
-            CoalEntry e{ws, d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, expected, o.max, st};
+            CoalEntry e{ws, d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, expected, o.max, ds};
             e.active = t_coal_active;
             if ((rc = coalesced_sha256(&e))) return rc;
         } else {
             if (t_coal_active) t_coal_active->go_solo();  // nothing to merge: do not hold a leader back
             cg::launch_sha256(d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, expected, o.max,
-                              ws->order.as<uint32_t>(), hash_base, sizeof(cg_desc), ws->sha_err.as<uint32_t>(), st);
+                              ws->order.as<uint32_t>(), hash_base, sizeof(cg_desc), ws->sha_err.as<uint32_t>(), ds);
         }
     } else {
         cg::launch_blake3(d_data, ws->chunk_abs.as<uint64_t>(), d_out, d_total, chunk_bound, total_len, hash_base,
                           sizeof(cg_desc), ws->b3_gmap.as<uint32_t>(), ws->b3_gbase.as<uint64_t>(),
                           ws->b3_gcount.as<uint32_t>(), ws->scan_tmp.as<uint64_t>(), ws->b3_gcv.as<uint32_t>(), true,
-                          st, b3_planned, b3_planned ? b3plan.leaf_base : nullptr, b3plan.lmap);
+                          ds, b3_planned, b3_planned ? b3plan.leaf_base : nullptr, b3plan.lmap);
     }
-    if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_DIGEST], st));
-    if (d_chunk_ids) HIP_TRY(hipStreamWaitEvent(st, ws->ev_join, 0));
+    if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_DIGEST], ds));
+    if (d_chunk_ids) HIP_TRY(hipStreamWaitEvent(ds, ws->ev_join, 0));
     HIP_TRY(hipGetLastError());
     if (first_on_host) {
         s_first = ws->first_host.as<uint64_t>();
     } else {
-        HIP_TRY(hipMemcpyAsync(s_first, ws->nar_first.p, (n_nars + 1) * 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(s_first, ws->nar_first.p, (n_nars + 1) * 8, hipMemcpyDeviceToHost, ds));
     }
     if (d_man && h_manifest_ids)
-        HIP_TRY(hipMemcpyAsync(h_manifest_ids, d_man, n_nars * 32, hipMemcpyDeviceToHost, st));
-    if (sha_armed && (rc = sha_err_fetch(ws, st))) return rc;
+        HIP_TRY(hipMemcpyAsync(h_manifest_ids, d_man, n_nars * 32, hipMemcpyDeviceToHost, ds));
+    if (sha_armed && (rc = sha_err_fetch(ws, ds))) return rc;
     // the batch's end: the digest-stage timing event when nothing was queued after it (each
     // event between two batches' kernels holds the second back by ~6 us), else one more
     const bool tail_ops = d_chunk_ids || !first_on_host || sha_armed || (d_man && h_manifest_ids);
     if (prof && !tail_ops) {
         bl->done = ws->ev[EV_DIGEST];
     } else {
-        HIP_TRY(hipEventRecord(ws->ev_done, st));
+        HIP_TRY(hipEventRecord(ws->ev_done, ds));
         bl->done = ws->ev_done;
     }
+    if (ds != st) HIP_TRY(hipStreamWaitEvent(st, bl->done, 0));  // later work on `st` follows the batch
     bl->s_first = s_first;
     bl->n_nars = n_nars;
     bl->out_cap = out_cap;
@@ -1304,6 +1328,8 @@ int push_append(cg_push *h, const uint8_t *data, uint64_t len) {
 }
 
 }  // namespace cgrt
+
+extern "C" int cg_test_split_mode(int v) { return cgrt::g_split_mode.exchange(v == 2 ? 2 : 1); }
 
 extern "C" uint32_t cg_test_coalesce(uint32_t v) {  // 0 = every device-entry call digests alone
     return cgrt::g_coalesce.exchange(v ? 1u : 0u);

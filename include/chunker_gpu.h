@@ -113,14 +113,15 @@ int cg_chunk_batch_device_async(const uint8_t *d_data, const uint64_t *nar_offse
                                 cg_desc *d_out, size_t out_cap, void *stream, cg_batch **batch);
 int cg_batch_wait(cg_batch *batch, uint64_t *nar_first);
 
-/* The same queued batch with its boundary stages (candidate scan, cut walk, descriptor
- * assembly) ordered after `inputs_ready` -- a hipEvent_t recorded after the last write to
- * d_data and the last use of d_out -- instead of after everything queued on `stream`
- * (NULL = cg_chunk_batch_device_async).  They run on a library stream, so a batch's
- * boundary stages overlap the digest of the batch queued before it on `stream` (SHA-256's
- * digest is bound by its longest chunk's serial chain and leaves most of the chip idle);
- * the digest, the NAR index and the batch's end stay in `stream` order, so batches on one
- * stream still complete in order.  Replaces the collect-then-hash sequence of
+/* The same queued batch ordered after `inputs_ready` -- a hipEvent_t recorded after the
+ * last write to d_data and the last use of d_out -- instead of after everything queued on
+ * `stream` (NULL = cg_chunk_batch_device_async).  The batch (candidate scan, cut walk,
+ * descriptor assembly, digest) runs on a library stream of its workspace and `stream` waits
+ * for its end: work queued on `stream` afterwards sees the finished descriptors, and
+ * cg_batch_wait waits for this batch alone.  So a caller that keeps two batches queued
+ * (double-buffered inputs) has the second batch's boundary stages AND digest run beside the
+ * first's digest -- SHA-256's digest is bound by its longest chunk's serial chain and leaves
+ * most of the chip idle.  Replaces the collect-then-hash sequence of
  * chunk_descriptors_with_hash (src/chunking.rs:334-342) across consecutive calls. */
 int cg_chunk_batch_device_async_after(const uint8_t *d_data, const uint64_t *nar_offsets, size_t n_nars,
                                       uint64_t min_size, uint64_t avg_size, uint64_t max_size, int algo,

@@ -266,49 +266,63 @@ __device__ __forceinline__ uint32_t add3x(uint32_t a, uint32_t b, uint32_t c) {
         return a + b + c;
     }
 }
-template <bool SPLIT, int NS>
+// SEP (kinds 107-108): between the op groups 0 = nothing, 1 = an `s_nop 0`, 2 = a
+// scheduling barrier (the groups stay in order, no instruction between them)
+template <int SEP>
+__device__ __forceinline__ void gsep() {
+    if constexpr (SEP == 1) asm volatile("s_nop 0");
+    if constexpr (SEP == 2) __builtin_amdgcn_sched_barrier(0);
+}
+template <bool SPLIT, int NS, int SEP = 0>
 __device__ __forceinline__ void g4x(uint32_t (*st)[16], const uint32_t (&m)[16], const int (&ix)[4][4], int mo) {
 #pragma unroll
     for (int s = 0; s < NS; ++s)
 #pragma unroll
         for (int j = 0; j < 4; ++j) st[s][ix[j][0]] = add3x<SPLIT>(st[s][ix[j][0]], st[s][ix[j][1]], m[(mo + 2 * j) & 15]);
+    gsep<SEP>();
 #pragma unroll
     for (int s = 0; s < NS; ++s)
 #pragma unroll
         for (int j = 0; j < 4; ++j) st[s][ix[j][3]] = rotr(st[s][ix[j][3]] ^ st[s][ix[j][0]], 16);
+    gsep<SEP>();
 #pragma unroll
     for (int s = 0; s < NS; ++s)
 #pragma unroll
         for (int j = 0; j < 4; ++j) st[s][ix[j][2]] = st[s][ix[j][2]] + st[s][ix[j][3]];
+    gsep<SEP>();
 #pragma unroll
     for (int s = 0; s < NS; ++s)
 #pragma unroll
         for (int j = 0; j < 4; ++j) st[s][ix[j][1]] = rotr(st[s][ix[j][1]] ^ st[s][ix[j][2]], 12);
+    gsep<SEP>();
 #pragma unroll
     for (int s = 0; s < NS; ++s)
 #pragma unroll
         for (int j = 0; j < 4; ++j) st[s][ix[j][0]] = add3x<SPLIT>(st[s][ix[j][0]], st[s][ix[j][1]], m[(mo + 2 * j + 1) & 15]);
+    gsep<SEP>();
 #pragma unroll
     for (int s = 0; s < NS; ++s)
 #pragma unroll
         for (int j = 0; j < 4; ++j) st[s][ix[j][3]] = rotr(st[s][ix[j][3]] ^ st[s][ix[j][0]], 8);
+    gsep<SEP>();
 #pragma unroll
     for (int s = 0; s < NS; ++s)
 #pragma unroll
         for (int j = 0; j < 4; ++j) st[s][ix[j][2]] = st[s][ix[j][2]] + st[s][ix[j][3]];
+    gsep<SEP>();
 #pragma unroll
     for (int s = 0; s < NS; ++s)
 #pragma unroll
         for (int j = 0; j < 4; ++j) st[s][ix[j][1]] = rotr(st[s][ix[j][1]] ^ st[s][ix[j][2]], 7);
 }
-template <bool SPLIT, int NS>
+template <bool SPLIT, int NS, int SEP = 0>
 __device__ __forceinline__ void b3_var(uint32_t (*st)[16], const uint32_t (&m)[16]) {
     constexpr int col[4][4] = {{0, 4, 8, 12}, {1, 5, 9, 13}, {2, 6, 10, 14}, {3, 7, 11, 15}};
     constexpr int dia[4][4] = {{0, 5, 10, 15}, {1, 6, 11, 12}, {2, 7, 8, 13}, {3, 4, 9, 14}};
 #pragma unroll
     for (int rr = 0; rr < 7; ++rr) {
-        g4x<SPLIT, NS>(st, m, col, 0);
-        g4x<SPLIT, NS>(st, m, dia, 8);
+        g4x<SPLIT, NS, SEP>(st, m, col, 0);
+        g4x<SPLIT, NS, SEP>(st, m, dia, 8);
     }
 }
 
@@ -474,7 +488,7 @@ __global__ __launch_bounds__(256) void k_issue(uint32_t iters, uint32_t *out, un
         for (int i = 0; i < 16; ++i)
 #pragma unroll
             for (int k = 0; k < NS; ++k) x ^= st[k][i];
-    } else if constexpr (K >= 101 && K <= 103) {
+    } else if constexpr ((K >= 101 && K <= 103) || K == 107 || K == 108) {
         constexpr int NS = K == 101 ? 1 : 2;
         uint32_t st[NS][16], m[16];
 #pragma unroll
@@ -486,7 +500,7 @@ __global__ __launch_bounds__(256) void k_issue(uint32_t iters, uint32_t *out, un
         t0 = __builtin_amdgcn_s_memtime();
         rt0 = __builtin_amdgcn_s_memrealtime();
         for (uint32_t it = 0; it < iters; ++it) {
-            b3_var<K != 102, NS>(st, m);
+            b3_var<K != 102 && K != 107 && K != 108, NS, K == 107 ? 1 : K == 108 ? 2 : 0>(st, m);
 #pragma unroll
             for (int k = 0; k < NS; ++k) asm volatile("" : "+v"(st[k][0]), "+v"(st[k][5]), "+v"(st[k][10]), "+v"(st[k][15]));
         }
@@ -597,6 +611,8 @@ static const char *kind_name(int k) {
     case 104: return "BLAKE3 pinned order, two interleaved + add3 split: F runs of 16-24 (1568 VALU)";
     case 105: return "BLAKE3 pinned order, one compression + add3 split: F runs of 8-12 (784 VALU)";
     case 106: return "BLAKE3 pinned order, two interleaved, add3 kept (1344 VALU)";
+    case 107: return "BLAKE3 kind 102 + s_nop 0 between op groups (1344 VALU)";
+    case 108: return "BLAKE3 kind 102 + sched_barrier between op groups (1344 VALU)";
     case 110: return "mix HF HF (add3 / add alternating)";
     case 111: return "mix 8H 8F";
     case 112: return "mix H FFF";
@@ -620,7 +636,7 @@ int main(int argc, char **argv) {
     reg<32>(ks); reg<33>(ks); reg<34>(ks); reg<35>(ks); reg<36>(ks); reg<37>(ks); reg<38>(ks); reg<39>(ks);
     reg<40>(ks); reg<41>(ks); reg<42>(ks); reg<43>(ks); reg<44>(ks); reg<45>(ks); reg<46>(ks); reg<47>(ks);
     reg<60>(ks); reg<61>(ks); reg<62>(ks); reg<63>(ks); reg<64>(ks); reg<65>(ks); reg<66>(ks); reg<67>(ks);
-    reg<68>(ks); reg<100>(ks); reg<101>(ks); reg<102>(ks); reg<103>(ks); reg<104>(ks); reg<105>(ks); reg<106>(ks);
+    reg<68>(ks); reg<100>(ks); reg<101>(ks); reg<102>(ks); reg<103>(ks); reg<104>(ks); reg<105>(ks); reg<106>(ks); reg<107>(ks); reg<108>(ks);
     reg<110>(ks); reg<111>(ks); reg<112>(ks); reg<113>(ks); reg<114>(ks); reg<115>(ks); reg<116>(ks);
     reg<117>(ks); reg<118>(ks); reg<119>(ks);
     std::vector<int> want;
@@ -645,7 +661,7 @@ int main(int argc, char **argv) {
     for (auto &kf : ks) {
         if (!want.empty() && std::find(want.begin(), want.end(), kf.first) == want.end()) continue;
         const int K = kf.first;
-        const uint32_t per_iter = K == 100 ? 672u : K == 101 || K == 105 ? 784u : K == 102 || K == 106 ? 1344u
+        const uint32_t per_iter = K == 100 ? 672u : K == 101 || K == 105 ? 784u : K == 102 || K == 106 || K == 107 || K == 108 ? 1344u
                                 : K == 103 || K == 104 ? 1568u : 256u;
         CHK(hipFuncSetAttribute((const void *)kf.second, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max));
         printf("%s{\"kind\": %d, \"name\": \"%s\"", first ? "" : ",\n", K, kind_name(K));

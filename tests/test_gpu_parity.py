@@ -815,7 +815,8 @@ def test_async_batches_match_sync(ca, O):
     assert np.array_equal(first, b[5])
 
 
-def test_async_after_inputs_ready_matches_sync(ca, O):
+@pytest.mark.parametrize("mode", [1, 2], ids=["boundary_split", "whole_batch_split"])
+def test_async_after_inputs_ready_matches_sync(ca, O, mode):
     """cg_chunk_batch_device_async_after: each batch's input is written on ANOTHER stream
     (a pinned H2D copy) and its boundary stages wait only for that copy's event, not for the
     batch queued before on the digest stream -- so they run under that batch's digest.
@@ -828,6 +829,7 @@ def test_async_after_inputs_ready_matches_sync(ca, O):
     stream = torch.cuda.Stream()
     copy = torch.cuda.Stream()
     batches = []
+    old_mode = ca.lib.cg_test_split_mode(mode)  # 2: the digests of queued batches overlap too
     for seed, algo in ((11, SHA), (12, B3), (13, SHA), (14, SHA), (15, B3)):
         sizes = [4 << 20] * 12 + [8 * seed + 4096, 300_008]
         data, offs = synth_nars(sizes, first_index=1000 * seed)
@@ -850,9 +852,17 @@ def test_async_after_inputs_ready_matches_sync(ca, O):
         inflight.append(ca.chunk_batch_device_async(devs[k].data_ptr(), b[1], outs[k].data_ptr(), b[2], 16384, 65536,
                                                     262144, hash=b[3], stream=stream.cuda_stream,
                                                     inputs_ready=ev.cuda_event))
+    # work queued on `stream` after the calls follows every batch (mode 2 joins each batch's
+    # end into it): copies queued now, before any wait, must see the finished descriptors
+    tails = [torch.empty_like(o) for o in outs]
+    with torch.cuda.stream(stream):
+        for t, o in zip(tails, outs):
+            t.copy_(o)
+    stream.synchronize()  # waits for the copies, which wait for every batch
     for k, h in enumerate(inflight):
         first = h.wait()
         _, offs, cap, algo, ref_out, ref_first, data = batches[k]
+        assert torch.equal(tails[k], outs[k]), f"batch{k}: work queued after it on the stream ran early"
         assert np.array_equal(first, ref_first), k
         n = int(first[-1])
         got = outs[k].cpu().numpy()
@@ -860,3 +870,4 @@ def test_async_after_inputs_ready_matches_sync(ca, O):
         descs = got.view(ca.DESC_DTYPE)
         want = O.chunk_descriptors(data[offs[12]:offs[13]], 16384, 65536, 262144, algo=algo)
         assert_same(descs[int(first[12]):int(first[13])], want, f"batch{k} nar12")
+    ca.lib.cg_test_split_mode(old_mode)
