@@ -335,14 +335,14 @@ def main():
     drop = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, n_per, nar_bytes, params, algo)
+    if world == 1 and args.drop_in:  # (before the concurrent leg: its 32 streams share the hardware queues)
+        drop = drop_in_rates(ca, args)
     if world == 1 and not args.no_concurrent:
         del d_outs, d_data
         torch.cuda.empty_cache()
         conc = concurrent_rates(ca, torch, args, n_per, nar_bytes, params, algo)
         if args.e2e:
             conc["e2e"] = e2e_rates(ca, torch, args, n_per, nar_bytes, params, algo, descs)
-    if world == 1 and args.drop_in:
-        drop = drop_in_rates(ca, args)
 
     if rank == 0:
         gear = "placeholder" if ca.lib.cg_gear_is_placeholder() else (
@@ -567,11 +567,9 @@ def drop_in_rates(ca, args):
     bufs = [synth_nars([ten], first_index=7 + k)[0] for k in range(kmax)]
     cap = int(ca.lib.cg_capacity(ten, P[0]))
     outs = [np.zeros(cap, ca.DESC_DTYPE) for _ in range(kmax)]
-    coal = bool(ca.lib.cg_test_coalesce(1))
-    ca.lib.cg_test_coalesce(int(coal))
     res = {"unit": "GiB/s", "call": "cg_chunk_descriptors, 10 MiB xorshift64 per call, 256K/1M/4M (BASELINE config 1)",
            "latency_unit": "ms per call", "cpu_threads_per_call": f"max(1, {nt} // K)",
-           "coalesced_host_calls": coal}
+           "digests": "one launch per call (the host entry never merges digests)"}
     for algo, name in ((1, "sha256"), (0, "blake3")):
         want = [O.chunk_descriptors(b, *P, algo=algo, nthreads=nt) for b in bufs]
         leg = {}

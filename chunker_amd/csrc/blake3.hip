@@ -69,6 +69,74 @@ __device__ __forceinline__ uint32_t rotr32b(uint32_t x, uint32_t n) { return __b
         v[b3] = rotr32b(v[b3] ^ v[c3], 7);                                                                          \
     }
 
+// The same step with every op pinned by its own asm statement (CG_B3_PINNED): the op
+// groups stay in the order above and v_xor_b32 / v_add_u32 write a register none of their
+// sources holds (early-clobber).  In the issue microbenchmark this stream issues 15-20 % of
+// its VALU instructions in pairs (two waves, one quad-cycle) where the compiler's schedule
+// of the same ops pairs 0.5 %: 3.82 vs 4.05 clocks per VALU at 4 waves per SIMD, 2,570 vs
+// 2,724 clocks per compression (scripts/micro/issue_rates.hip kinds 100 / 125,
+// profiles/r05_v6_b3_dual_issue.json).
+// On config 3 the pinned stream is the product: 1,342-1,371 vs 1,332-1,344 GiB/s, same box,
+// three alternating rounds (profiles/r05_v7_b3_pinned_ab.txt).
+#ifndef CG_B3_PINNED
+#define CG_B3_PINNED 1
+#endif
+#define B3P_ADD3(d, x, y, z) asm volatile("v_add3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(x), "v"(y), "v"(z))
+#define B3P_XOR(d, x, y) asm volatile("v_xor_b32 %0, %1, %2" : "=&v"(d) : "v"(x), "v"(y))
+#define B3P_ADD(d, x, y) asm volatile("v_add_u32 %0, %1, %2" : "=&v"(d) : "v"(x), "v"(y))
+#define B3P_ROT(d, x, n) asm volatile("v_alignbit_b32 %0, %1, %1, " #n : "=v"(d) : "v"(x))
+#define B3_G4P(a0, b0, c0, d0, a1, b1, c1, d1, a2, b2, c2, d2, a3, b3, c3, d3, mi)                                  \
+    {                                                                                                               \
+        B3P_ADD3(v[a0], v[a0], v[b0], m[mi[0]]);                                                                    \
+        B3P_ADD3(v[a1], v[a1], v[b1], m[mi[2]]);                                                                    \
+        B3P_ADD3(v[a2], v[a2], v[b2], m[mi[4]]);                                                                    \
+        B3P_ADD3(v[a3], v[a3], v[b3], m[mi[6]]);                                                                    \
+        B3P_XOR(v[d0], v[d0], v[a0]);                                                                               \
+        B3P_XOR(v[d1], v[d1], v[a1]);                                                                               \
+        B3P_XOR(v[d2], v[d2], v[a2]);                                                                               \
+        B3P_XOR(v[d3], v[d3], v[a3]);                                                                               \
+        B3P_ROT(v[d0], v[d0], 16);                                                                                  \
+        B3P_ROT(v[d1], v[d1], 16);                                                                                  \
+        B3P_ROT(v[d2], v[d2], 16);                                                                                  \
+        B3P_ROT(v[d3], v[d3], 16);                                                                                  \
+        B3P_ADD(v[c0], v[c0], v[d0]);                                                                               \
+        B3P_ADD(v[c1], v[c1], v[d1]);                                                                               \
+        B3P_ADD(v[c2], v[c2], v[d2]);                                                                               \
+        B3P_ADD(v[c3], v[c3], v[d3]);                                                                               \
+        B3P_XOR(v[b0], v[b0], v[c0]);                                                                               \
+        B3P_XOR(v[b1], v[b1], v[c1]);                                                                               \
+        B3P_XOR(v[b2], v[b2], v[c2]);                                                                               \
+        B3P_XOR(v[b3], v[b3], v[c3]);                                                                               \
+        B3P_ROT(v[b0], v[b0], 12);                                                                                  \
+        B3P_ROT(v[b1], v[b1], 12);                                                                                  \
+        B3P_ROT(v[b2], v[b2], 12);                                                                                  \
+        B3P_ROT(v[b3], v[b3], 12);                                                                                  \
+        B3P_ADD3(v[a0], v[a0], v[b0], m[mi[1]]);                                                                    \
+        B3P_ADD3(v[a1], v[a1], v[b1], m[mi[3]]);                                                                    \
+        B3P_ADD3(v[a2], v[a2], v[b2], m[mi[5]]);                                                                    \
+        B3P_ADD3(v[a3], v[a3], v[b3], m[mi[7]]);                                                                    \
+        B3P_XOR(v[d0], v[d0], v[a0]);                                                                               \
+        B3P_XOR(v[d1], v[d1], v[a1]);                                                                               \
+        B3P_XOR(v[d2], v[d2], v[a2]);                                                                               \
+        B3P_XOR(v[d3], v[d3], v[a3]);                                                                               \
+        B3P_ROT(v[d0], v[d0], 8);                                                                                   \
+        B3P_ROT(v[d1], v[d1], 8);                                                                                   \
+        B3P_ROT(v[d2], v[d2], 8);                                                                                   \
+        B3P_ROT(v[d3], v[d3], 8);                                                                                   \
+        B3P_ADD(v[c0], v[c0], v[d0]);                                                                               \
+        B3P_ADD(v[c1], v[c1], v[d1]);                                                                               \
+        B3P_ADD(v[c2], v[c2], v[d2]);                                                                               \
+        B3P_ADD(v[c3], v[c3], v[d3]);                                                                               \
+        B3P_XOR(v[b0], v[b0], v[c0]);                                                                               \
+        B3P_XOR(v[b1], v[b1], v[c1]);                                                                               \
+        B3P_XOR(v[b2], v[b2], v[c2]);                                                                               \
+        B3P_XOR(v[b3], v[b3], v[c3]);                                                                               \
+        B3P_ROT(v[b0], v[b0], 7);                                                                                   \
+        B3P_ROT(v[b1], v[b1], 7);                                                                                   \
+        B3P_ROT(v[b2], v[b2], 7);                                                                                   \
+        B3P_ROT(v[b3], v[b3], 7);                                                                                   \
+    }
+
 // Compress one block; returns the new chaining value in cv (first 8 output words).
 __device__ __forceinline__ void b3_compress(uint32_t cv[8], const uint32_t m[16], uint64_t counter, uint32_t blen,
                                             uint32_t flags) {
@@ -77,8 +145,13 @@ __device__ __forceinline__ void b3_compress(uint32_t cv[8], const uint32_t m[16]
                       blen, flags};
 #pragma unroll
     for (int r = 0; r < 7; ++r) {
+#if CG_B3_PINNED
+        B3_G4P(0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14, 3, 7, 11, 15, B3S.s[r]);
+        B3_G4P(0, 5, 10, 15, 1, 6, 11, 12, 2, 7, 8, 13, 3, 4, 9, 14, (B3S.s[r] + 8));
+#else
         B3_G4(0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14, 3, 7, 11, 15, B3S.s[r]);
         B3_G4(0, 5, 10, 15, 1, 6, 11, 12, 2, 7, 8, 13, 3, 4, 9, 14, (B3S.s[r] + 8));
+#endif
     }
 #pragma unroll
     for (int i = 0; i < 8; ++i) cv[i] = v[i] ^ v[i + 8];

@@ -15,8 +15,16 @@
 
 #include "scan_common.h"
 
-#ifndef CG_SCAN_FLUSH_OLD
-#define CG_SCAN_FLUSH_OLD 0
+// Segment flush: the product lets the compiler form the flush addresses,
+// which it hoists out of the row loop and, at 128 VGPRs, spills (3 VGPRs, 16 B of scratch;
+// each reload waits vmcnt and so drains the row ring on segments holding a candidate).
+// CG_SCAN_FLUSH_INPLACE=1 makes them in place from an opaque lane id (scan_common.h
+// flush_slots): no spill, no scratch -- and measured no faster: same box, three alternating
+// rounds, c2 0.1964-0.1967 vs 0.1943-0.1950 ms, c4 3.30-3.40 vs 3.24-3.29, c5 3.39-3.48 vs
+// 3.42-3.46 (profiles/r05_v5_scan_flush_ab.txt): the drain costs less than the extra live
+// registers of the in-place form.
+#ifndef CG_SCAN_FLUSH_INPLACE
+#define CG_SCAN_FLUSH_INPLACE 0
 #endif
 
 namespace cg {
@@ -445,7 +453,7 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
             if (u % F32_RPS == F32_RPS - 1) {  // segment end: flush its slots and count
                 const uint64_t seg = seg0 + row / F32_RPS;
                 if (row / F32_RPS < seg_lim) {
-#if CG_SCAN_FLUSH_OLD  // (A/B: the round-4 flush, whose addresses the compiler hoisted and spilled)
+#if !CG_SCAN_FLUSH_INPLACE  // (see CG_SCAN_FLUSH_INPLACE at the top)
                     if (lane < min(segc, cap)) seg_cand[seg * cap + lane] = slots[lane];
 #else
                     flush_slots(seg_cand + seg * cap, slots, min(segc, cap));
@@ -796,7 +804,7 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
                 if (uu == 1) {  // segment end: flush its slots and count
                     const uint64_t seg = seg0 + row / F32_RPS;
                     if (row / F32_RPS < seg_lim) {
-#if CG_SCAN_FLUSH_OLD  // (A/B: the round-4 flush, whose addresses the compiler hoisted and spilled)
+#if !CG_SCAN_FLUSH_INPLACE  // (see CG_SCAN_FLUSH_INPLACE at the top)
                         if (lane < min(segc, cap)) seg_cand[seg * cap + lane] = slots[lane];
 #else
                         flush_slots(seg_cand + seg * cap, slots, min(segc, cap));

@@ -428,7 +428,12 @@ cg_stream *cg_stream_new(uint64_t min_size, uint64_t avg_size, uint64_t max_size
     h->slot_bytes = (o.max + slice + 256 + 255) & ~255ull;
     const uint64_t budget = inflight_bytes ? inflight_bytes : 2048ull << 20;
     h->max_slots = std::max<uint64_t>(budget / h->slot_bytes, 4);
-    h->max_lanes = (size_t)std::min(std::max(g_hw_queues_at_load - 2, 2), 8);
+    // At HIP's default 4 queues ONE lane: a second lane's group chain ran beside the push's
+    // boundary passes and slowed them more than it overlapped (1 / 4 GiB streams 9.7 / 10.1
+    // GiB/s with one lane against 5.9 / 7.6 with two, profiles/r05_v5_stream_shape_q4.json;
+    // at 16 queues 8 lanes still win on long streams: 4 GiB 14.0 against 10.2,
+    // r05_v6_stream_shape_q16.json).
+    h->max_lanes = g_hw_queues_at_load <= 4 ? 1 : (size_t)std::min(g_hw_queues_at_load - 2, 8);
     if (g_stream_max_lanes) h->max_lanes = g_stream_max_lanes;
     h->lanes.reserve(h->max_lanes);
     // A group's SHA-256 launch takes one CU per 8 chunks (quad workgroups, padded to a CU

@@ -121,7 +121,9 @@ int cg_batch_wait(cg_batch *batch, uint64_t *nar_first);
  * cg_batch_wait waits for this batch alone.  So a caller that keeps two batches queued
  * (double-buffered inputs) has the second batch's boundary stages AND digest run beside the
  * first's digest -- SHA-256's digest is bound by its longest chunk's serial chain and leaves
- * most of the chip idle.  Replaces the collect-then-hash sequence of
+ * most of the chip idle.  (BLAKE3 batches are queued in `stream` order as by
+ * cg_chunk_batch_device_async: their digest fills the chip by itself.)  Replaces the
+ * collect-then-hash sequence of
  * chunk_descriptors_with_hash (src/chunking.rs:334-342) across consecutive calls. */
 int cg_chunk_batch_device_async_after(const uint8_t *d_data, const uint64_t *nar_offsets, size_t n_nars,
                                       uint64_t min_size, uint64_t avg_size, uint64_t max_size, int algo,
@@ -151,8 +153,9 @@ void cg_push_free(cg_push *h);
  * :713-716) bytes, each reused only after the digests reading it completed.  The arena
  * starts at two slots at the first push and grows to that budget only when no slot is
  * free (a short stream holds two slots); at the budget a push waits for the oldest
- * digests.  Digests run on up to one HIP stream per hardware queue beside the call's
- * own and the null stream's (GPU_MAX_HW_QUEUES - 2, 2..8, read at cg_stream_new),
+ * digests.  Digests run on one HIP stream at up to 4 hardware queues (HIP's default) and
+ * otherwise on up to one per queue beside the call's own and the null stream's
+ * (GPU_MAX_HW_QUEUES - 2, at most 8; the variable as the library was loaded),
  * created as they are needed, each on groups of at most 2048 / lanes chunks' expected
  * bytes (so all lanes' SHA-256 workgroups fit the chip at once).
  * push returns once its bytes are copied: the caller may reuse `data` right away.  take

@@ -140,6 +140,15 @@ pub fn available() -> bool {
 pub const BLAKE3: i32 = 0;
 pub const SHA256: i32 = 1;
 
+/// Dispatch rule (measured by bench.py's drop_in leg): BLAKE3 pays on the
+/// GPU from one 10 MiB call on (29 vs 2.9 GiB/s); a SHA-256 call lasts its longest chunk's
+/// serial chain (~30-90 ms), so it pays only for large inputs (1 GiB: 11.3 vs 4.9 GiB/s;
+/// 256 MiB: even).  Smaller SHA-256 calls stay on the reference's CPU path.
+pub const SHA256_SINGLE_CALL_MIN: usize = 512 << 20;
+pub fn pays(algo: i32, len: usize) -> bool {
+    algo == BLAKE3 || len >= SHA256_SINGLE_CALL_MIN
+}
+
 /// chunk_descriptors_with_hash (src/chunking.rs:323-374) for one input.
 pub fn chunk_descriptors(data: &[u8], min: usize, avg: usize, max: usize, algo: i32)
     -> Result<Vec<CgDesc>, CgError> {

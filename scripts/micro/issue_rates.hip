@@ -116,6 +116,12 @@ __device__ __forceinline__ void mix_op(uint32_t (&r)[16], uint64_t (&q)[8], int 
         asm volatile("v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:BYTE_2" : "+v"(r[c]) : "v"(r[8 + c]));
     if constexpr (T == 'M') OP3("v_min3_u32");
     if constexpr (T == 'R') asm volatile("v_lshrrev_b32 %0, 3, %0" : "+v"(r[c]));
+    // operand-order probes (kinds 120-123): the accumulated register as src1 (the form the
+    // compiler emits for a commutative op: v_add_u32_e32 vD, vS, vD), or a fresh destination
+    if constexpr (T == 'f') asm volatile("v_add_u32 %0, %1, %0" : "+v"(r[c]) : "v"(r[8 + c]));
+    if constexpr (T == 'x') asm volatile("v_xor_b32 %0, %1, %0" : "+v"(r[c]) : "v"(r[8 + c]));
+    if constexpr (T == 'X') asm volatile("v_xor_b32 %0, %0, %1" : "+v"(r[c]) : "v"(r[8 + c]));
+    if constexpr (T == 'n') asm volatile("v_add_u32 %0, %1, %2" : "=v"(r[c]) : "v"(r[8 + c]), "v"(r[(c + 1) & 7]));
 }
 template <char... P>
 __device__ __forceinline__ void mix_body(uint32_t (&r)[16], uint64_t (&q)[8]) {
@@ -133,6 +139,10 @@ __device__ __forceinline__ void mix_body(uint32_t (&r)[16], uint64_t (&q)[8]) {
             if (pat[j] == 'S') mix_op<'S'>(r, q, c);
             if (pat[j] == 'M') mix_op<'M'>(r, q, c);
             if (pat[j] == 'R') mix_op<'R'>(r, q, c);
+            if (pat[j] == 'f') mix_op<'f'>(r, q, c);
+            if (pat[j] == 'x') mix_op<'x'>(r, q, c);
+            if (pat[j] == 'X') mix_op<'X'>(r, q, c);
+            if (pat[j] == 'n') mix_op<'n'>(r, q, c);
         }
     }
 }
@@ -149,6 +159,11 @@ __device__ __forceinline__ void mix_kind(uint32_t (&r)[16], uint64_t (&q)[8]) {
     MIXK(117, 'H','H','H','H','H','H','H','H','H','H','H','H','H','H','H','F')
     MIXK(118, 'R','F','R','F','R','F','R','F','R','F','R','F','R','F','R','F')
     MIXK(119, 'L','L','L','L','F','F','F','F','M','M','F','F','S','S','S','S')
+    MIXK(120, 'H','f','H','f','H','f','H','f','H','f','H','f','H','f','H','f')
+    MIXK(121, 'f','f','f','f','f','f','f','f','f','f','f','f','f','f','f','f')
+    MIXK(122, 'H','x','H','x','H','x','H','x','H','x','H','x','H','x','H','x')
+    MIXK(123, 'H','X','H','X','H','X','H','X','H','X','H','X','H','X','H','X')
+    MIXK(124, 'H','n','H','n','H','n','H','n','H','n','H','n','H','n','H','n')
 }
 
 // Explicit-register variants (VGPR bank hypothesis): v40..v63 written / read by hand.
@@ -337,7 +352,16 @@ __device__ __forceinline__ void b3_var(uint32_t (*st)[16], const uint32_t (&m)[1
 #define A_ADD3(d, x, y, z) asm volatile("v_add3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(x), "v"(y), "v"(z))
 #define A_XOR(d, x, y) asm volatile("v_xor_b32 %0, %1, %2" : "=v"(d) : "v"(x), "v"(y))
 #define A_ROT(d, x, n) asm volatile("v_alignbit_b32 %0, %1, %1, " #n : "=v"(d) : "v"(x))
-template <bool SPLIT, int NS>
+// early-clobber forms: the destination register differs from every source (kinds 109, 125-126)
+#define E_ADD(d, x, y) asm volatile("v_add_u32 %0, %1, %2" : "=&v"(d) : "v"(x), "v"(y))
+#define E_ADD3(d, x, y, z) asm volatile("v_add3_u32 %0, %1, %2, %3" : "=&v"(d) : "v"(x), "v"(y), "v"(z))
+#define E_XOR(d, x, y) asm volatile("v_xor_b32 %0, %1, %2" : "=&v"(d) : "v"(x), "v"(y))
+#define E_ROT(d, x, n) asm volatile("v_alignbit_b32 %0, %1, %1, " #n : "=&v"(d) : "v"(x))
+#define F_ADD(...) do { if constexpr (FRESH >= 1) E_ADD(__VA_ARGS__); else A_ADD(__VA_ARGS__); } while (0)
+#define F_XOR(...) do { if constexpr (FRESH >= 1) E_XOR(__VA_ARGS__); else A_XOR(__VA_ARGS__); } while (0)
+#define H_ADD3(...) do { if constexpr (FRESH >= 2) E_ADD3(__VA_ARGS__); else A_ADD3(__VA_ARGS__); } while (0)
+#define H_ROT(d, x, n) do { if constexpr (FRESH >= 2) E_ROT(d, x, n); else A_ROT(d, x, n); } while (0)
+template <bool SPLIT, int NS, int FRESH = 0>
 __device__ __forceinline__ void g4p(uint32_t (*st)[16], const uint32_t (&m)[16], const int (&ix)[4][4], int mo) {
     // a += b + m0
 #pragma unroll
@@ -345,78 +369,78 @@ __device__ __forceinline__ void g4p(uint32_t (*st)[16], const uint32_t (&m)[16],
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             uint32_t &a = st[s][ix[j][0]];
-            if constexpr (SPLIT) A_ADD(a, a, st[s][ix[j][1]]);
-            else A_ADD3(a, a, st[s][ix[j][1]], m[(mo + 2 * j) & 15]);
+            if constexpr (SPLIT) F_ADD(a, a, st[s][ix[j][1]]);
+            else H_ADD3(a, a, st[s][ix[j][1]], m[(mo + 2 * j) & 15]);
         }
     if constexpr (SPLIT) {
 #pragma unroll
         for (int s = 0; s < NS; ++s)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) A_ADD(st[s][ix[j][0]], st[s][ix[j][0]], m[(mo + 2 * j) & 15]);
+            for (int j = 0; j < 4; ++j) F_ADD(st[s][ix[j][0]], st[s][ix[j][0]], m[(mo + 2 * j) & 15]);
     }
 #pragma unroll
     for (int s = 0; s < NS; ++s)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) A_XOR(st[s][ix[j][3]], st[s][ix[j][3]], st[s][ix[j][0]]);
+        for (int j = 0; j < 4; ++j) F_XOR(st[s][ix[j][3]], st[s][ix[j][3]], st[s][ix[j][0]]);
 #pragma unroll
     for (int s = 0; s < NS; ++s)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) A_ROT(st[s][ix[j][3]], st[s][ix[j][3]], 16);
+        for (int j = 0; j < 4; ++j) H_ROT(st[s][ix[j][3]], st[s][ix[j][3]], 16);
 #pragma unroll
     for (int s = 0; s < NS; ++s)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) A_ADD(st[s][ix[j][2]], st[s][ix[j][2]], st[s][ix[j][3]]);
+        for (int j = 0; j < 4; ++j) F_ADD(st[s][ix[j][2]], st[s][ix[j][2]], st[s][ix[j][3]]);
 #pragma unroll
     for (int s = 0; s < NS; ++s)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) A_XOR(st[s][ix[j][1]], st[s][ix[j][1]], st[s][ix[j][2]]);
+        for (int j = 0; j < 4; ++j) F_XOR(st[s][ix[j][1]], st[s][ix[j][1]], st[s][ix[j][2]]);
 #pragma unroll
     for (int s = 0; s < NS; ++s)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) A_ROT(st[s][ix[j][1]], st[s][ix[j][1]], 12);
+        for (int j = 0; j < 4; ++j) H_ROT(st[s][ix[j][1]], st[s][ix[j][1]], 12);
 #pragma unroll
     for (int s = 0; s < NS; ++s)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             uint32_t &a = st[s][ix[j][0]];
-            if constexpr (SPLIT) A_ADD(a, a, st[s][ix[j][1]]);
-            else A_ADD3(a, a, st[s][ix[j][1]], m[(mo + 2 * j + 1) & 15]);
+            if constexpr (SPLIT) F_ADD(a, a, st[s][ix[j][1]]);
+            else H_ADD3(a, a, st[s][ix[j][1]], m[(mo + 2 * j + 1) & 15]);
         }
     if constexpr (SPLIT) {
 #pragma unroll
         for (int s = 0; s < NS; ++s)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) A_ADD(st[s][ix[j][0]], st[s][ix[j][0]], m[(mo + 2 * j + 1) & 15]);
+            for (int j = 0; j < 4; ++j) F_ADD(st[s][ix[j][0]], st[s][ix[j][0]], m[(mo + 2 * j + 1) & 15]);
     }
 #pragma unroll
     for (int s = 0; s < NS; ++s)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) A_XOR(st[s][ix[j][3]], st[s][ix[j][3]], st[s][ix[j][0]]);
+        for (int j = 0; j < 4; ++j) F_XOR(st[s][ix[j][3]], st[s][ix[j][3]], st[s][ix[j][0]]);
 #pragma unroll
     for (int s = 0; s < NS; ++s)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) A_ROT(st[s][ix[j][3]], st[s][ix[j][3]], 8);
+        for (int j = 0; j < 4; ++j) H_ROT(st[s][ix[j][3]], st[s][ix[j][3]], 8);
 #pragma unroll
     for (int s = 0; s < NS; ++s)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) A_ADD(st[s][ix[j][2]], st[s][ix[j][2]], st[s][ix[j][3]]);
+        for (int j = 0; j < 4; ++j) F_ADD(st[s][ix[j][2]], st[s][ix[j][2]], st[s][ix[j][3]]);
 #pragma unroll
     for (int s = 0; s < NS; ++s)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) A_XOR(st[s][ix[j][1]], st[s][ix[j][1]], st[s][ix[j][2]]);
+        for (int j = 0; j < 4; ++j) F_XOR(st[s][ix[j][1]], st[s][ix[j][1]], st[s][ix[j][2]]);
 #pragma unroll
     for (int s = 0; s < NS; ++s)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) A_ROT(st[s][ix[j][1]], st[s][ix[j][1]], 7);
+        for (int j = 0; j < 4; ++j) H_ROT(st[s][ix[j][1]], st[s][ix[j][1]], 7);
 }
-template <bool SPLIT, int NS>
+template <bool SPLIT, int NS, int FRESH = 0>
 __device__ __forceinline__ void b3_pinned(uint32_t (*st)[16], const uint32_t (&m)[16]) {
     constexpr int col[4][4] = {{0, 4, 8, 12}, {1, 5, 9, 13}, {2, 6, 10, 14}, {3, 7, 11, 15}};
     constexpr int dia[4][4] = {{0, 5, 10, 15}, {1, 6, 11, 12}, {2, 7, 8, 13}, {3, 4, 9, 14}};
 #pragma unroll
     for (int rr = 0; rr < 7; ++rr) {
-        g4p<SPLIT, NS>(st, m, col, 0);
-        g4p<SPLIT, NS>(st, m, dia, 8);
+        g4p<SPLIT, NS, FRESH>(st, m, col, 0);
+        g4p<SPLIT, NS, FRESH>(st, m, dia, 8);
     }
 }
 
@@ -448,7 +472,7 @@ __global__ __launch_bounds__(256) void k_issue(uint32_t iters, uint32_t *out, un
         for (int i = 0; i < 16; ++i) x ^= r[i] ^ __float_as_uint(f[i]);
 #pragma unroll
         for (int i = 0; i < 8; ++i) x ^= (uint32_t)q[i] ^ (uint32_t)(q[i] >> 32);
-    } else if constexpr (K >= 110) {
+    } else if constexpr (K >= 110 && K < 125) {
         uint32_t r[16];
         uint64_t q[8];
 #pragma unroll
@@ -470,8 +494,9 @@ __global__ __launch_bounds__(256) void k_issue(uint32_t iters, uint32_t *out, un
         for (uint32_t it = 0; it < iters; ++it) body_x<K>();
         t1 = __builtin_amdgcn_s_memtime();
         rt1 = __builtin_amdgcn_s_memrealtime();
-    } else if constexpr (K >= 104 && K <= 106) {
-        constexpr int NS = K == 105 ? 1 : 2;
+    } else if constexpr ((K >= 104 && K <= 106) || K == 109 || K == 125 || K == 126) {
+        constexpr int NS = K == 105 || K == 125 || K == 126 ? 1 : 2;
+        constexpr int FRESH = K == 109 || K == 125 ? 1 : K == 126 ? 2 : 0;
         uint32_t st[NS][16], m[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -481,7 +506,7 @@ __global__ __launch_bounds__(256) void k_issue(uint32_t iters, uint32_t *out, un
         }
         t0 = __builtin_amdgcn_s_memtime();
         rt0 = __builtin_amdgcn_s_memrealtime();
-        for (uint32_t it = 0; it < iters; ++it) b3_pinned<K != 106, NS>(st, m);
+        for (uint32_t it = 0; it < iters; ++it) b3_pinned<K != 106 && K < 109, NS, FRESH>(st, m);
         t1 = __builtin_amdgcn_s_memtime();
         rt1 = __builtin_amdgcn_s_memrealtime();
 #pragma unroll
@@ -612,6 +637,9 @@ static const char *kind_name(int k) {
     case 105: return "BLAKE3 pinned order, one compression + add3 split: F runs of 8-12 (784 VALU)";
     case 106: return "BLAKE3 pinned order, two interleaved, add3 kept (1344 VALU)";
     case 107: return "BLAKE3 kind 102 + s_nop 0 between op groups (1344 VALU)";
+    case 109: return "BLAKE3 kind 106 with fresh destinations for v_add_u32 / v_xor_b32 (1344 VALU)";
+    case 125: return "BLAKE3 pinned, one compression, add3 kept, fresh F destinations (672 VALU)";
+    case 126: return "BLAKE3 pinned, one compression, add3 kept, every destination fresh (672 VALU)";
     case 108: return "BLAKE3 kind 102 + sched_barrier between op groups (1344 VALU)";
     case 110: return "mix HF HF (add3 / add alternating)";
     case 111: return "mix 8H 8F";
@@ -623,6 +651,11 @@ static const char *kind_name(int k) {
     case 117: return "mix 15H 1F";
     case 118: return "mix RF (lshrrev / add)";
     case 119: return "mix scan-like 4L 4F 2M 2F 4S";
+    case 120: return "mix H f (f = v_add_u32 vD, vS, vD: accumulator as src1)";
+    case 121: return "all f (v_add_u32 vD, vS, vD)";
+    case 122: return "mix H x (x = v_xor_b32 vD, vS, vD)";
+    case 123: return "mix H X (X = v_xor_b32 vD, vD, vS)";
+    case 124: return "mix H n (n = v_add_u32 vD, vS, vT, fresh destination)";
     default: return "?";
     }
 }
@@ -636,9 +669,9 @@ int main(int argc, char **argv) {
     reg<32>(ks); reg<33>(ks); reg<34>(ks); reg<35>(ks); reg<36>(ks); reg<37>(ks); reg<38>(ks); reg<39>(ks);
     reg<40>(ks); reg<41>(ks); reg<42>(ks); reg<43>(ks); reg<44>(ks); reg<45>(ks); reg<46>(ks); reg<47>(ks);
     reg<60>(ks); reg<61>(ks); reg<62>(ks); reg<63>(ks); reg<64>(ks); reg<65>(ks); reg<66>(ks); reg<67>(ks);
-    reg<68>(ks); reg<100>(ks); reg<101>(ks); reg<102>(ks); reg<103>(ks); reg<104>(ks); reg<105>(ks); reg<106>(ks); reg<107>(ks); reg<108>(ks);
+    reg<68>(ks); reg<100>(ks); reg<101>(ks); reg<102>(ks); reg<103>(ks); reg<104>(ks); reg<105>(ks); reg<106>(ks); reg<107>(ks); reg<108>(ks); reg<109>(ks); reg<125>(ks); reg<126>(ks);
     reg<110>(ks); reg<111>(ks); reg<112>(ks); reg<113>(ks); reg<114>(ks); reg<115>(ks); reg<116>(ks);
-    reg<117>(ks); reg<118>(ks); reg<119>(ks);
+    reg<117>(ks); reg<118>(ks); reg<119>(ks); reg<120>(ks); reg<121>(ks); reg<122>(ks); reg<123>(ks); reg<124>(ks);
     std::vector<int> want;
     if (argc > 1) {
         char *s = strdup(argv[1]);
@@ -661,7 +694,8 @@ int main(int argc, char **argv) {
     for (auto &kf : ks) {
         if (!want.empty() && std::find(want.begin(), want.end(), kf.first) == want.end()) continue;
         const int K = kf.first;
-        const uint32_t per_iter = K == 100 ? 672u : K == 101 || K == 105 ? 784u : K == 102 || K == 106 || K == 107 || K == 108 ? 1344u
+        const uint32_t per_iter = K == 100 || K == 125 || K == 126 ? 672u : K == 101 || K == 105 ? 784u
+                                : K == 102 || K == 106 || K == 107 || K == 108 || K == 109 ? 1344u
                                 : K == 103 || K == 104 ? 1568u : 256u;
         CHK(hipFuncSetAttribute((const void *)kf.second, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max));
         printf("%s{\"kind\": %d, \"name\": \"%s\"", first ? "" : ",\n", K, kind_name(K));
