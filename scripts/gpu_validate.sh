@@ -27,7 +27,7 @@ for s in $STEPS; do
          tail -1 ${o}_pytest_slow.log ;;
   smoke) timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > ${o}_smoke.log 2>&1 || fail smoke ${o}_smoke.log
          tail -2 ${o}_smoke.log ;;
-  bench) timeout -k 10 600 python bench.py > ${o}_bench_c2.json 2> ${o}_bench_c2.err || fail bench ${o}_bench_c2.err
+  bench) timeout -k 10 600 python bench.py --steps 20 --warmup 5 > ${o}_bench_c2.json 2> ${o}_bench_c2.err || fail bench ${o}_bench_c2.err
          cut -c1-300 ${o}_bench_c2.json ;;
   configs)
          for c in c3 c4 c5; do
