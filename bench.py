@@ -93,6 +93,8 @@ def parse_args():
     ap.add_argument("--bound-priority", action="store_true",
                     help="boundary stages of overlapped batches on a highest-priority stream "
                          "(CHUNKER_AMD_BOUND_PRIORITY=1; A/B)")
+    ap.add_argument("--bound-cus", type=int, default=0,
+                    help="overlapped batches' library stream restricted to N CUs (CHUNKER_AMD_BOUND_CUS; A/B)")
     ap.add_argument("--no-coalesce", action="store_true",
                     help="concurrent callers digest their batches alone (cg_test_coalesce(0)); A/B of the coalescer")
     ap.add_argument("--dist-force", action="store_true",
@@ -131,6 +133,8 @@ def main():
         os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     if args.bound_priority:
         os.environ["CHUNKER_AMD_BOUND_PRIORITY"] = "1"
+    if args.bound_cus:
+        os.environ["CHUNKER_AMD_BOUND_CUS"] = str(args.bound_cus)
 
     import torch
     import torch.distributed as dist

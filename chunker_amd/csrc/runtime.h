@@ -123,11 +123,12 @@ struct Workspace {
     // end of a launched batch: its wait syncs this event, not the stream (a batch queued
     // behind it on the same stream must not be waited for too)
     hipEvent_t ev_done = nullptr;
-    // Boundary stages of a batch queued with an inputs-ready event
-    // (cg_chunk_batch_device_async_after): they run on bound_stream, ordered after that
-    // event only, so they overlap the digest of the batch queued before on the caller's
-    // stream; ev_bdone (recorded on bound_stream after the assembly) holds the digest back,
-    // ev_dstart (on the caller's stream after that wait) opens the digest stage's timing.
+    // A SHA-256 batch queued with an inputs-ready event (cg_chunk_batch_device_async_after)
+    // runs on bound_stream, ordered after that event only, beside the batch queued before
+    // it on the caller's stream, which then waits for its done event.  Split mode 1 (A/B):
+    // only the boundary stages run there; ev_bdone (recorded after the assembly) holds the
+    // digest on the caller's stream back, and ev_dstart (after that wait) opens the digest
+    // stage's timing.
     hipStream_t bound_stream = nullptr;
     hipEvent_t ev_bdone = nullptr, ev_dstart = nullptr;
     // Streams map onto the process's few hardware queues (GPU_MAX_HW_QUEUES, 4 by default)

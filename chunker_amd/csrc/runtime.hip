@@ -618,13 +618,27 @@ int ensure_pass_buffers(Workspace *ws, uint64_t total_len, size_t n_nars, uint64
 // The boundary stages' stream of a split batch.  CHUNKER_AMD_BOUND_PRIORITY=1 (read once)
 // creates it at the device's highest stream priority, so its workgroups are dispatched ahead
 // of the digest's as CU slots free up (A/B: a chip-filling digest leaves the scan few slots).
+// CHUNKER_AMD_BOUND_CUS=N (A/B, read once) restricts it to N of the device's CUs spread
+// over the XCDs (every (CUs / N)-th CU), leaving the others to the digest it runs beside.
 int Workspace::ensure_bound_stream() {
     if (bound_stream) return CG_OK;
     static const bool high = [] {
         const char *e = getenv("CHUNKER_AMD_BOUND_PRIORITY");
         return e && e[0] == '1';
     }();
-    if (high) {
+    static const int cus = [] {
+        const char *e = getenv("CHUNKER_AMD_BOUND_CUS");
+        return e ? atoi(e) : 0;
+    }();
+    if (cus > 0) {
+        hipDeviceProp_t prop;
+        HIP_TRY(hipGetDeviceProperties(&prop, device));
+        const int total = prop.multiProcessorCount;
+        const int stride = std::max(1, total / std::min(cus, total));
+        std::vector<uint32_t> mask((total + 31) / 32, 0u);
+        for (int c = 0, n = 0; c < total && n < cus; c += stride, ++n) mask[c / 32] |= 1u << (c % 32);
+        HIP_TRY(hipExtStreamCreateWithCUMask(&bound_stream, (uint32_t)mask.size(), mask.data()));
+    } else if (high) {
         int least = 0, greatest = 0;
         HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
         HIP_TRY(hipStreamCreateWithPriority(&bound_stream, hipStreamNonBlocking, greatest));
@@ -789,9 +803,9 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
     if ((rc = ensure_gear(ws, *tab))) return rc;
     if ((rc = ensure_pass_buffers(ws, total_len, n_nars, total_cap, chunk_bound, slots, algo))) return rc;
     // The boundary stages' stream: `st` itself, or -- with an inputs-ready event -- the
-    // workspace's bound_stream, ordered after that event only, so the stages run under the
-    // digest of the batch queued before on `st` (which reads another workspace); the digest
-    // waits for them below.
+    // workspace's bound_stream, ordered after that event only, so the stages (and, in split
+    // mode 2, the digest: `ds` below) run beside the digest of the batch queued before on
+    // `st`, which reads another workspace.
     // (BLAKE3 batches stay in stream order: their digest fills the chip by itself, and
     // overlapping it with the next batch measured 1.7 % slower on config 3,
     // profiles/r05_v3_split_ab.txt; waiting for more than inputs_ready is always allowed)

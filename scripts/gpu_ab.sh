@@ -6,7 +6,8 @@
 #   VARIANTS="prod NAME" CONFIGS="c2 c4" ROUNDS=3 TAG=r04_x bash scripts/gpu_ab.sh
 # Environment:
 #   VARIANTS   product = "prod", others = library names under chunker_amd/_ab (required);
-#              "+FLAG" = the product library with bench.py flag FLAG (e.g. "+--no-overlap")
+#              "+FLAG[,FLAG...]" = the product library with those bench.py flags
+#              (e.g. "+--no-overlap", "+--split-mode=1,--bound-cus=32")
 #   CONFIGS    bench.py configs to alternate (default "c2")
 #   ROUNDS     alternating rounds (default 3)
 #   STEPS      bench.py --steps (default 8)
@@ -26,7 +27,7 @@ STEPS=${STEPS:-8}
 TAG=${TAG:-ab}
 TESTS=${TESTS:-"tests/test_gpu_parity.py tests/test_gpu_configs.py tests/test_gpu_fuzz.py"}
 lib_of() { case "$1" in prod|+*) echo "" ;; *) echo "chunker_amd/_ab/libchunker_amd_$1.so" ;; esac; }
-flag_of() { case "$1" in +*) echo "${1#+}" ;; *) echo "" ;; esac; }
+flag_of() { case "$1" in +*) echo "${1#+}" | tr ',' ' ' ;; *) echo "" ;; esac; }
 if [ "$TESTS" != none ]; then
   for v in $VARIANTS; do
     case "$v" in prod|+*) continue ;; esac
