@@ -1,5 +1,2 @@
 cd "${GRAFT_REPO_ROOT:-.}"; export TMPDIR=/tmp; mkdir -p gpurun_out
-T=r05_v11
-CONFIGS="c4" TAG=${T}_prod bash scripts/gpu_pmc_all.sh || exit 1
-CHUNKER_AMD_LIB=chunker_amd/_ab/libchunker_amd_inplace.so CONFIGS="c2 c4" TAG=${T}_inplace bash scripts/gpu_pmc_all.sh || exit 1
-echo done
+VARIANTS="prod +--split-mode=1,--bound-cus=32 +--split-mode=1,--bound-cus=64 +--split-mode=1" CONFIGS="c4 c5" ROUNDS=2 STEPS=10 TESTS=none TAG=r05_v12 bash scripts/gpu_ab.sh || exit 1
