@@ -553,7 +553,56 @@ def e2e_rates(ca, torch, args, n_per, nar_bytes, params, algo, want):
             assert n == len(want) and np.array_equal(out[:n].view(np.uint8), want.view(np.uint8)), \
                 f"e2e batch {k}: descriptors differ from the device-resident run"
         res[f"K{K}"] = round(K * reps * nbytes / dt / GIB, 3)
+    if algo == 1:
+        res["one_caller_overlapped"] = e2e_one_caller(ca, torch, bufs, offs, nbytes, cap, n_per, params, algo, want)
     return res
+
+
+def e2e_one_caller(ca, torch, bufs, offs, nbytes, cap, n_per, params, algo, want, reps=8):
+    """Host to host from ONE caller thread with two batches in flight: batch k's pinned H2D
+    copy runs on a copy stream, its inputs-ready event orders the batch
+    (cg_chunk_batch_device_async_after), so the copy and the batch overlap the previous
+    batch's digest; the descriptors come back D2H after its wait.  Two device input and
+    output buffers alternate; batch k + 2 is issued only after batch k was waited for and
+    its descriptors copied out.  GiB/s = reps x batch bytes / wall time."""
+    host = bufs[0][0]
+    dins = [torch.empty(nbytes + 256, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    douts = [torch.empty(cap * 48, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    outs = [np.zeros(cap * 48, np.uint8) for _ in range(2)]
+    copy = torch.cuda.Stream()
+    bstream = torch.cuda.Stream()
+
+    def issue(k):
+        j = k % 2
+        with torch.cuda.stream(copy):
+            dins[j][:nbytes].copy_(host, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        return ca.chunk_batch_device_async(dins[j].data_ptr(), offs, douts[j].data_ptr(), cap, *params, hash=algo,
+                                           stream=bstream.cuda_stream, inputs_ready=ev.cuda_event), ev
+
+    def complete(k, h):
+        first = h[0].wait()
+        n = int(first[-1])
+        j = k % 2
+        outs[j][: n * 48] = douts[j][: n * 48].cpu().numpy()
+        return n
+
+    for timed in (False, True):
+        count = reps if timed else 2
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        pending = issue(0)
+        for k in range(count):
+            nxt = issue(k + 1) if k + 1 < count else None
+            n = complete(k, pending)
+            pending = nxt
+        dt = time.perf_counter() - t0
+    assert n == len(want) and np.array_equal(outs[(count - 1) % 2][: n * 48], want.view(np.uint8)), \
+        "e2e one caller: descriptors differ from the device-resident run"
+    return {"GiBps": round(reps * nbytes / dt / GIB, 3), "reps": reps,
+            "shape": "one thread, two batches in flight: pinned H2D on a copy stream -> inputs-ready event -> "
+                     "cg_chunk_batch_device_async_after -> wait -> descriptors D2H"}
 
 
 def drop_in_rates(ca, args):
