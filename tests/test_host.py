@@ -73,3 +73,18 @@ def test_blocking_adapter_reads_through_private_loop():
     r = R()
     a = chunking.BlockingAsyncReadAdapter(r)
     assert a.read(1) == b"a" and a.read(5) == b"ab" and r.n == 2
+
+
+def test_bench_cli_contract():
+    """bench.py's command line (the driver's `--gpus N --steps K --warmup W`, the A/B flags
+    the round-5 measurements use) parses without touching a GPU, and the help lists them."""
+    import subprocess
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parent.parent
+    r = subprocess.run([sys.executable, str(root / "bench.py"), "--help"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    for flag in ("--gpus", "--steps", "--warmup", "--config", "--no-overlap", "--split-mode", "--drop-in",
+                 "--drop-in-sizes", "--no-coalesce", "--dist-force"):
+        assert flag in r.stdout, flag
