@@ -137,6 +137,39 @@ __device__ __forceinline__ uint32_t rotr32b(uint32_t x, uint32_t n) { return __b
         B3P_ROT(v[b3], v[b3], 7);                                                                                   \
     }
 
+// CG_B3_PINNED=2: each G4 step (48 ops, the order above) as ONE asm statement.  The compiler
+// pads between inline-asm statements with an s_nop (its hazard model cannot see inside
+// them): one per op group with per-op statements (~170 per compression, an issue slot
+// each), one per step here.
+#define B3A_BODY(R1, R2)                                                                                            \
+    "v_add3_u32 %[a0], %[a0], %[b0], %[x0]\n v_add3_u32 %[a1], %[a1], %[b1], %[x1]\n"                            \
+    " v_add3_u32 %[a2], %[a2], %[b2], %[x2]\n v_add3_u32 %[a3], %[a3], %[b3], %[x3]\n"                           \
+    " v_xor_b32 %[d0], %[d0], %[a0]\n v_xor_b32 %[d1], %[d1], %[a1]\n"                                           \
+    " v_xor_b32 %[d2], %[d2], %[a2]\n v_xor_b32 %[d3], %[d3], %[a3]\n"                                           \
+    " v_alignbit_b32 %[d0], %[d0], %[d0], " R1 "\n v_alignbit_b32 %[d1], %[d1], %[d1], " R1 "\n"                 \
+    " v_alignbit_b32 %[d2], %[d2], %[d2], " R1 "\n v_alignbit_b32 %[d3], %[d3], %[d3], " R1 "\n"                 \
+    " v_add_u32 %[c0], %[c0], %[d0]\n v_add_u32 %[c1], %[c1], %[d1]\n"                                           \
+    " v_add_u32 %[c2], %[c2], %[d2]\n v_add_u32 %[c3], %[c3], %[d3]\n"                                           \
+    " v_xor_b32 %[b0], %[b0], %[c0]\n v_xor_b32 %[b1], %[b1], %[c1]\n"                                           \
+    " v_xor_b32 %[b2], %[b2], %[c2]\n v_xor_b32 %[b3], %[b3], %[c3]\n"                                           \
+    " v_alignbit_b32 %[b0], %[b0], %[b0], " R2 "\n v_alignbit_b32 %[b1], %[b1], %[b1], " R2 "\n"                 \
+    " v_alignbit_b32 %[b2], %[b2], %[b2], " R2 "\n v_alignbit_b32 %[b3], %[b3], %[b3], " R2 "\n"
+#define B3_G4A(A0, B0, C0, D0, A1, B1, C1, D1, A2, B2, C2, D2, A3, B3, C3, D3, MI)                                  \
+    {                                                                                                               \
+        asm volatile(B3A_BODY("16", "12")                                                                          \
+                     : [a0] "+v"(v[A0]), [b0] "+v"(v[B0]), [c0] "+v"(v[C0]), [d0] "+v"(v[D0]), [a1] "+v"(v[A1]), \
+                       [b1] "+v"(v[B1]), [c1] "+v"(v[C1]), [d1] "+v"(v[D1]), [a2] "+v"(v[A2]), [b2] "+v"(v[B2]), \
+                       [c2] "+v"(v[C2]), [d2] "+v"(v[D2]), [a3] "+v"(v[A3]), [b3] "+v"(v[B3]), [c3] "+v"(v[C3]), \
+                       [d3] "+v"(v[D3])                                                                          \
+                     : [x0] "v"(m[MI[0]]), [x1] "v"(m[MI[2]]), [x2] "v"(m[MI[4]]), [x3] "v"(m[MI[6]]));         \
+        asm volatile(B3A_BODY("8", "7")                                                                            \
+                     : [a0] "+v"(v[A0]), [b0] "+v"(v[B0]), [c0] "+v"(v[C0]), [d0] "+v"(v[D0]), [a1] "+v"(v[A1]), \
+                       [b1] "+v"(v[B1]), [c1] "+v"(v[C1]), [d1] "+v"(v[D1]), [a2] "+v"(v[A2]), [b2] "+v"(v[B2]), \
+                       [c2] "+v"(v[C2]), [d2] "+v"(v[D2]), [a3] "+v"(v[A3]), [b3] "+v"(v[B3]), [c3] "+v"(v[C3]), \
+                       [d3] "+v"(v[D3])                                                                          \
+                     : [x0] "v"(m[MI[1]]), [x1] "v"(m[MI[3]]), [x2] "v"(m[MI[5]]), [x3] "v"(m[MI[7]]));         \
+    }
+
 // Compress one block; returns the new chaining value in cv (first 8 output words).
 __device__ __forceinline__ void b3_compress(uint32_t cv[8], const uint32_t m[16], uint64_t counter, uint32_t blen,
                                             uint32_t flags) {
@@ -145,7 +178,10 @@ __device__ __forceinline__ void b3_compress(uint32_t cv[8], const uint32_t m[16]
                       blen, flags};
 #pragma unroll
     for (int r = 0; r < 7; ++r) {
-#if CG_B3_PINNED
+#if CG_B3_PINNED == 2
+        B3_G4A(0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14, 3, 7, 11, 15, B3S.s[r]);
+        B3_G4A(0, 5, 10, 15, 1, 6, 11, 12, 2, 7, 8, 13, 3, 4, 9, 14, (B3S.s[r] + 8));
+#elif CG_B3_PINNED
         B3_G4P(0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14, 3, 7, 11, 15, B3S.s[r]);
         B3_G4P(0, 5, 10, 15, 1, 6, 11, 12, 2, 7, 8, 13, 3, 4, 9, 14, (B3S.s[r] + 8));
 #else

@@ -1,3 +1,10 @@
 cd "${GRAFT_REPO_ROOT:-.}"; export TMPDIR=/tmp; mkdir -p gpurun_out
-timeout -k 10 400 python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --concurrent '' --e2e 1,8,16 --drop-in '' --no-clock > gpurun_out/r05_v13_e2e.json 2> gpurun_out/r05_v13_e2e.err || { tail -20 gpurun_out/r05_v13_e2e.err; exit 1; }
-python3 -c "import json; d=json.loads(open('gpurun_out/r05_v13_e2e.json').read().strip().splitlines()[-1]); print(d['value'], json.dumps(d['concurrent']))"
+KINDS=100,125,127 PMC_KINDS=100,125,127 TAG=r05_v14_dual bash scripts/micro/dual_issue.sh || exit 1
+python3 -c "
+import json
+d=json.load(open('gpurun_out/r05_v14_dual_issue_b3.json'))
+for r in d['rows']: print(r['kind'], {k:v['cyc'] for k,v in r.items() if k.startswith('w')})
+d=json.load(open('gpurun_out/r05_v14_dual_dual_b3.json'))
+for r in d['rows']: print(r['kernel'][:20], r['w'], r['dual_frac'])
+"
+VARIANTS="prod b3asm" CONFIGS="c3" ROUNDS=3 STEPS=20 TESTS="tests/test_gpu_parity.py" TAG=r05_v14_b3 bash scripts/gpu_ab.sh || exit 1

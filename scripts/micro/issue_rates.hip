@@ -444,6 +444,45 @@ __device__ __forceinline__ void b3_pinned(uint32_t (*st)[16], const uint32_t (&m
     }
 }
 
+// Kind 127: each G4 step (48 ops) as ONE asm statement: the compiler pads between asm
+// statements with s_nop (its hazard model cannot see inside them), so per-op statements
+// (kinds 104-126) carry ~1 s_nop per op group; one statement per step carries 1 per 48 ops.
+#define G4ASM_BODY(M0, M1, M2, M3, R) \
+    "v_add3_u32 %[a0], %[a0], %[b0], %[" M0 "0]\n v_add3_u32 %[a1], %[a1], %[b1], %[" M0 "1]\n" \
+    " v_add3_u32 %[a2], %[a2], %[b2], %[" M0 "2]\n v_add3_u32 %[a3], %[a3], %[b3], %[" M0 "3]\n" \
+    " v_xor_b32 %[d0], %[d0], %[a0]\n v_xor_b32 %[d1], %[d1], %[a1]\n v_xor_b32 %[d2], %[d2], %[a2]\n v_xor_b32 %[d3], %[d3], %[a3]\n" \
+    " v_alignbit_b32 %[d0], %[d0], %[d0], " M1 "\n v_alignbit_b32 %[d1], %[d1], %[d1], " M1 "\n" \
+    " v_alignbit_b32 %[d2], %[d2], %[d2], " M1 "\n v_alignbit_b32 %[d3], %[d3], %[d3], " M1 "\n" \
+    " v_add_u32 %[c0], %[c0], %[d0]\n v_add_u32 %[c1], %[c1], %[d1]\n v_add_u32 %[c2], %[c2], %[d2]\n v_add_u32 %[c3], %[c3], %[d3]\n" \
+    " v_xor_b32 %[b0], %[b0], %[c0]\n v_xor_b32 %[b1], %[b1], %[c1]\n v_xor_b32 %[b2], %[b2], %[c2]\n v_xor_b32 %[b3], %[b3], %[c3]\n" \
+    " v_alignbit_b32 %[b0], %[b0], %[b0], " M2 "\n v_alignbit_b32 %[b1], %[b1], %[b1], " M2 "\n" \
+    " v_alignbit_b32 %[b2], %[b2], %[b2], " M2 "\n v_alignbit_b32 %[b3], %[b3], %[b3], " M2 "\n" \
+    " v_add3_u32 %[a0], %[a0], %[b0], %[" M3 "0]\n v_add3_u32 %[a1], %[a1], %[b1], %[" M3 "1]\n" \
+    " v_add3_u32 %[a2], %[a2], %[b2], %[" M3 "2]\n v_add3_u32 %[a3], %[a3], %[b3], %[" M3 "3]\n" \
+    " v_xor_b32 %[d0], %[d0], %[a0]\n v_xor_b32 %[d1], %[d1], %[a1]\n v_xor_b32 %[d2], %[d2], %[a2]\n v_xor_b32 %[d3], %[d3], %[a3]\n" \
+    " v_alignbit_b32 %[d0], %[d0], %[d0], 8\n v_alignbit_b32 %[d1], %[d1], %[d1], 8\n" \
+    " v_alignbit_b32 %[d2], %[d2], %[d2], 8\n v_alignbit_b32 %[d3], %[d3], %[d3], 8\n" \
+    " v_add_u32 %[c0], %[c0], %[d0]\n v_add_u32 %[c1], %[c1], %[d1]\n v_add_u32 %[c2], %[c2], %[d2]\n v_add_u32 %[c3], %[c3], %[d3]\n" \
+    " v_xor_b32 %[b0], %[b0], %[c0]\n v_xor_b32 %[b1], %[b1], %[c1]\n v_xor_b32 %[b2], %[b2], %[c2]\n v_xor_b32 %[b3], %[b3], %[c3]\n" \
+    " v_alignbit_b32 %[b0], %[b0], %[b0], " R "\n v_alignbit_b32 %[b1], %[b1], %[b1], " R "\n" \
+    " v_alignbit_b32 %[b2], %[b2], %[b2], " R "\n v_alignbit_b32 %[b3], %[b3], %[b3], " R
+#define G4ASM(A0, B0, C0, D0, A1, B1, C1, D1, A2, B2, C2, D2, A3, B3, C3, D3, MO)                                 \
+    asm volatile(G4ASM_BODY("x", "16", "12", "y", "7")                                                          \
+                 : [a0] "+v"(v[A0]), [b0] "+v"(v[B0]), [c0] "+v"(v[C0]), [d0] "+v"(v[D0]), [a1] "+v"(v[A1]),     \
+                   [b1] "+v"(v[B1]), [c1] "+v"(v[C1]), [d1] "+v"(v[D1]), [a2] "+v"(v[A2]), [b2] "+v"(v[B2]),     \
+                   [c2] "+v"(v[C2]), [d2] "+v"(v[D2]), [a3] "+v"(v[A3]), [b3] "+v"(v[B3]), [c3] "+v"(v[C3]),     \
+                   [d3] "+v"(v[D3])                                                                              \
+                 : [x0] "v"(m[(MO) & 15]), [x1] "v"(m[((MO) + 2) & 15]), [x2] "v"(m[((MO) + 4) & 15]),          \
+                   [x3] "v"(m[((MO) + 6) & 15]), [y0] "v"(m[((MO) + 1) & 15]), [y1] "v"(m[((MO) + 3) & 15]),    \
+                   [y2] "v"(m[((MO) + 5) & 15]), [y3] "v"(m[((MO) + 7) & 15]))
+__device__ __forceinline__ void b3_asm_step(uint32_t (&v)[16], const uint32_t (&m)[16]) {
+#pragma unroll
+    for (int rr = 0; rr < 7; ++rr) {
+        G4ASM(0, 4, 8, 12, 1, 5, 9, 13, 2, 6, 10, 14, 3, 7, 11, 15, 0);
+        G4ASM(0, 5, 10, 15, 1, 6, 11, 12, 2, 7, 8, 13, 3, 4, 9, 14, 8);
+    }
+}
+
 template <int K>
 __global__ __launch_bounds__(256) void k_issue(uint32_t iters, uint32_t *out, unsigned long long *stamps) {
     extern __shared__ uint32_t lds_pad[];
@@ -472,7 +511,7 @@ __global__ __launch_bounds__(256) void k_issue(uint32_t iters, uint32_t *out, un
         for (int i = 0; i < 16; ++i) x ^= r[i] ^ __float_as_uint(f[i]);
 #pragma unroll
         for (int i = 0; i < 8; ++i) x ^= (uint32_t)q[i] ^ (uint32_t)(q[i] >> 32);
-    } else if constexpr (K >= 110 && K < 125) {
+    } else if constexpr (K >= 110 && K < 125) {  // (125-127: BLAKE3 forms below)
         uint32_t r[16];
         uint64_t q[8];
 #pragma unroll
@@ -494,6 +533,20 @@ __global__ __launch_bounds__(256) void k_issue(uint32_t iters, uint32_t *out, un
         for (uint32_t it = 0; it < iters; ++it) body_x<K>();
         t1 = __builtin_amdgcn_s_memtime();
         rt1 = __builtin_amdgcn_s_memrealtime();
+    } else if constexpr (K == 127) {
+        uint32_t v[16], m[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            v[i] = tid * 0x9E3779B9u + i;
+            m[i] = tid ^ (i * 0x01010101u);
+        }
+        t0 = __builtin_amdgcn_s_memtime();
+        rt0 = __builtin_amdgcn_s_memrealtime();
+        for (uint32_t it = 0; it < iters; ++it) b3_asm_step(v, m);
+        t1 = __builtin_amdgcn_s_memtime();
+        rt1 = __builtin_amdgcn_s_memrealtime();
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x ^= v[i];
     } else if constexpr ((K >= 104 && K <= 106) || K == 109 || K == 125 || K == 126) {
         constexpr int NS = K == 105 || K == 125 || K == 126 ? 1 : 2;
         constexpr int FRESH = K == 109 || K == 125 ? 1 : K == 126 ? 2 : 0;
@@ -640,6 +693,7 @@ static const char *kind_name(int k) {
     case 109: return "BLAKE3 kind 106 with fresh destinations for v_add_u32 / v_xor_b32 (1344 VALU)";
     case 125: return "BLAKE3 pinned, one compression, add3 kept, fresh F destinations (672 VALU)";
     case 126: return "BLAKE3 pinned, one compression, add3 kept, every destination fresh (672 VALU)";
+    case 127: return "BLAKE3 one compression, each G4 step one asm statement (672 VALU)";
     case 108: return "BLAKE3 kind 102 + sched_barrier between op groups (1344 VALU)";
     case 110: return "mix HF HF (add3 / add alternating)";
     case 111: return "mix 8H 8F";
@@ -669,7 +723,7 @@ int main(int argc, char **argv) {
     reg<32>(ks); reg<33>(ks); reg<34>(ks); reg<35>(ks); reg<36>(ks); reg<37>(ks); reg<38>(ks); reg<39>(ks);
     reg<40>(ks); reg<41>(ks); reg<42>(ks); reg<43>(ks); reg<44>(ks); reg<45>(ks); reg<46>(ks); reg<47>(ks);
     reg<60>(ks); reg<61>(ks); reg<62>(ks); reg<63>(ks); reg<64>(ks); reg<65>(ks); reg<66>(ks); reg<67>(ks);
-    reg<68>(ks); reg<100>(ks); reg<101>(ks); reg<102>(ks); reg<103>(ks); reg<104>(ks); reg<105>(ks); reg<106>(ks); reg<107>(ks); reg<108>(ks); reg<109>(ks); reg<125>(ks); reg<126>(ks);
+    reg<68>(ks); reg<100>(ks); reg<101>(ks); reg<102>(ks); reg<103>(ks); reg<104>(ks); reg<105>(ks); reg<106>(ks); reg<107>(ks); reg<108>(ks); reg<109>(ks); reg<125>(ks); reg<126>(ks); reg<127>(ks);
     reg<110>(ks); reg<111>(ks); reg<112>(ks); reg<113>(ks); reg<114>(ks); reg<115>(ks); reg<116>(ks);
     reg<117>(ks); reg<118>(ks); reg<119>(ks); reg<120>(ks); reg<121>(ks); reg<122>(ks); reg<123>(ks); reg<124>(ks);
     std::vector<int> want;
@@ -694,7 +748,7 @@ int main(int argc, char **argv) {
     for (auto &kf : ks) {
         if (!want.empty() && std::find(want.begin(), want.end(), kf.first) == want.end()) continue;
         const int K = kf.first;
-        const uint32_t per_iter = K == 100 || K == 125 || K == 126 ? 672u : K == 101 || K == 105 ? 784u
+        const uint32_t per_iter = K == 100 || K == 125 || K == 126 || K == 127 ? 672u : K == 101 || K == 105 ? 784u
                                 : K == 102 || K == 106 || K == 107 || K == 108 || K == 109 ? 1344u
                                 : K == 103 || K == 104 ? 1568u : 256u;
         CHK(hipFuncSetAttribute((const void *)kf.second, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_max));
