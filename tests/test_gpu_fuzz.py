@@ -1,6 +1,6 @@
 """Randomized parity sweep over the device entries (slow): random valid options, ragged
 batches of 1..64 NARs of random / low-entropy / zero-run / fixture-pattern bytes, both
-digests, through the queued-batch pair (cg_chunk_batch_device_async + cg_batch_wait: NAR
+digests, through the queued-batch pair (cg_chunk_batch_device_async[_after] + cg_batch_wait: NAR
 index written into mapped host memory, host tables through the stage-in kernel, the
 BLAKE3 group map from the assembly) and the host entry; every NAR bit-exact vs the oracle.
 In the spirit of the reference's tests/proptest_suite.rs and fuzz/fuzz_targets/chunking.rs.
@@ -49,11 +49,15 @@ def test_fuzz_device_batches(ca, O, seed):
     stream = torch.cuda.current_stream().cuda_stream
     for algo in (SHA, B3):
         outs = [torch.zeros(cap * 48, dtype=torch.uint8, device="cuda") for _ in range(2)]
-        # two queued batches on one stream, the second waited for first
+        # two queued batches on one stream, the second waited for first; on odd seeds the
+        # second is ordered after an inputs-ready event only (cg_chunk_batch_device_async_after,
+        # the bench's path), so it runs beside the first
         a = ca.chunk_batch_device_async(d.data_ptr(), offs, outs[0].data_ptr(), cap, *params, hash=algo,
                                         stream=stream)
+        ready = torch.cuda.Event()
+        ready.record()
         b = ca.chunk_batch_device_async(d.data_ptr(), offs, outs[1].data_ptr(), cap, *params, hash=algo,
-                                        stream=stream)
+                                        stream=stream, inputs_ready=ready.cuda_event if seed % 2 else 0)
         fb, fa = b.wait(), a.wait()
         assert np.array_equal(fa, fb)
         ga, gb = outs[0].cpu().numpy(), outs[1].cpu().numpy()
