@@ -52,10 +52,10 @@ def test_fuzz_device_batches(ca, O, seed):
         # two queued batches on one stream, the second waited for first; on odd seeds the
         # second is ordered after an inputs-ready event only (cg_chunk_batch_device_async_after,
         # the bench's path), so it runs beside the first
+        ready = torch.cuda.Event()  # (recorded before `a` is queued: it does not wait for `a`)
+        ready.record()
         a = ca.chunk_batch_device_async(d.data_ptr(), offs, outs[0].data_ptr(), cap, *params, hash=algo,
                                         stream=stream)
-        ready = torch.cuda.Event()
-        ready.record()
         b = ca.chunk_batch_device_async(d.data_ptr(), offs, outs[1].data_ptr(), cap, *params, hash=algo,
                                         stream=stream, inputs_ready=ready.cuda_event if seed % 2 else 0)
         fb, fa = b.wait(), a.wait()
