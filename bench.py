@@ -90,15 +90,6 @@ def parse_args():
     ap.add_argument("--split-mode", type=int, default=2, choices=(1, 2),
                     help="overlapped batches: 1 = boundary stages on the library stream, digests in stream order; "
                          "2 = the whole batch on the library stream (digests of consecutive batches overlap too)")
-    ap.add_argument("--chain-bound", action="store_true",
-                    help="an overlapped batch's boundary stages also wait for the previous batch's (A/B)")
-    ap.add_argument("--bound-priority", action="store_true",
-                    help="boundary stages of overlapped batches on a highest-priority stream "
-                         "(CHUNKER_AMD_BOUND_PRIORITY=1; A/B)")
-    ap.add_argument("--digest-cus", type=int, default=0,
-                    help="overlapped batches' digests on a stream restricted to N CUs (CHUNKER_AMD_DIGEST_CUS; A/B)")
-    ap.add_argument("--bound-cus", type=int, default=0,
-                    help="overlapped batches' library stream restricted to N CUs (CHUNKER_AMD_BOUND_CUS; A/B)")
     ap.add_argument("--no-coalesce", action="store_true",
                     help="concurrent callers digest their batches alone (cg_test_coalesce(0)); A/B of the coalescer")
     ap.add_argument("--dist-force", action="store_true",
@@ -135,12 +126,6 @@ def main():
     # --hw-queues 0 keeps the environment's value.
     if args.hw_queues:
         os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
-    if args.bound_priority:
-        os.environ["CHUNKER_AMD_BOUND_PRIORITY"] = "1"
-    if args.bound_cus:
-        os.environ["CHUNKER_AMD_BOUND_CUS"] = str(args.bound_cus)
-    if args.digest_cus:
-        os.environ["CHUNKER_AMD_DIGEST_CUS"] = str(args.digest_cus)
 
     import torch
     import torch.distributed as dist
@@ -169,8 +154,6 @@ def main():
     if args.no_coalesce:
         ca.lib.cg_test_coalesce(0)
     ca.lib.cg_test_split_mode(args.split_mode)
-    if args.chain_bound:
-        ca.lib.cg_test_chain_bound(1)
     if args.concurrent_only:
         print(json.dumps({"concurrent": concurrent_rates(ca, torch, args, n_per, nar_bytes, params, algo)}))
         return

@@ -54,7 +54,7 @@ TEST_HOOKS = ("cg_test_sha_quad_max", "cg_test_sha_split_max", "cg_test_sha_spin
               "cg_test_fail_alloc", "cg_test_sha_quad_fill", "cg_test_sha_pair_fill", "cg_test_scan_path", "cg_test_scan_kernel", "cg_test_coalesce", "cg_test_scan_grid",
               "cg_test_stream_group_cap", "cg_test_stream_max_lanes", "cg_test_stream_eager",
               "cg_test_b3_fused_plan", "cg_test_b3_packed", "cg_coalesce_stats",
-              "cg_test_split_mode", "cg_test_chain_bound")
+              "cg_test_split_mode")
 
 
 def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
@@ -162,8 +162,6 @@ def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
             getattr(L, name).restype = i
     L.cg_test_split_mode.argtypes = [i]
     L.cg_test_split_mode.restype = i
-    L.cg_test_chain_bound.argtypes = [i]
-    L.cg_test_chain_bound.restype = i
     L.cg_coalesce_stats.argtypes = [p]
     L.cg_coalesce_stats.restype = None
     L.cg_test_fail_alloc.argtypes = [ctypes.c_uint32]

@@ -130,8 +130,6 @@ struct Workspace {
     // digest on the caller's stream back, and ev_dstart (after that wait) opens the digest
     // stage's timing.
     hipStream_t bound_stream = nullptr;
-    hipStream_t digest_stream = nullptr;  // (A/B, CHUNKER_AMD_DIGEST_CUS) CU-masked digest stream
-    int ensure_digest_stream();
     hipEvent_t ev_bdone = nullptr, ev_dstart = nullptr;
     // Streams map onto the process's few hardware queues (GPU_MAX_HW_QUEUES, 4 by default)
     // and two streams on one queue serialise: the side stream exists only where used.

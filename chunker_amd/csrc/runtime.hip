@@ -18,7 +18,6 @@
 #include <mutex>
 #include <string>
 #include <thread>
-#include <unordered_map>
 #include <vector>
 
 #include "gear_table.h"
@@ -339,15 +338,7 @@ std::atomic<uint32_t> g_coalesce{1};  // test hook cg_test_coalesce
 // profiles/r05_v3_split_ab.txt); 1 = only the boundary stages do and the digest joins the
 // caller's stream (test hook cg_test_split_mode)
 std::atomic<int> g_split_mode{2};
-// cg_test_chain_bound(1): the boundary stages of an overlapped batch also wait for those of
-// the batch queued before it on the same caller stream (one event per stream, below), so
-// two batches issued together do not scan side by side but one scan apart (A/B)
-std::atomic<int> g_chain_bound{0};
-struct BoundChain {
-    std::mutex mu;
-    std::unordered_map<hipStream_t, hipEvent_t> last;  // caller stream -> its last batch's boundary end
-};
-BoundChain g_bound_chain;
+
 #ifndef CG_COAL_WINDOW_US
 #define CG_COAL_WINDOW_US 3000
 #endif
@@ -625,57 +616,12 @@ int ensure_pass_buffers(Workspace *ws, uint64_t total_len, size_t n_nars, uint64
     return CG_OK;
 }
 
-// The boundary stages' stream of a split batch.  CHUNKER_AMD_BOUND_PRIORITY=1 (read once)
-// creates it at the device's highest stream priority, so its workgroups are dispatched ahead
-// of the digest's as CU slots free up (A/B: a chip-filling digest leaves the scan few slots).
-// A stream restricted to n of the device's CUs, spread over the XCDs (every (CUs / n)-th CU).
-static int create_cu_masked_stream(int device, int n, hipStream_t *out) {
-    hipDeviceProp_t prop;
-    HIP_TRY(hipGetDeviceProperties(&prop, device));
-    const int total = prop.multiProcessorCount;
-    const int stride = std::max(1, total / std::min(n, total));
-    std::vector<uint32_t> mask((total + 31) / 32, 0u);
-    for (int c = 0, k = 0; c < total && k < n; c += stride, ++k) mask[c / 32] |= 1u << (c % 32);
-    HIP_TRY(hipExtStreamCreateWithCUMask(out, (uint32_t)mask.size(), mask.data()));
-    return CG_OK;
-}
-
-// CHUNKER_AMD_DIGEST_CUS=N (A/B, read once): an overlapped batch's digest runs on a stream of
-// N CUs (the first N of the spread above), so the next batch's scan always has the others.
-static int digest_cus() {
-    static const int n = [] {
-        const char *e = getenv("CHUNKER_AMD_DIGEST_CUS");
-        return e ? atoi(e) : 0;
-    }();
-    return n;
-}
-int Workspace::ensure_digest_stream() {
-    if (digest_stream) return CG_OK;
-    return create_cu_masked_stream(device, digest_cus(), &digest_stream);
-}
-
-// CHUNKER_AMD_BOUND_CUS=N (A/B, read once) restricts it to N of the device's CUs spread
-// over the XCDs (every (CUs / N)-th CU), leaving the others to the digest it runs beside.
+// The stream an overlapped batch runs on (cg_chunk_batch_device_async_after), one per
+// workspace.  (Measured without gain and removed since, commit 686ad6b: this stream at the
+// highest priority, restricted to 32 / 64 CUs, the digest on a CU-masked stream of its own,
+// profiles/r05_v3_split_ab.txt, r05_v12_cumask_ab.txt, r05_v16_v17_stagger_ab.txt.)
 int Workspace::ensure_bound_stream() {
-    if (bound_stream) return CG_OK;
-    static const bool high = [] {
-        const char *e = getenv("CHUNKER_AMD_BOUND_PRIORITY");
-        return e && e[0] == '1';
-    }();
-    static const int cus = [] {
-        const char *e = getenv("CHUNKER_AMD_BOUND_CUS");
-        return e ? atoi(e) : 0;
-    }();
-    if (cus > 0) {
-        int rc = create_cu_masked_stream(device, cus, &bound_stream);
-        if (rc) return rc;
-    } else if (high) {
-        int least = 0, greatest = 0;
-        HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        HIP_TRY(hipStreamCreateWithPriority(&bound_stream, hipStreamNonBlocking, greatest));
-    } else {
-        HIP_TRY(hipStreamCreateWithFlags(&bound_stream, hipStreamNonBlocking));
-    }
+    if (!bound_stream) HIP_TRY(hipStreamCreateWithFlags(&bound_stream, hipStreamNonBlocking));
     return CG_OK;
 }
 
@@ -841,18 +787,10 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
     // overlapping it with the next batch measured 1.7 % slower on config 3,
     // profiles/r05_v3_split_ab.txt; waiting for more than inputs_ready is always allowed)
     hipStream_t bs = st;
-    hipEvent_t chain_ev = nullptr;  // this caller stream's boundary-chain event (g_chain_bound)
     if (inputs_ready && algo == CG_SHA256) {
         if ((rc = ws->ensure_bound_stream())) return rc;
         bs = ws->bound_stream;
         HIP_TRY(hipStreamWaitEvent(bs, inputs_ready, 0));
-        if (g_chain_bound.load(std::memory_order_relaxed)) {
-            std::lock_guard<std::mutex> g(g_bound_chain.mu);
-            hipEvent_t &e = g_bound_chain.last[st];
-            if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            else HIP_TRY(hipStreamWaitEvent(bs, e, 0));  // the previous batch's boundary stages
-            chain_ev = e;
-        }
     }
     if ((rc = ensure_scan_queue(ws, bs))) return rc;
     // nar_off (n+1) then cap_base (n+1): one block, one copy (s_cap follows s_off in staging)
@@ -907,27 +845,13 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
                             ws->scan_tmp.as<uint64_t>(), bs, b3_fuse ? &b3plan : nullptr,
                             static_cast<uint64_t *>(ws->first_host.dev), &first_on_host);
     if (prof) HIP_TRY(hipEventRecord(ws->ev[EV_ASSEMBLE], bs));
-    if (chain_ev) {  // (the next overlapped batch on `st` waits for this one's boundary stages)
-        std::lock_guard<std::mutex> g(g_bound_chain.mu);
-        HIP_TRY(hipEventRecord(chain_ev, bs));
-    }
     bl->dstart = ws->ev[EV_ASSEMBLE];
     // The digest's stream: `st`, joined after the boundary stages (split mode 1), or -- split
     // mode 2 -- the library stream itself, so the whole batch is ordered after inputs_ready
     // only and `st` waits for its end (below): a batch's digest then runs beside the digest of
     // the batch queued before it.
     hipStream_t ds = st;
-    if (bs != st && g_split_mode.load(std::memory_order_relaxed) == 2 && digest_cus() > 0) {
-        // (A/B) the digest on a CU-masked stream of the workspace, after the boundary stages
-        if ((rc = ws->ensure_digest_stream())) return rc;
-        ds = ws->digest_stream;
-        HIP_TRY(hipEventRecord(ws->ev_bdone, bs));
-        HIP_TRY(hipStreamWaitEvent(ds, ws->ev_bdone, 0));
-        if (prof) {
-            HIP_TRY(hipEventRecord(ws->ev_dstart, ds));
-            bl->dstart = ws->ev_dstart;
-        }
-    } else if (bs != st && g_split_mode.load(std::memory_order_relaxed) == 2) {
+    if (bs != st && g_split_mode.load(std::memory_order_relaxed) == 2) {
         ds = bs;
     } else if (bs != st) {  // join: the digest (and everything after it) follows the boundary stages
         HIP_TRY(hipEventRecord(ws->ev_bdone, bs));
@@ -1400,7 +1324,6 @@ int push_append(cg_push *h, const uint8_t *data, uint64_t len) {
 }  // namespace cgrt
 
 extern "C" int cg_test_split_mode(int v) { return cgrt::g_split_mode.exchange(v == 2 ? 2 : 1); }
-extern "C" int cg_test_chain_bound(int v) { return cgrt::g_chain_bound.exchange(v ? 1 : 0); }
 
 extern "C" uint32_t cg_test_coalesce(uint32_t v) {  // 0 = every device-entry call digests alone
     return cgrt::g_coalesce.exchange(v ? 1u : 0u);
