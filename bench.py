@@ -34,6 +34,7 @@ import subprocess
 import sys
 import threading
 import time
+from collections import deque
 from pathlib import Path
 
 import numpy as np
@@ -87,9 +88,15 @@ def parse_args():
     ap.add_argument("--no-overlap", action="store_true",
                     help="queue each batch after everything on the stream (cg_chunk_batch_device_async): its "
                          "boundary stages wait for the previous batch's digest (A/B of the overlap)")
+    ap.add_argument("--depth", type=int, default=0, choices=range(0, 17), metavar="0..16",
+                    help="batches in flight from the one caller (each its own output array and workspace); "
+                         "1 = each batch waited for before the next is queued; 0 = auto (default_depth)")
     ap.add_argument("--split-mode", type=int, default=2, choices=(1, 2),
                     help="overlapped batches: 1 = boundary stages on the library stream, digests in stream order; "
                          "2 = the whole batch on the library stream (digests of consecutive batches overlap too)")
+    ap.add_argument("--sha-tiers", default="",
+                    help="SHA-256 latency tiers 'QUAD_PM,PAIR_PM[,FILL_QUAD_PM,FILL_PAIR_PM]' (cg_test_sha_tiers, "
+                         "cg_test_sha_tiers_fill; quad 0 = off; '' = the library's)")
     ap.add_argument("--no-coalesce", action="store_true",
                     help="concurrent callers digest their batches alone (cg_test_coalesce(0)); A/B of the coalescer")
     ap.add_argument("--dist-force", action="store_true",
@@ -99,6 +106,26 @@ def parse_args():
                     help="N > 1: nccl = RCCL over xGMI, one GPU per rank (the product); gloo = host-copy "
                          "gather, ranks may share a GPU (rehearses the N > 1 path on a one-GPU box)")
     return ap.parse_args()
+
+
+def default_depth(algo: int, batch_bytes: int) -> int:
+    """Batches the one caller keeps in flight (DESIGN.md §7 "Batches in flight").
+    SHA-256 under 4 GiB a batch: 10.  Such a batch's digest is latency-bound -- every chunk
+    is one serial chain, config 2's longest is 52,345 blocks = 53 ms, and its ~1,000 chains
+    leave most of the chip idle -- so the batches queued behind it fill the chip instead
+    (config 2, 20 steps: 18.1 / 35.8 / 85 / 105 / 126 / 131 GiB/s at 1 / 2 / 6 / 8 / 10 /
+    12 in flight, per-batch p50 latency 55 -> 65-80 ms; profiles/r05_v22_depth_ab.txt).
+    SHA-256 from 4 GiB: 4 (configs 4 / 5: the digest fills the chip by itself and the
+    overlap hides the scan; 697 -> 703-727 and 324 -> 379-400 GiB/s from 2 to 4, within
+    noise beyond).  BLAKE3: 2 (its batches stay in stream order; the second one queued
+    covers the host's per-call work).  Each batch in flight runs on a HIP stream of its own,
+    so the depth is held to GPU_MAX_HW_QUEUES - 2 (the caller's stream and torch's take two
+    queues): at HIP's default 4 queues streams share them and config 2 stays at 36 GiB/s
+    whatever the depth (profiles/r05_v23_depth_ab.txt)."""
+    if algo != 1:
+        return 2
+    hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+    return max(2, min(10 if batch_bytes < 4 * GIB else 4, hwq - 2))
 
 
 def launch_ranks(n: int) -> int:
@@ -154,6 +181,11 @@ def main():
     if args.no_coalesce:
         ca.lib.cg_test_coalesce(0)
     ca.lib.cg_test_split_mode(args.split_mode)
+    if args.sha_tiers:
+        t = [int(v) for v in args.sha_tiers.split(",")]
+        ca.lib.cg_test_sha_tiers(t[0], t[1])
+        if len(t) == 4:
+            ca.lib.cg_test_sha_tiers_fill(t[2], t[3])
     if args.concurrent_only:
         print(json.dumps({"concurrent": concurrent_rates(ca, torch, args, n_per, nar_bytes, params, algo)}))
         return
@@ -168,16 +200,17 @@ def main():
     # RCCL gather: fixed per-rank sizes agreed once here, so a step's gather needs no count
     # exchange and no host sync (chunker_amd.dist.gather_batch_async)
     gcap, gnars = gather_shape(cap, len(mine)) if multi and nccl else (cap, len(mine))
-    # two output arrays, alternate steps: while step k's descriptors are gathered, step k + 1
-    # writes the other one
-    d_outs = [torch.empty(gcap * 48, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    # `depth` output arrays, used in turn: while step k's descriptors are gathered, steps
+    # k + 1 .. k + depth - 1 write the others
+    depth = args.depth or default_depth(algo, int(offs[-1]))
+    d_outs = [torch.empty(gcap * 48, dtype=torch.uint8, device="cuda") for _ in range(depth)]
     # The batches run on a stream of their own.  The gather of step k is queued on torch's
     # current stream (RCCL's stream waits for that one), which holds none of the batches, so
     # it runs while step k + 1's kernels do instead of queueing behind them; an event after
-    # it holds back step k + 2, the next writer of the same output array.
+    # it holds back step k + depth, the next writer of the same output array.
     bstream = torch.cuda.Stream()
     sptr = bstream.cuda_stream
-    gathered_ev = [None, None]
+    gathered_ev = [None] * depth
     gathered = [None]
     # Inputs-ready events (cg_chunk_batch_device_async_after): a batch's boundary stages
     # (scan, walk, assembly) wait only for its input and output array to be free -- the NARs
@@ -188,35 +221,47 @@ def main():
     synth_ev.record()
 
     def issue(k):
-        ev = gathered_ev[k % 2]
+        ev = gathered_ev[k % depth]
         if ev is not None:
             bstream.wait_event(ev)  # (the digest writes the output array's hashes)
         ready = 0 if args.no_overlap else (ev or synth_ev).cuda_event
-        return ca.chunk_batch_device_async(d_data.data_ptr(), offs, d_outs[k % 2].data_ptr(), gcap, *params,
+        return ca.chunk_batch_device_async(d_data.data_ptr(), offs, d_outs[k % depth].data_ptr(), gcap, *params,
                                            hash=algo, stream=sptr, inputs_ready=ready)
 
     def complete(k, batch):
         first = batch.wait()
         if multi and nccl:  # descriptors + NAR index to rank 0 over RCCL (the path's only exchange)
-            gathered[0] = gather_batch_async(d_outs[k % 2], first, gcap, gnars)
+            gathered[0] = gather_batch_async(d_outs[k % depth], first, gcap, gnars)
             ev = torch.cuda.Event()
             ev.record()
-            gathered_ev[k % 2] = ev
+            gathered_ev[k % depth] = ev
         elif multi:  # gloo rehearsal: host copies
-            gathered[0] = gather_batch(d_outs[k % 2][: int(first[-1]) * 48].cpu(), first)
+            gathered[0] = gather_batch(d_outs[k % depth][: int(first[-1]) * 48].cpu(), first)
         return first
 
     def step(k=0):  # one batch, waited for
         return complete(k, issue(k))
 
-    # warm-up in the timed loop's pattern (two batches queued, so both workspaces the pool
-    # hands out are sized before the timed region)
-    pending = issue(0)
-    for k in range(args.warmup):
-        nxt = issue(k + 1)
-        first = complete(k, pending)
-        pending = nxt
-    complete(args.warmup, pending)
+    def run(n, on_done=None):
+        """n steps, up to `depth` queued: step k + depth - 1 is queued before step k is
+        waited for, so the host side of each call -- validation, staging, launches, the
+        wait -- overlaps the GPU's work instead of idling it between batches (~65 us per
+        step, 8 % of a config-3 step)."""
+        q = deque()
+        first = None
+        for k in range(n + depth - 1):
+            if k < n:
+                q.append((k, time.perf_counter(), issue(k)))
+            if len(q) == depth or (k >= n and q):
+                kk, t_issue, b = q.popleft()
+                first = complete(kk, b)
+                if on_done:
+                    on_done(kk, time.perf_counter() - t_issue)
+        return first
+
+    # warm-up in the timed loop's pattern (depth batches queued, so every workspace the pool
+    # hands out is sized before the timed region)
+    run(max(args.warmup, depth) + 1)
     # Digest-stage device time: the two HIP events the library records around the digest
     # on the stream the kernels run on (cg_set_profiling(2)), live inside the timed region
     # (each step already ends in a stream sync for the NAR->chunk index, so reading them
@@ -230,18 +275,16 @@ def main():
     if multi:
         dist.barrier()
     t0 = time.perf_counter()
-    # Steps run back to back on one stream: step k + 1 is queued before step k is waited
-    # for (cg_chunk_batch_device_async), so the host side of each call -- validation,
-    # staging, launches, the wait -- overlaps the GPU's work instead of idling it between
-    # batches (~65 us per step, 8 % of a config-3 step).
-    pending = issue(0)
-    for k in range(args.steps):
-        nxt = issue(k + 1) if k + 1 < args.steps else None
-        first = complete(k, pending)
+
+    latency = np.zeros(max(args.steps, 1))
+
+    def record(k, waited):
         ca.lib.cg_last_stage_times(buf, 5)
         stage[k] = list(buf)
-        pending = nxt
-    last = (args.steps - 1) % 2
+        latency[k] = waited
+
+    first = run(args.steps, record)
+    last = (args.steps - 1) % depth
     torch.cuda.synchronize()  # every stream: the batches' and the last gather
     if multi:
         dist.barrier()
@@ -319,7 +362,7 @@ def main():
     # wall time (= `value` in GB/s).
     roofline["aggregate"] = {"achieved": round(total_bytes * args.steps / elapsed / 1e9, 2),
                              "frac": round(total_bytes * args.steps / elapsed / 1e9 / HBM_PEAK_GBS, 5),
-                             "launches_in_flight": 1 if args.no_overlap or algo != 1 else 2,
+                             "launches_in_flight": 1 if args.no_overlap or algo != 1 else depth,
                              "note": "this rank's algorithmic bytes of all timed steps / the timed wall time"}
     if algo == 1:
         clk = sha_clock(args) if world == 1 and not args.no_clock else None
@@ -357,12 +400,15 @@ def main():
             "unit": "GiB/s",
             "n_gpus": world,
             "steps": args.steps,
-            "steps_queued": 2,
-            "overlap": "none" if args.no_overlap else (
+            "steps_queued": depth,
+            "overlap": "none" if args.no_overlap or depth == 1 else (
                 "none (BLAKE3 batches stay in stream order)" if algo == 0 else
-                "boundary stages" if args.split_mode == 1 else "whole batch: two batches in flight"),
+                "boundary stages" if args.split_mode == 1 else f"whole batch: {depth} batches in flight"),
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            # what one batch waits, queued -> results on the host, with `depth` in flight
+            "batch_latency_ms": {"p50": round(float(np.percentile(latency[: args.steps], 50)) * 1e3, 3),
+                                 "p99": round(float(np.percentile(latency[: args.steps], 99)) * 1e3, 3)},
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

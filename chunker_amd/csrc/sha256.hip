@@ -708,9 +708,16 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
                                                uint8_t *__restrict__ hash_base, size_t stride,
                                                unsigned long long *__restrict__ diag, uint32_t mode,
                                                uint32_t nquad, uint32_t npair, uint32_t spin_limit,
-                                               uint32_t *__restrict__ err) {
+                                               uint32_t *__restrict__ err, const uint32_t *__restrict__ need) {
     unsigned long long t_start = diag ? __builtin_amdgcn_s_memtime() : 0ull, t_spin = 0;
     const unsigned long long rt_start = diag ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    if (need) {  // latency tiers (k_len_base): no more lanes per chunk than its length needs
+        const uint32_t nq = (need[0] + 7u) / 8u;
+        if (nq < nquad) nquad = nq;
+        const uint32_t rest = need[1] > 8u * nquad ? need[1] - 8u * nquad : 0u;
+        const uint32_t np = (rest + 31u) / 32u;
+        if (np < npair) npair = np;
+    }
     __shared__ __attribute__((aligned(16))) uint32_t sW[PC_RING][64 * PC_ROW];
     // hand-off words (SY_*): blocks filled by the producer / consumed by the consumer,
     // the spin guard's timeout flag and limit
@@ -861,10 +868,22 @@ __global__ __launch_bounds__(256) void k_len_hist(const DescRaw *__restrict__ de
         if (h[i]) atomicAdd(&bkt[i], h[i]);
 }
 
-// one workgroup: bkt[i] <- exclusive prefix sum of the bucket counts
-__global__ __launch_bounds__(SHA_NBKT) void k_len_base(uint32_t *__restrict__ bkt) {
+// one workgroup: bkt[i] <- exclusive prefix sum of the bucket counts.
+// With `need` (latency tiers, k_sha256): need[0] = the chunks longer than quad_pm / 1000 of
+// the longest one (in buckets), need[1] = those longer than pair_pm / 1000 of it.  A chunk
+// runs on one lane unless its one-lane chain (59.4 clocks per round) would outlast the
+// longest chunk's quad chain (37.95), and on a lane pair unless its pair chain (42.2) would
+// (DESIGN.md §4 "Latency tiers"): the longest chunk still sets the batch's digest time, and
+// the other chunks take 1/8 and 1/2 of the SIMD time a quad would give them.
+__global__ __launch_bounds__(SHA_NBKT) void k_len_base(uint32_t *__restrict__ bkt, uint32_t *__restrict__ need,
+                                                      uint32_t quad_pm, uint32_t pair_pm) {
     __shared__ uint32_t wsum[SHA_NBKT / 64];
+    __shared__ uint32_t s_first, s_need[2];
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+    if (t == 0) {
+        s_first = SHA_NBKT;
+        s_need[0] = s_need[1] = 0;
+    }
     const uint32_t v = bkt[t];
     uint32_t x = v;
 #pragma unroll
@@ -874,9 +893,22 @@ __global__ __launch_bounds__(SHA_NBKT) void k_len_base(uint32_t *__restrict__ bk
     }
     if (lane == 63) wsum[w] = x;
     __syncthreads();
+    if (v) atomicMin(&s_first, t);  // the longest chunk's bucket (buckets descend)
     uint32_t off = 0;
     for (uint32_t k = 0; k < w; ++k) off += wsum[k];
     bkt[t] = off + x - v;
+    if (!need) return;
+    __syncthreads();
+    // bucket value (blocks >> shift) of bucket t is SHA_NBKT - 1 - t; the chunks in buckets
+    // above a threshold are a prefix of the order, counted by the inclusive prefix sum
+    const uint32_t bmax = SHA_NBKT - 1u - min(s_first, SHA_NBKT - 1u), bv = SHA_NBKT - 1u - t;
+    if (bv * 1000u > bmax * quad_pm) atomicMax(&s_need[0], off + x);
+    if (bv * 1000u > bmax * pair_pm) atomicMax(&s_need[1], off + x);
+    __syncthreads();
+    if (t == 0) {
+        need[0] = max(s_need[0], 1u);
+        need[1] = max(s_need[1], s_need[0]);
+    }
 }
 
 __global__ __launch_bounds__(256) void k_len_scatter(const DescRaw *__restrict__ desc,
@@ -904,8 +936,21 @@ __global__ __launch_bounds__(256) void k_len_scatter(const DescRaw *__restrict__
 
 size_t sha256_order_tmp_elems(uint64_t max_chunks) { return max_chunks + SHA_NBKT + 64; }
 
+// Latency tiers (k_len_base), in per-mille of the longest chunk's blocks: a chunk longer
+// than quad_pm needs a quad (on a pair it would outlast the longest chunk's quad chain:
+// 37.95 / 42.2 = 0.899 of it), one longer than pair_pm at least a pair (on one lane:
+// 37.95 / 59.4 = 0.639).  [0] a launch that leaves the chip idle but for its chains:
+// a little under those ratios; [1] a launch that fills the GPU (sha256_grid's fill
+// tiers, config 4), where one lane's SIMD time is what the others queue behind: above
+// them (DESIGN.md §4 "Latency tiers", profiles/r05_v24_v25_tiers_ab.txt).  Test hooks
+// cg_test_sha_tiers / cg_test_sha_tiers_fill (quad_pm 0 = off: every chunk on the widest
+// tier the grid holds).
+uint32_t g_sha_tier_quad_pm[2] = {850, 950};
+uint32_t g_sha_tier_pair_pm[2] = {600, 700};
+
 const uint32_t *launch_len_order(const void *d_desc, const uint64_t *d_total, uint64_t max_chunks, uint64_t max_len,
-                                 uint32_t *d_order_tmp, hipStream_t st) {
+                                 uint32_t *d_order_tmp, hipStream_t st, uint32_t *d_need, uint32_t quad_pm,
+                                 uint32_t pair_pm) {
     if (!d_order_tmp || max_chunks == 0) return nullptr;
     uint32_t shift = 0;
     while ((((max_len + 72) >> 6) >> shift) >= SHA_NBKT - 1) ++shift;
@@ -914,7 +959,7 @@ const uint32_t *launch_len_order(const void *d_desc, const uint64_t *d_total, ui
     (void)hipMemsetAsync(bkt, 0, SHA_NBKT * sizeof(uint32_t), st);
     hipLaunchKernelGGL(k_len_hist, dim3(nb), dim3(256), 0, st, (const DescRaw *)d_desc, d_total, max_chunks, shift,
                        bkt);
-    hipLaunchKernelGGL(k_len_base, dim3(1), dim3(SHA_NBKT), 0, st, bkt);
+    hipLaunchKernelGGL(k_len_base, dim3(1), dim3(SHA_NBKT), 0, st, bkt, d_need, quad_pm, pair_pm);
     hipLaunchKernelGGL(k_len_scatter, dim3(nb), dim3(256), 0, st, (const DescRaw *)d_desc, d_total, max_chunks,
                        shift, bkt, ord);
     return ord;
@@ -949,7 +994,8 @@ uint32_t g_sha_spin_limit = 1u << 26;
 // LDS for 8 chunks, so up to 256 quads are used only when the one-lane tier left
 // behind them fits in one round of workgroups (<= 256 x 64 chunks); on a batch that
 // fills the GPU (config 4) only g_sha_quad_fill of them, for the longest chunks.
-uint32_t sha256_grid(uint64_t max_chunks, uint64_t expected, uint32_t *nquad_out, uint32_t *npair_out) {
+uint32_t sha256_grid(uint64_t max_chunks, uint64_t expected, uint32_t *nquad_out, uint32_t *npair_out,
+                     bool *fill_out) {
     auto tiers = [&](uint64_t qmax, uint64_t pmax, uint64_t &nq, uint64_t &np) {
         nq = (max_chunks + 7) / 8;
         if (nq > qmax) nq = qmax;
@@ -959,7 +1005,9 @@ uint32_t sha256_grid(uint64_t max_chunks, uint64_t expected, uint32_t *nquad_out
     };
     uint64_t nq, np;
     tiers(g_sha_quad_max, g_sha_split_max, nq, np);
-    if (expected > 8 * nq + 32 * np + 256 * 64)
+    const bool fill = expected > 8 * nq + 32 * np + 256 * 64;
+    if (fill_out) *fill_out = fill;
+    if (fill)
         tiers(std::min<uint64_t>(g_sha_quad_max, g_sha_quad_fill), std::min<uint64_t>(g_sha_split_max, g_sha_pair_fill),
               nq, np);
     const uint64_t rest = max_chunks > 8 * nq + 32 * np ? max_chunks - 8 * nq - 32 * np : 0;
@@ -977,10 +1025,16 @@ void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
                    uint8_t *d_hash_base, size_t hash_stride, uint32_t *d_err, hipStream_t st) {
     if (max_chunks == 0) return;
     uint32_t nquad = 0, npair = 0;
-    const uint32_t nwg = sha256_grid(max_chunks, expected, &nquad, &npair);
+    bool fill = false;
+    const uint32_t nwg = sha256_grid(max_chunks, expected, &nquad, &npair, &fill);
     // one workgroup has nothing to balance
-    const uint32_t *order = max_chunks > 8 ? launch_len_order(d_desc, d_total, max_chunks, max_len, d_order_tmp, st)
-                                           : nullptr;
+    // latency tiers: k_len_base counts the chunks that need a quad / a pair into the two
+    // words after the order (sha256_order_tmp_elems' slack)
+    const uint32_t qpm = g_sha_tier_quad_pm[fill], ppm = g_sha_tier_pair_pm[fill];
+    uint32_t *need = max_chunks > 8 && d_order_tmp && qpm ? d_order_tmp + SHA_NBKT + max_chunks : nullptr;
+    const uint32_t *order = max_chunks > 8
+                                ? launch_len_order(d_desc, d_total, max_chunks, max_len, d_order_tmp, st, need, qpm, ppm)
+                                : nullptr;
     // Latency-bound batches (no more workgroups than CUs): pad the LDS request past half
     // a CU's 160 KiB so no two workgroups share a CU, and a consumer wave never shares a
     // SIMD with another workgroup's wave (which costs it 20-90 % per round).
@@ -992,7 +1046,7 @@ void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
     t_sha_tiers[3] = (uint32_t)pad;
     hipLaunchKernelGGL(k_sha256, dim3(nwg), dim3(128), pad, st, d_data, d_abs,
                        (const DescRaw *)d_desc, d_total, max_chunks, order, d_hash_base, hash_stride, g_sha_diag,
-                       g_sha_mode, nquad, npair, g_sha_spin_limit, d_err);
+                       g_sha_mode, nquad, npair, g_sha_spin_limit, d_err, order ? need : nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -1150,7 +1204,7 @@ extern "C" int cg_diag_dpp_probe(uint32_t *h_out) {
 
 // workgroups the digest launch uses for `max_chunks` (diagnostics: sizes cg_diag_sha_stats)
 extern "C" uint32_t cg_diag_sha_grid(uint64_t max_chunks, uint64_t expected) {
-    return cg::sha256_grid(max_chunks, expected, nullptr, nullptr);
+    return cg::sha256_grid(max_chunks, expected, nullptr, nullptr, nullptr);
 }
 #endif  // CG_DIAG
 
@@ -1183,6 +1237,20 @@ extern "C" uint32_t cg_test_sha_pair_fill(uint32_t v) {
     const uint32_t old = cg::g_sha_pair_fill;
     cg::g_sha_pair_fill = v;
     return old;
+}
+
+// Latency tiers: per-mille thresholds (quad, pair) of the longest chunk for launches that
+// leave the chip idle (cg_test_sha_tiers) and for GPU-filling ones (cg_test_sha_tiers_fill);
+// quad_pm 0 = off.  Each returns its previous quad_pm * 1000 + pair_pm.
+static uint32_t set_sha_tiers(int k, uint32_t quad_pm, uint32_t pair_pm) {
+    const uint32_t old = cg::g_sha_tier_quad_pm[k] * 1000u + cg::g_sha_tier_pair_pm[k];
+    cg::g_sha_tier_quad_pm[k] = quad_pm > 1000u ? 1000u : quad_pm;
+    cg::g_sha_tier_pair_pm[k] = pair_pm > cg::g_sha_tier_quad_pm[k] ? cg::g_sha_tier_quad_pm[k] : pair_pm;
+    return old;
+}
+extern "C" uint32_t cg_test_sha_tiers(uint32_t quad_pm, uint32_t pair_pm) { return set_sha_tiers(0, quad_pm, pair_pm); }
+extern "C" uint32_t cg_test_sha_tiers_fill(uint32_t quad_pm, uint32_t pair_pm) {
+    return set_sha_tiers(1, quad_pm, pair_pm);
 }
 
 extern "C" uint32_t cg_test_sha_quad_max(uint32_t v) {

@@ -532,6 +532,44 @@ def test_sha_workgroup_kinds_agree(ca, O, quad_max, pair_max):
         _sha_kinds(ca, *prev)
 
 
+@pytest.mark.parametrize("quad_pm,pair_pm", [(850, 600), (1000, 1000), (1, 1), (900, 0), (500, 499)],
+                         ids=["product", "longest_only", "all_quad", "no_one_lane", "close"])
+def test_sha_latency_tiers_agree(ca, O, quad_pm, pair_pm):
+    """Latency tiers (k_len_base -> k_sha256): the chunks needing a quad / a pair are
+    counted on the device from the length histogram and the workgroup kinds follow them,
+    so a chunk's lane count depends on its length; every threshold pair gives hashlib's
+    digests over the span sweep and the oracle's descriptors through the pipeline."""
+    import torch
+
+    prev = ca.lib.cg_test_sha_tiers(quad_pm, pair_pm)
+    prev_fill = ca.lib.cg_test_sha_tiers_fill(quad_pm, pair_pm)
+    try:
+        rng = np.random.default_rng(23)
+        data = rng.integers(0, 256, 3 << 20, dtype=np.uint8)
+        lens = list(range(0, 130)) + [511, 4097, 65537, 300_000, 600_000, 900_000, 1 << 20, 1_500_000, 2_000_001]
+        offs = [int(rng.integers(0, len(data) - n + 1)) for n in lens]
+        d = torch.from_numpy(data).cuda()
+        o = torch.tensor(offs, dtype=torch.int64).cuda()
+        ln = torch.tensor(lens, dtype=torch.int64).cuda()
+        dig = torch.zeros(len(lens) * 32, dtype=torch.uint8, device="cuda")
+        assert ca.lib.cg_hash_spans_device(d.data_ptr(), o.data_ptr(), ln.data_ptr(), len(lens), SHA,
+                                           dig.data_ptr(), None) == 0
+        dig = dig.cpu().numpy().reshape(-1, 32)
+        for k, (a, n) in enumerate(zip(offs, lens)):
+            assert bytes(dig[k]) == hashlib.sha256(data[a:a + n].tobytes()).digest(), (quad_pm, pair_pm, n, a)
+        from chunker_amd.nar import synth_nars
+
+        sizes = [2 * 1024 * 1024 + 8 * k for k in range(6)]
+        nd, no = synth_nars(sizes, first_index=5)
+        nars = [nd[no[i]:no[i + 1]] for i in range(len(sizes))]
+        got = ca.chunk_batch(nars, 4096, 16384, 65536)
+        for i, nar in enumerate(nars):
+            assert_same(got[i], O.chunk_descriptors(nar, 4096, 16384, 65536, algo=SHA), f"nar{i}")
+    finally:
+        ca.lib.cg_test_sha_tiers(prev // 1000, prev % 1000)
+        ca.lib.cg_test_sha_tiers_fill(prev_fill // 1000, prev_fill % 1000)
+
+
 @pytest.mark.slow
 def test_full_size_config2_batch(ca, O):
     """BASELINE config 2 at full size (256 x 4 MiB NARs, defaults, SHA-256): every

@@ -86,5 +86,26 @@ def test_bench_cli_contract():
     r = subprocess.run([sys.executable, str(root / "bench.py"), "--help"], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stderr
     for flag in ("--gpus", "--steps", "--warmup", "--config", "--no-overlap", "--split-mode", "--drop-in",
-                 "--drop-in-sizes", "--no-coalesce", "--dist-force"):
+                 "--drop-in-sizes", "--no-coalesce", "--dist-force", "--depth"):
         assert flag in r.stdout, flag
+
+
+def test_bench_default_depth(monkeypatch):
+    """bench.py's batches in flight: 10 for sub-4-GiB SHA-256 batches (latency-bound
+    digest), 4 from 4 GiB, 2 for BLAKE3, and never more than the hardware queues allow
+    (each batch in flight holds a stream of its own)."""
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    import bench
+
+    G = bench.GIB
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "16")
+    assert bench.default_depth(1, G) == 10
+    assert bench.default_depth(1, 16 * G) == 4
+    assert bench.default_depth(0, G) == 2
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "8")
+    assert bench.default_depth(1, G) == 6
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    assert bench.default_depth(1, G) == 2 and bench.default_depth(1, 16 * G) == 2
