@@ -442,7 +442,8 @@ def concurrent_rates(ca, torch, args, n_per, nar_bytes, params, algo):
     Aggregate GiB/s = K x reps x batch bytes / wall time (after one untimed round that
     sizes every workspace), and what a caller waits per call (p50 / p99 ms).  For SHA-256
     both coalescer settings run, one after the other in this process: `merged` (digests
-    of more than 8 concurrent callers share one launch, the product) and `per_batch`
+    of more concurrent callers than per-batch launches run side by side share one launch, the
+    product) and `per_batch`
     (cg_test_coalesce(0)), so the merged rate and its latency cost sit side by side; the
     coalescer's own counters (groups, members, leader wait, windows run out) are reported
     for the merged runs.  The headline `value` stays the single-batch rate."""
@@ -467,7 +468,8 @@ def concurrent_rates(ca, torch, args, n_per, nar_bytes, params, algo):
     ca.lib.cg_test_coalesce(int(coal))
     res = {"unit": "GiB/s", "latency_unit": "ms per call", "batch": f"{n_per}x{nar_bytes >> 20}MiB",
            "reps": max(1, args.concurrent_reps), "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default (4)"),
-           "digests": "coalesced (one SHA-256 launch per group of more than 8 concurrent callers)"
+           "digests": "coalesced (one SHA-256 launch per group once more callers are in flight than the hardware "
+                      "queues less 4)"
            if coal and algo == 1 else "one launch per batch"}
     modes = [("merged", 1), ("per_batch", 0)] if coal and algo == 1 else [("per_batch", int(coal))]
     stats = (ctypes.c_uint64 * 4)()

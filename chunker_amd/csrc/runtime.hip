@@ -291,8 +291,8 @@ uint32_t seg_slots(const CdcParams &p) {
 // launch on the member's own stream, so a lone caller's latency is unchanged.
 //
 // What a member can wait for, beyond its own digest's chain: callers only merge past
-// CG_COAL_MIN (8) in the entry, so a lone caller and up to 8 concurrent ones never enter a
-// group (they go solo and no leader counts them: test_lone_and_few_callers_never_wait_for_the
+// coal_min() (the hardware queues less 4, at least 4) in the entry, so a lone caller and up
+// to that many concurrent ones never enter a group (they go solo and no leader counts them: test_lone_and_few_callers_never_wait_for_the
 // _window); a merged member waits at most kCoalWindow (3 ms) for its group to form plus the
 // previous group's remaining chain on the one set (lease_set: <= one longest-chunk chain,
 // ~55-75 ms at the default 4 MiB max), i.e. its call returns within window + 2 chains + its
@@ -483,20 +483,33 @@ static int launch_group(CoalSet *S, std::vector<CoalEntry *> &grp, std::shared_p
 }
 
 // Merge only when more callers are in flight than per-batch launches run side by side:
-// up to CG_COAL_MIN callers (8) each batch's own launch overlaps the others' on their own
-// hardware queues as well as one merged launch would (K = 8: 105-110 GiB/s per batch
-// against 87-111 always merged, profiles/r04_v18_*, r04_v19_*), and past them the per-batch
-// launches queue behind one another (K = 16 / 32: 110-118 / 114-175 per batch against
-// 155 / 286-305 merged).  Leader window 3 ms: 10 ms gave K = 32 220-279.
+// the process's hardware queues (GPU_MAX_HW_QUEUES, HIP's default 4) less the 4 its other
+// streams take (at least CG_COAL_MIN = 4).  Up to that each batch's own launch overlaps
+// the others' on a queue of its own, and with the SHA-256 latency tiers (sha256.hip) as
+// well as one merged launch (16 queues, K = 12: 169 GiB/s per batch, p99 73 ms); past it
+// the per-batch launches queue behind one another on shared queues (K = 16 / 24 / 32:
+// 127-133 / 134 / 137 per batch with p99 121-127 ms, against 170 / 182 / 227-241 merged;
+// profiles/r05_v28_*, r05_v29_*, r05_v30_*).  Round 4, before the tiers, merged from 8
+// callers (profiles/r04_v18_*, r04_v19_*).  Leader window 3 ms: 10 ms gave K = 32 220-279.
 #ifndef CG_COAL_MIN
-#define CG_COAL_MIN 8
+#define CG_COAL_MIN 4
 #endif
+static size_t coal_min() {
+    static const size_t n = [] {
+        const char *e = getenv("GPU_MAX_HW_QUEUES");
+        char *end = nullptr;
+        const unsigned long v = e && *e ? strtoul(e, &end, 10) : 0;
+        const size_t q = (e && *e && end && *end == 0 && v >= 1 && v <= 64) ? (size_t)v : (size_t)4;
+        return std::max<size_t>(q > 4 ? q - 4 : 0, CG_COAL_MIN);
+    }();
+    return n;
+}
 bool coalesce_worth(int dev) {
     Coalescer &C = coalescer(dev);
     std::lock_guard<std::mutex> g(C.mu);
     const auto now = std::chrono::steady_clock::now();
     while (!C.returned.empty() && now - C.returned.front() > kCoalRecent) C.returned.pop_front();
-    return (size_t)C.inside + C.returned.size() > CG_COAL_MIN;  // (pending callers are inside)
+    return (size_t)C.inside + C.returned.size() > coal_min();  // (pending callers are inside)
 }
 
 int coalesced_sha256(CoalEntry *e) {

@@ -942,7 +942,7 @@ size_t sha256_order_tmp_elems(uint64_t max_chunks) { return max_chunks + SHA_NBK
 // 37.95 / 59.4 = 0.639).  [0] a launch that leaves the chip idle but for its chains:
 // a little under those ratios; [1] a launch that fills the GPU (sha256_grid's fill
 // tiers, config 4), where one lane's SIMD time is what the others queue behind: above
-// them (DESIGN.md §4 "Latency tiers", profiles/r05_v24_v25_tiers_ab.txt).  Test hooks
+// them (DESIGN.md §4 "Latency tiers", profiles/r05_v24_v26_tiers_ab.txt).  Test hooks
 // cg_test_sha_tiers / cg_test_sha_tiers_fill (quad_pm 0 = off: every chunk on the widest
 // tier the grid holds).
 uint32_t g_sha_tier_quad_pm[2] = {850, 950};

@@ -1,13 +1,12 @@
 cd "${GRAFT_REPO_ROOT:-.}"; export TMPDIR=/tmp; mkdir -p gpurun_out
-T=r05_v26
-out=gpurun_out/${T}_tiers_fill_ab.txt
-: > $out
+T=r05_v31
+timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_robust.py -m gpu > gpurun_out/${T}_robust.log 2>&1 || { tail -30 gpurun_out/${T}_robust.log; exit 1; }
+tail -1 gpurun_out/${T}_robust.log
 for rep in 1 2; do
-for cd in c4:4:850,600,950,700 c4:4:850,600,980,750 c4:4:850,600,1000,800 c4:4:850,600,1000,1000 c4:4:850,600,980,600 c4:4:850,600,0,0 c4:2:850,600,950,700 c4:8:850,600,950,700; do
-    IFS=: read cfg d t <<< "$cd"
-    f=gpurun_out/${T}_${cfg}_d${d}_t${t//,/_}_$rep
-    timeout -k 10 240 python -u bench.py --config $cfg --steps 20 --warmup 5 --depth $d --sha-tiers $t --no-cpu-baseline \
-      --no-concurrent --drop-in '' --e2e '' --no-clock > $f.json 2> $f.err || exit $?
-    python3 scripts/depth_row.py $f.json $cfg "$d t$t" | tee -a $out
-done
+timeout -k 10 400 python -u bench.py --concurrent-only --concurrent 8,12,16,32 --concurrent-reps 6 > gpurun_out/${T}_conc_$rep.json 2> gpurun_out/${T}_conc_$rep.err || exit 1
+python3 -c "
+import json;d=json.load(open('gpurun_out/${T}_conc_$rep.json'))['concurrent']
+for k in ('K8','K12','K16','K32'):
+    x=d[k+'_detail'];print(k, d[k], 'merged', x['merged']['GiBps'], x['merged']['p50'], x['merged']['p99'], x['merged']['coalescer']['groups'], 'per_batch', x['per_batch']['GiBps'], x['per_batch']['p50'], x['per_batch']['p99'])
+"
 done

@@ -2,8 +2,9 @@
 
 Runs with GPU_MAX_HW_QUEUES=16 set by the parent before anything in this process touches
 HIP (HIP reads the variable once, at initialisation; the library sizes its stream lanes
-from the value it saw at load, stream.hip g_hw_queues_at_load): 8 concurrent callers of
-the synchronous device entry (12 merged, 8 per-batch, 12 with coalescing off), and a
+from the value it saw at load, stream.hip g_hw_queues_at_load): concurrent callers of
+the synchronous device entry (20 merged -- past the 12 callers 16 queues run side by
+side, runtime.hip coal_min --, 12 per-batch, 12 with coalescing off), and a
 ChunkStream whose 8 digest
 lanes (queues - 2) each hold a HIP stream of their own -- every result checked against
 the oracle.  Prints one line "hw16 ok ..." on success; any mismatch raises."""
@@ -84,8 +85,19 @@ def stream_with_all_lanes():
 if __name__ == "__main__":
     assert os.environ.get("GPU_MAX_HW_QUEUES") == "16", "the parent sets GPU_MAX_HW_QUEUES=16"
     torch.cuda.set_device(0)
-    concurrent_callers(12, 1, seed=21)  # more than CG_COAL_MIN (8) callers: merged digests
-    concurrent_callers(8, 1, seed=23)   # per-batch launches (coalescing on, too few callers)
+    import ctypes
+
+    def groups():
+        out = (ctypes.c_uint64 * 4)()
+        ca.lib.cg_coalesce_stats(out)
+        return int(out[0])
+
+    g0 = groups()
+    concurrent_callers(12, 1, seed=23)  # per-batch launches (coalescing on, no more callers than coal_min)
+    g1 = groups()
+    assert g1 == g0, ("12 callers at 16 queues merged", g0, g1)
+    concurrent_callers(20, 1, seed=21)  # more callers than coal_min: merged digests
+    assert groups() > g1, "20 callers at 16 queues formed no merged group"
     concurrent_callers(12, 0, seed=22)
     n = stream_with_all_lanes()
-    print(f"hw16 ok: 12 / 8 callers coalesced + per-batch, ChunkStream {n} chunks")
+    print(f"hw16 ok: 20 / 12 callers coalesced + per-batch, ChunkStream {n} chunks")

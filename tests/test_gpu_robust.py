@@ -192,9 +192,10 @@ def _coal_stats(ca):
 
 def test_lone_and_few_callers_never_wait_for_the_window(ca, O):
     """The coalescer's latency cost: a lone SHA-256 caller, calling
-    back to back, and up to CG_COAL_MIN (8) concurrent callers never enter a merged group,
-    so no leader window delays them (cg_coalesce_stats: no group formed, no window run
-    out); more than 8 callers do form groups, and every result is oracle-exact."""
+    back to back, and no more concurrent callers than per-batch launches run side by side
+    (runtime.hip coal_min: 4 at HIP's default 4 hardware queues) never enter a merged group, so no leader window
+    delays them (cg_coalesce_stats: no group formed, no window run out); 12 callers do form
+    groups, and every result is oracle-exact."""
     import torch
 
     old = ca.lib.cg_test_coalesce(1)
@@ -228,8 +229,8 @@ def test_lone_and_few_callers_never_wait_for_the_window(ca, O):
 
 def test_sixteen_hardware_queues():
     """The deployment setting DESIGN.md §7 / INTEGRATION.md recommend for concurrent
-    callers, GPU_MAX_HW_QUEUES=16, in a fresh process (HIP reads it once, at start): 12
-    concurrent device callers with merged digests, 8 with per-batch launches, 12 with
+    callers, GPU_MAX_HW_QUEUES=16, in a fresh process (HIP reads it once, at start): 20
+    concurrent device callers with merged digests, 12 with per-batch launches, 12 with
     coalescing off, and a ChunkStream using
     all 8 of its digest lanes (one HIP stream each, queues - 2), all oracle-exact
     (tests/hw16_child.py)."""
@@ -246,7 +247,7 @@ def test_coalesced_spin_guard_reaches_every_member(ca):
     """A spin-guard expiry inside a merged digest fails every member's call with CG_E_IO
     (the merged launch's error word is copied into each member's), and the next round is
     exact again."""
-    jobs = _coalesced_jobs(ca, 12, seed=9)  # more than CG_COAL_MIN (8): the merged path
+    jobs = _coalesced_jobs(ca, 12, seed=9)  # more callers than hardware queues: the merged path
     old = ca.lib.cg_test_sha_spin_limit(0)
     try:
         _, errors = _run_threads(ca, jobs)
