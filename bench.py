@@ -97,6 +97,8 @@ def parse_args():
     ap.add_argument("--sha-tiers", default="",
                     help="SHA-256 latency tiers 'QUAD_PM,PAIR_PM[,FILL_QUAD_PM,FILL_PAIR_PM]' (cg_test_sha_tiers, "
                          "cg_test_sha_tiers_fill; quad 0 = off; '' = the library's)")
+    ap.add_argument("--profile-rest", type=float, default=0.0,
+                    help="seconds the GPU idles between the timed region and the per-stage profile steps")
     ap.add_argument("--no-coalesce", action="store_true",
                     help="concurrent callers digest their batches alone (cg_test_coalesce(0)); A/B of the coalescer")
     ap.add_argument("--dist-force", action="store_true",
@@ -290,6 +292,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ca.lib.cg_set_profiling(1)
+    time.sleep(args.profile_rest)  # (A/B: clocks after the pipelined timed region)
     prof = np.zeros((PROFILE_STEPS, 5))
     for k in range(PROFILE_STEPS):
         step(last)

@@ -1,12 +1,12 @@
 cd "${GRAFT_REPO_ROOT:-.}"; export TMPDIR=/tmp; mkdir -p gpurun_out
-T=r05_v31
-timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_robust.py -m gpu > gpurun_out/${T}_robust.log 2>&1 || { tail -30 gpurun_out/${T}_robust.log; exit 1; }
-tail -1 gpurun_out/${T}_robust.log
+T=r05_v32
 for rep in 1 2; do
-timeout -k 10 400 python -u bench.py --concurrent-only --concurrent 8,12,16,32 --concurrent-reps 6 > gpurun_out/${T}_conc_$rep.json 2> gpurun_out/${T}_conc_$rep.err || exit 1
-python3 -c "
-import json;d=json.load(open('gpurun_out/${T}_conc_$rep.json'))['concurrent']
-for k in ('K8','K12','K16','K32'):
-    x=d[k+'_detail'];print(k, d[k], 'merged', x['merged']['GiBps'], x['merged']['p50'], x['merged']['p99'], x['merged']['coalescer']['groups'], 'per_batch', x['per_batch']['GiBps'], x['per_batch']['p50'], x['per_batch']['p99'])
-"
+for cd in 1:0 10:0 10:1 10:3; do
+    IFS=: read d r <<< "$cd"
+    f=gpurun_out/${T}_c2_d${d}_rest${r}_$rep
+    timeout -k 10 240 python -u bench.py --config c2 --steps 20 --warmup 5 --depth $d --profile-rest $r --no-cpu-baseline \
+      --no-concurrent --drop-in '' --e2e '' --no-clock > $f.json 2> $f.err || exit $?
+    python3 -c "
+import json,sys;d=json.load(open(sys.argv[1]));print(sys.argv[1], d['value'], d['stages_ms']['scan'], d['roofline']['scan_kernel']['cold_hbm']['ms'])" $f.json
+done
 done
