@@ -97,8 +97,8 @@ def parse_args():
     ap.add_argument("--sha-tiers", default="",
                     help="SHA-256 latency tiers 'QUAD_PM,PAIR_PM[,FILL_QUAD_PM,FILL_PAIR_PM]' (cg_test_sha_tiers, "
                          "cg_test_sha_tiers_fill; quad 0 = off; '' = the library's)")
-    ap.add_argument("--profile-rest", type=float, default=0.0,
-                    help="seconds the GPU idles between the timed region and the per-stage profile steps")
+    ap.add_argument("--profile-after", action="store_true",
+                    help="time the stages (PROFILE_STEPS single steps) after the timed region instead of before it")
     ap.add_argument("--no-coalesce", action="store_true",
                     help="concurrent callers digest their batches alone (cg_test_coalesce(0)); A/B of the coalescer")
     ap.add_argument("--dist-force", action="store_true",
@@ -268,11 +268,39 @@ def main():
     # on the stream the kernels run on (cg_set_profiling(2)), live inside the timed region
     # (each step already ends in a stream sync for the NAR->chunk index, so reading them
     # adds only host bookkeeping).  A timing event between two kernels holds the second
-    # back by ~6 us, so the other stages are timed on PROFILE_STEPS untimed steps after
+    # back by ~6 us, so the other stages are timed on PROFILE_STEPS untimed steps before
     # the timed region (cg_set_profiling(1), every stage boundary an event).
+    def profile_stages(k_out):
+        """Every stage timed (cg_set_profiling(1)) on PROFILE_STEPS single steps, then the
+        scan stage right after a 2 GiB write (the 256 MB MALL holds none of the batch): the
+        cold-HBM rate, reported beside the warm one (the previous digest just read the batch)."""
+        ca.lib.cg_set_profiling(1)
+        prof = np.zeros((PROFILE_STEPS, 5))
+        for k in range(PROFILE_STEPS):
+            step(k_out)
+            ca.lib.cg_last_stage_times(buf, 5)
+            prof[k] = list(buf)
+        cold = np.zeros(PROFILE_STEPS)
+        scratch = torch.empty(2 * GIB, dtype=torch.uint8, device="cuda")
+        for k in range(PROFILE_STEPS):
+            scratch.fill_(k)
+            torch.cuda.synchronize()
+            step(k_out)
+            ca.lib.cg_last_stage_times(buf, 5)
+            cold[k] = buf[0]
+        del scratch
+        ca.lib.cg_set_profiling(0)
+        return prof, cold
+
+    # The stage profile runs before the timed region (after the warm-up): run after a deep
+    # pipelined region every stage's events read 20-200 % longer (scan 0.239-0.253 vs
+    # 0.198 ms, compact 0.057 vs 0.017; profiles/r05_v33_profile_order.txt) -- the events'
+    # timestamps, not the kernels: the same single steps before it match one batch at a time.
+    buf = (np.ctypeslib.ctypes.c_double * 5)()
+    if not args.profile_after:
+        pre_prof = profile_stages(0)
     ca.lib.cg_set_profiling(2)
     stage = np.zeros((max(args.steps, 1), 5))
-    buf = (np.ctypeslib.ctypes.c_double * 5)()
     torch.cuda.synchronize()
     if multi:
         dist.barrier()
@@ -291,25 +319,7 @@ def main():
     if multi:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ca.lib.cg_set_profiling(1)
-    time.sleep(args.profile_rest)  # (A/B: clocks after the pipelined timed region)
-    prof = np.zeros((PROFILE_STEPS, 5))
-    for k in range(PROFILE_STEPS):
-        step(last)
-        ca.lib.cg_last_stage_times(buf, 5)
-        prof[k] = list(buf)
-    # The scan stage right after a 2 GiB write (the 256 MB MALL holds none of the batch): the
-    # cold-HBM rate, reported beside the warm pipeline's (the digest just read the batch)
-    cold = np.zeros(PROFILE_STEPS)
-    scratch = torch.empty(2 * GIB, dtype=torch.uint8, device="cuda")
-    for k in range(PROFILE_STEPS):
-        scratch.fill_(k)
-        torch.cuda.synchronize()
-        step(last)
-        ca.lib.cg_last_stage_times(buf, 5)
-        cold[k] = buf[0]
-    del scratch
-    ca.lib.cg_set_profiling(0)
+    prof, cold = profile_stages(last) if args.profile_after else pre_prof
     if multi:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if nccl else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -347,7 +357,7 @@ def main():
         "traffic": None,
         "note": "digest stage: algorithmic bytes = every NAR byte once, / mean digest-stage duration over the "
                 "timed steps (HIP events around the digest only); scan stage (scan_kernel) from "
-                f"{PROFILE_STEPS} untimed steps with every stage timed",
+                f"{PROFILE_STEPS} untimed single steps with every stage timed, before the timed region",
         "scan_kernel": {"kernel": scan_kernel_name(ca, params[1], total_bytes),
                         "achieved": round(total_bytes / (scan_ms * 1e-3) / 1e9, 2),
                         "frac": round(total_bytes / (scan_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -596,26 +606,29 @@ def e2e_rates(ca, torch, args, n_per, nar_bytes, params, algo, want):
                 f"e2e batch {k}: descriptors differ from the device-resident run"
         res[f"K{K}"] = round(K * reps * nbytes / dt / GIB, 3)
     if algo == 1:
-        res["one_caller_overlapped"] = e2e_one_caller(ca, torch, bufs, offs, nbytes, cap, n_per, params, algo, want)
+        res["one_caller_overlapped"] = e2e_one_caller(ca, torch, bufs, offs, nbytes, cap, n_per, params, algo, want,
+                                                      args.depth or default_depth(algo, nbytes))
     return res
 
 
-def e2e_one_caller(ca, torch, bufs, offs, nbytes, cap, n_per, params, algo, want, reps=8):
-    """Host to host from ONE caller thread with two batches in flight: batch k's pinned H2D
-    copy runs on a copy stream, its inputs-ready event orders the batch
-    (cg_chunk_batch_device_async_after), so the copy and the batch overlap the previous
-    batch's digest; the descriptors come back D2H after its wait.  Two device input and
-    output buffers alternate; batch k + 2 is issued only after batch k was waited for and
-    its descriptors copied out.  GiB/s = reps x batch bytes / wall time."""
+def e2e_one_caller(ca, torch, bufs, offs, nbytes, cap, n_per, params, algo, want, depth=2):
+    """Host to host from ONE caller thread with `depth` batches in flight (bench.py's
+    default_depth for the config): batch k's pinned H2D copy runs on a copy stream, its
+    inputs-ready event orders the batch (cg_chunk_batch_device_async_after), so the copy and
+    the batch overlap the batches before it; the descriptors come back D2H after its wait.
+    `depth` device input and output buffers are used in turn; batch k + depth is issued only
+    after batch k was waited for and its descriptors copied out.  GiB/s = reps x batch
+    bytes / wall time, reps = max(8, 2 x depth)."""
     host = bufs[0][0]
-    dins = [torch.empty(nbytes + 256, dtype=torch.uint8, device="cuda") for _ in range(2)]
-    douts = [torch.empty(cap * 48, dtype=torch.uint8, device="cuda") for _ in range(2)]
-    outs = [np.zeros(cap * 48, np.uint8) for _ in range(2)]
+    reps = max(8, 2 * depth)
+    dins = [torch.empty(nbytes + 256, dtype=torch.uint8, device="cuda") for _ in range(depth)]
+    douts = [torch.empty(cap * 48, dtype=torch.uint8, device="cuda") for _ in range(depth)]
+    outs = [np.zeros(cap * 48, np.uint8) for _ in range(depth)]
     copy = torch.cuda.Stream()
     bstream = torch.cuda.Stream()
 
     def issue(k):
-        j = k % 2
+        j = k % depth
         with torch.cuda.stream(copy):
             dins[j][:nbytes].copy_(host, non_blocking=True)
             ev = torch.cuda.Event()
@@ -626,24 +639,26 @@ def e2e_one_caller(ca, torch, bufs, offs, nbytes, cap, n_per, params, algo, want
     def complete(k, h):
         first = h[0].wait()
         n = int(first[-1])
-        j = k % 2
+        j = k % depth
         outs[j][: n * 48] = douts[j][: n * 48].cpu().numpy()
         return n
 
     for timed in (False, True):
-        count = reps if timed else 2
+        count = reps if timed else depth
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        pending = issue(0)
-        for k in range(count):
-            nxt = issue(k + 1) if k + 1 < count else None
-            n = complete(k, pending)
-            pending = nxt
+        q = deque()
+        for k in range(count + depth - 1):
+            if k < count:
+                q.append((k, issue(k)))
+            if len(q) == depth or (k >= count and q):
+                kk, h = q.popleft()
+                n = complete(kk, h)
         dt = time.perf_counter() - t0
-    assert n == len(want) and np.array_equal(outs[(count - 1) % 2][: n * 48], want.view(np.uint8)), \
+    assert n == len(want) and np.array_equal(outs[(count - 1) % depth][: n * 48], want.view(np.uint8)), \
         "e2e one caller: descriptors differ from the device-resident run"
-    return {"GiBps": round(reps * nbytes / dt / GIB, 3), "reps": reps,
-            "shape": "one thread, two batches in flight: pinned H2D on a copy stream -> inputs-ready event -> "
+    return {"GiBps": round(reps * nbytes / dt / GIB, 3), "reps": reps, "depth": depth,
+            "shape": f"one thread, {depth} batches in flight: pinned H2D on a copy stream -> inputs-ready event -> "
                      "cg_chunk_batch_device_async_after -> wait -> descriptors D2H"}
 
 
