@@ -168,7 +168,8 @@ bool launch_assemble(const uint64_t *d_nar_off, const uint64_t *d_cap_base, cons
 // by the caller) becomes nonzero if a producer/consumer hand-off hit its spin guard.
 void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
                    uint64_t max_chunks, uint64_t expected, uint64_t max_len, uint32_t *d_order_tmp,
-                   uint8_t *d_hash_base, size_t hash_stride, uint32_t *d_err, hipStream_t st);
+                   uint8_t *d_hash_base, size_t hash_stride, uint32_t *d_err, hipStream_t st,
+                   bool latency_tiers = true);
 size_t sha256_order_tmp_elems(uint64_t max_chunks);
 
 // Coalesced SHA-256 digest (runtime.hip's per-device coalescer): the chunks of up to

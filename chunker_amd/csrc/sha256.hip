@@ -1022,7 +1022,8 @@ thread_local uint32_t t_sha_tiers[4];
 
 void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
                    uint64_t max_chunks, uint64_t expected, uint64_t max_len, uint32_t *d_order_tmp,
-                   uint8_t *d_hash_base, size_t hash_stride, uint32_t *d_err, hipStream_t st) {
+                   uint8_t *d_hash_base, size_t hash_stride, uint32_t *d_err, hipStream_t st,
+                   bool latency_tiers) {
     if (max_chunks == 0) return;
     uint32_t nquad = 0, npair = 0;
     bool fill = false;
@@ -1030,7 +1031,7 @@ void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
     // one workgroup has nothing to balance
     // latency tiers: k_len_base counts the chunks that need a quad / a pair into the two
     // words after the order (sha256_order_tmp_elems' slack)
-    const uint32_t qpm = g_sha_tier_quad_pm[fill], ppm = g_sha_tier_pair_pm[fill];
+    const uint32_t qpm = latency_tiers ? g_sha_tier_quad_pm[fill] : 0u, ppm = g_sha_tier_pair_pm[fill];
     uint32_t *need = max_chunks > 8 && d_order_tmp && qpm ? d_order_tmp + SHA_NBKT + max_chunks : nullptr;
     const uint32_t *order = max_chunks > 8
                                 ? launch_len_order(d_desc, d_total, max_chunks, max_len, d_order_tmp, st, need, qpm, ppm)

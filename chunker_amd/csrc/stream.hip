@@ -241,8 +241,12 @@ int launch_open(cg_stream *h) {
     const uint64_t *d_total = l.total.as<uint64_t>();
     if (h->algo == CG_SHA256) {
         if ((rc = l.ensure(l.order, cg::sha256_order_tmp_elems(n) * 4, "order"))) return rc;
+        // (no latency tiers: a stream's rate is its groups' chains one after another, and a
+        // one-lane chain sharing the CUs with the next slices' scans ran slower than the quad
+        // it replaced -- 1 / 4 GiB at 4 queues 9.86 / 10.20 -> 8.92 / 8.74 GiB/s with them,
+        // profiles/r05_v36_stream_tiers_ab.txt)
         cg::launch_sha256(base, l.abs.as<uint64_t>(), l.desc.p, d_total, n, n, h->o.max, l.order.as<uint32_t>(), hb,
-                          sizeof(cg_desc), l.err.as<uint32_t>(), l.st);
+                          sizeof(cg_desc), l.err.as<uint32_t>(), l.st, /*latency_tiers=*/false);
     } else {
         const uint64_t gb = cg::blake3_group_bound(g.bytes, n);
         if ((rc = l.ensure(l.b3_gcount, (n + 1) * 4, "b3_gcount"))) return rc;

@@ -24,11 +24,14 @@ SL = 8 << 20
 shapes = [(0, 0), (1, 0), (1, 2), (2, 0), (2, 2)]  # (max lanes, eager mode); lanes 0 = the built-in rule
 if "--shapes" in sys.argv:
     shapes = [tuple(int(v) for v in s.split(":")) for s in sys.argv[sys.argv.index("--shapes") + 1].split(",")]
+if "--tiers-off" in sys.argv:  # SHA-256 latency tiers off (A/B)
+    lib.cg_test_sha_tiers(0, 0)
+    lib.cg_test_sha_tiers_fill(0, 0)
 sizes = [1 << 30, 4 << 30]
 if "--sizes-gib" in sys.argv:
     sizes = [int(v) << 30 for v in sys.argv[sys.argv.index("--sizes-gib") + 1].split(",")]
 res = {"workload": "synthetic NAR stream, SHA-256, 256K/1M/4M, 8 MiB pushes, 2 GiB in-flight budget",
-       "hw_queues": os.environ["GPU_MAX_HW_QUEUES"], "rows": []}
+       "hw_queues": os.environ["GPU_MAX_HW_QUEUES"], "sha_tiers": "--tiers-off" not in sys.argv, "rows": []}
 
 
 def run(data, lanes, eager):
