@@ -111,23 +111,21 @@ def parse_args():
 
 
 def default_depth(algo: int, batch_bytes: int) -> int:
-    """Batches the one caller keeps in flight (DESIGN.md §7 "Batches in flight").
-    SHA-256 under 4 GiB a batch: 10.  Such a batch's digest is latency-bound -- every chunk
-    is one serial chain, config 2's longest is 52,345 blocks = 53 ms, and its ~1,000 chains
-    leave most of the chip idle -- so the batches queued behind it fill the chip instead
-    (config 2, 20 steps: 18.1 / 35.8 / 85 / 105 / 126 / 131 GiB/s at 1 / 2 / 6 / 8 / 10 /
-    12 in flight, per-batch p50 latency 55 -> 65-80 ms; profiles/r05_v22_depth_ab.txt).
-    SHA-256 from 4 GiB: 4 (configs 4 / 5: the digest fills the chip by itself and the
-    overlap hides the scan; 697 -> 703-727 and 324 -> 379-400 GiB/s from 2 to 4, within
-    noise beyond).  BLAKE3: 2 (its batches stay in stream order; the second one queued
-    covers the host's per-call work).  Each batch in flight runs on a HIP stream of its own,
-    so the depth is held to GPU_MAX_HW_QUEUES - 2 (the caller's stream and torch's take two
-    queues): at HIP's default 4 queues streams share them and config 2 stays at 36 GiB/s
-    whatever the depth (profiles/r05_v23_depth_ab.txt)."""
-    if algo != 1:
-        return 2
-    hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
-    return max(2, min(10 if batch_bytes < 4 * GIB else 4, hwq - 2))
+    """Batches the one caller keeps in flight: chunker_amd.default_depth (DESIGN.md §7
+    "Batches in flight").  SHA-256 under 4 GiB a batch: 10 -- such a batch's digest is
+    latency-bound, every chunk one serial chain (config 2's longest: 52,345 blocks = 53
+    ms), and with the latency tiers its ~1,000 chains take ~18 workgroups, so the batches
+    queued behind it fill the chip (config 2, 20 steps: 18.1 one at a time, 169.5 GiB/s
+    with ten, per-batch p50 latency 55 -> 58.5 ms; profiles/r05_v24_v26_tiers_ab.txt,
+    r05_v19_v23_depth_ab.txt before the tiers).  From 4 GiB: 4 (configs 4 / 5: the digest
+    fills the chip by itself and the overlap hides the scan).  BLAKE3: 2 (its batches stay
+    in stream order; the second one queued covers the host's per-call work).  Held to
+    GPU_MAX_HW_QUEUES - 2: each batch in flight runs on a HIP stream of its own, and at
+    HIP's default 4 queues config 2 stays at 36 GiB/s whatever the depth
+    (profiles/r05_v23 in r05_v19_v23_depth_ab.txt)."""
+    from chunker_amd.chunking import default_depth as rule
+
+    return rule(algo, batch_bytes)
 
 
 def launch_ranks(n: int) -> int:

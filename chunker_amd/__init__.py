@@ -7,7 +7,7 @@ Importing this package loads the in-tree HIP library and raises if it is missing
 from .chunking import (  # noqa: F401
     BoundsError, BufferLimitExceededError, ChunkDescriptor, ChunkingError, ChunkingOptions, ChunkMetadata,
     BlockingAsyncReadAdapter, ChunkStream, ChunkStreamAsync, DeviceUnavailableError, HashAlgorithm, InvalidOptionsError, IoError, PushChunker, TablesError,
-    BatchInFlight, ZeroLengthChunkError, chunk_batch, chunk_batch_device, chunk_batch_device_async, chunk_data, chunk_data_with_hash, chunk_descriptors,
+    BatchInFlight, BatchPipeline, ZeroLengthChunkError, default_depth, chunk_batch, chunk_batch_device, chunk_batch_device_async, chunk_data, chunk_data_with_hash, chunk_descriptors,
     chunk_descriptors_array, chunk_descriptors_with_hash, chunk_data_async, chunk_stream, chunk_stream_async, chunk_stream_blocking_adapter,
     chunk_stream_with_hash, get_cdc_tables, metrics,
     selftest, set_cdc_tables, tables_verified,

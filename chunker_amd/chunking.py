@@ -395,6 +395,82 @@ def chunk_batch_device_async(d_data_ptr: int, nar_offsets: np.ndarray, d_out_ptr
     return BatchInFlight(h.value, n)
 
 
+def default_depth(hash: HashAlgorithm, batch_bytes: int) -> int:
+    """Device batches one caller keeps in flight (DESIGN.md §7 "Batches in flight"):
+    SHA-256 under 4 GiB a batch 10 -- its digest is its longest chunk's serial chain on a
+    few workgroups (SHA-256 latency tiers), so the batches queued behind it fill the chip
+    (config 2: 18.1 GiB/s one at a time, 169.5 with ten, per-batch latency 55 -> 58.5 ms);
+    from 4 GiB 4 (the digest fills the chip; the overlap hides the scan); BLAKE3 2 (its
+    batches stay in stream order).  Every batch in flight holds a HIP stream, so the depth
+    is held to GPU_MAX_HW_QUEUES - 2 (HIP's default 4 queues: 2)."""
+    if HashAlgorithm(hash) != HashAlgorithm.Sha256:
+        return 2
+    try:
+        hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+    except ValueError:
+        hwq = 4
+    return max(2, min(10 if batch_bytes < (4 << 30) else 4, hwq - 2))
+
+
+class BatchPipeline:
+    """Up to `depth` device batches in flight from one thread (an ingest worker draining
+    NAR batches): submit() queues a batch after its inputs-ready event only
+    (cg_chunk_batch_device_async_after) and, once `depth` are queued, waits for the oldest
+    and returns it; drain() waits for the rest.  Results come back in submission order as
+    (tag, nar_first).  The caller owns the buffers: a batch's input and output arrays must
+    stay untouched until its result has been returned (one output array per batch in
+    flight).  depth None = default_depth for the first batch's size."""
+
+    def __init__(self, depth: int | None = None, min_size=None, avg_size=None, max_size=None,
+                 hash: HashAlgorithm = HashAlgorithm.Sha256, stream: int = 0):
+        if depth is not None and depth < 1:
+            raise InvalidOptionsError(f"pipeline depth must be at least 1, got {depth}")
+        self.depth = depth
+        self.options = ChunkingOptions.resolve(min_size, avg_size, max_size)
+        self.hash = HashAlgorithm(hash)
+        self.stream = stream
+        self._q: deque = deque()
+
+    def submit(self, d_data_ptr: int, nar_offsets: np.ndarray, d_out_ptr: int, out_cap: int,
+               inputs_ready: int = 0, tag=None) -> list:
+        offs = np.ascontiguousarray(nar_offsets, dtype=np.uint64)
+        if self.depth is None:
+            self.depth = default_depth(self.hash, int(offs[-1]) if len(offs) else 0)
+        o = self.options
+        b = chunk_batch_device_async(d_data_ptr, offs, d_out_ptr, out_cap, o.min_size, o.avg_size, o.max_size,
+                                     hash=self.hash, stream=self.stream, inputs_ready=inputs_ready)
+        self._q.append((tag, b))
+        done = []
+        while len(self._q) >= self.depth:
+            t, oldest = self._q.popleft()
+            done.append((t, oldest.wait()))
+        return done
+
+    def drain(self) -> list:
+        done = []
+        while self._q:
+            t, b = self._q.popleft()
+            done.append((t, b.wait()))
+        return done
+
+    def __len__(self) -> int:
+        return len(self._q)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        # wait for everything queued, whatever happened (the workspaces go back to the pool)
+        while self._q:
+            _, b = self._q.popleft()
+            try:
+                b.wait()
+            except ChunkingError:
+                if exc[0] is None:
+                    raise
+        return False
+
+
 def batch_capacity(nar_offsets: np.ndarray, min_size=None) -> int:
     m = DEFAULT_MIN if min_size is None else int(min_size)
     lens = np.diff(np.asarray(nar_offsets, dtype=np.uint64))

@@ -909,3 +909,60 @@ def test_async_after_inputs_ready_matches_sync(ca, O, mode):
         want = O.chunk_descriptors(data[offs[12]:offs[13]], 16384, 65536, 262144, algo=algo)
         assert_same(descs[int(first[12]):int(first[13])], want, f"batch{k} nar12")
     ca.lib.cg_test_split_mode(old_mode)
+
+
+@pytest.mark.parametrize("depth", [None, 1, 3], ids=["default", "one", "three"])
+def test_batch_pipeline_matches_sync(ca, O, depth):
+    """chunker_amd.BatchPipeline (one thread, up to `depth` batches in flight, each after
+    its own inputs-ready event, DESIGN.md §7 "Batches in flight"): twelve SHA-256 batches
+    through one pipeline (default depth: 2 at this process's 4 hardware queues; with fewer
+    output arrays than the depth the test drains early) come back in submission order, each
+    equal to the synchronous entry, with the oracle on a sampled NAR; the output arrays
+    rotate, each reused only after its batch was returned."""
+    import torch
+
+    from chunker_amd.nar import synth_nars
+
+    sizes = [2 << 20] * 6 + [12345 * 8, 300_008]
+    data, offs = synth_nars(sizes, first_index=77)
+    cap = ca.chunking.batch_capacity(offs, 16384)
+    d = torch.from_numpy(np.concatenate([data, np.zeros(256, np.uint8)])).cuda()
+    ref_out = torch.zeros(cap * 48, dtype=torch.uint8, device="cuda")
+    ref_first = ca.chunk_batch_device(d.data_ptr(), offs, ref_out.data_ptr(), cap, 16384, 65536, 262144)
+    ref = ref_out.cpu().numpy()
+    n_out = 4 if depth is None else depth + 1
+    outs = [torch.full((cap * 48,), 0xAB, dtype=torch.uint8, device="cuda") for _ in range(n_out)]
+    ready = torch.cuda.Event()
+    ready.record()
+    stream = torch.cuda.Stream()
+    results = []
+    free = list(range(n_out))
+    busy = {}
+    with ca.BatchPipeline(depth, 16384, 65536, 262144, stream=stream.cuda_stream) as pipe:
+        for k in range(12):
+            j = free.pop(0)
+            busy[k] = j
+            for tag, first in pipe.submit(d.data_ptr(), offs, outs[j].data_ptr(), cap, inputs_ready=ready.cuda_event,
+                                          tag=k):
+                results.append((tag, first, outs[busy[tag]].cpu().numpy()))
+                free.append(busy.pop(tag))
+            if not free:  # more batches in flight than output arrays: take the oldest back
+                for tag, first in pipe.drain():
+                    results.append((tag, first, outs[busy[tag]].cpu().numpy()))
+                    free.append(busy.pop(tag))
+        for tag, first in pipe.drain():
+            results.append((tag, first, outs[busy[tag]].cpu().numpy()))
+    assert [t for t, _, _ in results] == list(range(12))
+    n = int(ref_first[-1])
+    want = O.chunk_descriptors(data[offs[6]:offs[7]], 16384, 65536, 262144, algo=SHA)
+    for k, first, got in results:
+        assert np.array_equal(first, ref_first), k
+        assert np.array_equal(got[: n * 48], ref[: n * 48]), k
+        assert_same(got.view(ca.DESC_DTYPE)[int(first[6]):int(first[7])], want, f"batch{k} nar6")
+
+
+def test_batch_pipeline_depth_rule(ca):
+    """default_depth (the pipeline's and bench.py's rule) and the pipeline's option checks."""
+    assert ca.default_depth(ca.HashAlgorithm.Blake3, 1 << 30) == 2
+    with pytest.raises(ca.InvalidOptionsError):
+        ca.BatchPipeline(0)
