@@ -124,12 +124,11 @@ struct Workspace {
     // behind it on the same stream must not be waited for too)
     hipEvent_t ev_done = nullptr;
     // A SHA-256 batch queued with an inputs-ready event (cg_chunk_batch_device_async_after)
-    // runs on bound_stream, ordered after that event only, beside the batch queued before
-    // it on the caller's stream, which then waits for its done event.  Split mode 1 (A/B):
-    // only the boundary stages run there; ev_bdone (recorded after the assembly) holds the
-    // digest on the caller's stream back, and ev_dstart (after that wait) opens the digest
-    // stage's timing.
-    hipStream_t bound_stream = nullptr;
+    // runs on the workspace's own `stream` (idle while an async batch holds the workspace),
+    // ordered after that event only, beside the batches queued before it on the caller's
+    // stream, which then waits for its done event.  Split mode 1 (A/B): only the boundary
+    // stages run there; ev_bdone (recorded after the assembly) holds the digest on the
+    // caller's stream back, and ev_dstart (after that wait) opens the digest stage's timing.
     hipEvent_t ev_bdone = nullptr, ev_dstart = nullptr;
     // Streams map onto the process's few hardware queues (GPU_MAX_HW_QUEUES, 4 by default)
     // and two streams on one queue serialise: the side stream exists only where used.
@@ -137,7 +136,6 @@ struct Workspace {
         if (!side_stream) HIP_TRY(hipStreamCreateWithFlags(&side_stream, hipStreamNonBlocking));
         return CG_OK;
     }
-    int ensure_bound_stream();
     int init(int dev) {
         device = dev;
         HIP_TRY(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));

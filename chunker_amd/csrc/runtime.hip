@@ -629,14 +629,6 @@ int ensure_pass_buffers(Workspace *ws, uint64_t total_len, size_t n_nars, uint64
     return CG_OK;
 }
 
-// The stream an overlapped batch runs on (cg_chunk_batch_device_async_after), one per
-// workspace.  (Measured without gain and removed since, commit 686ad6b: this stream at the
-// highest priority, restricted to 32 / 64 CUs, the digest on a CU-masked stream of its own,
-// profiles/r05_v3_split_ab.txt, r05_v12_cumask_ab.txt, r05_v16_v17_stagger_ab.txt.)
-int Workspace::ensure_bound_stream() {
-    if (!bound_stream) HIP_TRY(hipStreamCreateWithFlags(&bound_stream, hipStreamNonBlocking));
-    return CG_OK;
-}
 
 // The persistent scan's queue: allocated and zeroed (on the batch's stream, ahead of its
 // first scan) once per workspace; every scan launch leaves it zeroed again.
@@ -793,16 +785,19 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
     if ((rc = ensure_gear(ws, *tab))) return rc;
     if ((rc = ensure_pass_buffers(ws, total_len, n_nars, total_cap, chunk_bound, slots, algo))) return rc;
     // The boundary stages' stream: `st` itself, or -- with an inputs-ready event -- the
-    // workspace's bound_stream, ordered after that event only, so the stages (and, in split
+    // workspace's own stream, ordered after that event only, so the stages (and, in split
     // mode 2, the digest: `ds` below) run beside the digest of the batch queued before on
-    // `st`, which reads another workspace.
+    // `st`, which reads another workspace.  (One stream per workspace: streams beyond the
+    // hardware queues share them and serialise; a second, dedicated stream per workspace
+    // measured no better, profiles/r05_v40_one_stream_ab.txt.  Without gain either, commit 686ad6b: that
+    // stream at the highest priority, restricted to 32 / 64 CUs, the digest on a CU-masked
+    // stream, profiles/r05_v3_split_ab.txt, r05_v12_cumask_ab.txt, r05_v16_v17_stagger_ab.txt.)
     // (BLAKE3 batches stay in stream order: their digest fills the chip by itself, and
     // overlapping it with the next batch measured 1.7 % slower on config 3,
     // profiles/r05_v3_split_ab.txt; waiting for more than inputs_ready is always allowed)
     hipStream_t bs = st;
     if (inputs_ready && algo == CG_SHA256) {
-        if ((rc = ws->ensure_bound_stream())) return rc;
-        bs = ws->bound_stream;
+        bs = ws->stream;
         HIP_TRY(hipStreamWaitEvent(bs, inputs_ready, 0));
     }
     if ((rc = ensure_scan_queue(ws, bs))) return rc;
@@ -1452,7 +1447,7 @@ int cg_chunk_batch_device_async_after(const uint8_t *d_data, const uint64_t *nar
                       false, static_cast<hipEvent_t>(inputs_ready));
     if (rc) {
         (void)hipStreamSynchronize(st);
-        if (ws->bound_stream) (void)hipStreamSynchronize(ws->bound_stream);
+        (void)hipStreamSynchronize(ws->stream);
         release(ws);
         return rc;
     }
