@@ -789,9 +789,10 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
     // mode 2, the digest: `ds` below) run beside the digest of the batch queued before on
     // `st`, which reads another workspace.  (One stream per workspace: streams beyond the
     // hardware queues share them and serialise; a second, dedicated stream per workspace
-    // measured no better, profiles/r05_v40_one_stream_ab.txt.  Without gain either, commit 686ad6b: that
-    // stream at the highest priority, restricted to 32 / 64 CUs, the digest on a CU-masked
-    // stream, profiles/r05_v3_split_ab.txt, r05_v12_cumask_ab.txt, r05_v16_v17_stagger_ab.txt.)
+    // measured no better, profiles/r05_v40_one_stream_ab.txt.  Without gain either, commit
+    // 686ad6b: that stream at the highest priority, restricted to 32 / 64 CUs, the digest
+    // on a CU-masked stream; profiles/r05_v3_split_ab.txt, r05_v12_cumask_ab.txt,
+    // r05_v16_v17_stagger_ab.txt.)
     // (BLAKE3 batches stay in stream order: their digest fills the chip by itself, and
     // overlapping it with the next batch measured 1.7 % slower on config 3,
     // profiles/r05_v3_split_ab.txt; waiting for more than inputs_ready is always allowed)
