@@ -99,8 +99,6 @@ def parse_args():
                          "cg_test_sha_tiers_fill; quad 0 = off; '' = the library's)")
     ap.add_argument("--profile-after", action="store_true",
                     help="time the stages (PROFILE_STEPS single steps) after the timed region instead of before it")
-    ap.add_argument("--sha-solo", default="",
-                    help="SHA-256 solo tier 'LATENCY_PM,FILL_PM' (cg_test_sha_solo; 0 = off; '' = the library's)")
     ap.add_argument("--no-coalesce", action="store_true",
                     help="concurrent callers digest their batches alone (cg_test_coalesce(0)); A/B of the coalescer")
     ap.add_argument("--dist-force", action="store_true",
@@ -188,8 +186,6 @@ def main():
         ca.lib.cg_test_sha_tiers(t[0], t[1])
         if len(t) == 4:
             ca.lib.cg_test_sha_tiers_fill(t[2], t[3])
-    if args.sha_solo:
-        ca.lib.cg_test_sha_solo(*(int(v) for v in args.sha_solo.split(",")))
     if args.concurrent_only:
         print(json.dumps({"concurrent": concurrent_rates(ca, torch, args, n_per, nar_bytes, params, algo)}))
         return

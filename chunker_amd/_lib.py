@@ -54,7 +54,7 @@ TEST_HOOKS = ("cg_test_sha_quad_max", "cg_test_sha_split_max", "cg_test_sha_spin
               "cg_test_fail_alloc", "cg_test_sha_quad_fill", "cg_test_sha_pair_fill", "cg_test_scan_path", "cg_test_scan_kernel", "cg_test_coalesce", "cg_test_scan_grid",
               "cg_test_stream_group_cap", "cg_test_stream_max_lanes", "cg_test_stream_eager",
               "cg_test_b3_fused_plan", "cg_test_b3_packed", "cg_coalesce_stats",
-              "cg_test_split_mode", "cg_test_sha_tiers", "cg_test_sha_tiers_fill", "cg_test_sha_solo")
+              "cg_test_split_mode", "cg_test_sha_tiers", "cg_test_sha_tiers_fill")
 
 
 def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
@@ -146,7 +146,7 @@ def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
                  "cg_test_sha_pair_fill", "cg_test_scan_path", "cg_test_scan_kernel", "cg_test_coalesce"):
         getattr(L, name).argtypes = [u32]
         getattr(L, name).restype = u32
-    for name in ("cg_test_sha_tiers", "cg_test_sha_tiers_fill", "cg_test_sha_solo"):
+    for name in ("cg_test_sha_tiers", "cg_test_sha_tiers_fill"):
         getattr(L, name).argtypes = [u32, u32]
         getattr(L, name).restype = u32
     L.cg_test_scan_grid.argtypes = [u64]

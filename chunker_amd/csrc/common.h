@@ -198,7 +198,7 @@ void launch_sha256_coalesced(const CoalTable &t, uint64_t bound_sum, uint64_t ex
 // d_need (2 u32, optional): the latency-tier counts for k_sha256 (k_len_base).
 const uint32_t *launch_len_order(const void *d_desc, const uint64_t *d_total, uint64_t max_chunks, uint64_t max_len,
                                  uint32_t *d_order_tmp, hipStream_t st, uint32_t *d_need = nullptr,
-                                 uint32_t quad_pm = 0, uint32_t pair_pm = 0, uint32_t solo_pm = 1000);
+                                 uint32_t quad_pm = 0, uint32_t pair_pm = 0);
 
 // K5: CAS content ids (cas.hip): SHAKE256-256 of the framed span, ContentId::compute
 // (crates/core/cas/src/lib.rs:53-69); id of span g -> d_ids + g * id_stride.

@@ -708,8 +708,7 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
                                                uint8_t *__restrict__ hash_base, size_t stride,
                                                unsigned long long *__restrict__ diag, uint32_t mode,
                                                uint32_t nquad, uint32_t npair, uint32_t spin_limit,
-                                               uint32_t *__restrict__ err, const uint32_t *__restrict__ need,
-                                               bool solo) {
+                                               uint32_t *__restrict__ err, const uint32_t *__restrict__ need) {
     unsigned long long t_start = diag ? __builtin_amdgcn_s_memtime() : 0ull, t_spin = 0;
     const unsigned long long rt_start = diag ? __builtin_amdgcn_s_memrealtime() : 0ull;
     if (need) {  // latency tiers (k_len_base): no more lanes per chunk than its length needs
@@ -743,7 +742,6 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
     const uint32_t row = split ? split_row(slot) : lane;
     uint64_t total = *total_p;
     if (total > max_chunks) total = max_chunks;
-    if (solo && total > need[2]) total = need[2];  // the rest is k_sha256_solo's
     if (wg_base >= total) return;  // whole workgroup idle (uniform)
     if (threadIdx.x == 0) {
         s_ready = 0;
@@ -841,101 +839,6 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
 }
 
 // ---------------------------------------------------------------------------
-// Solo tier (round 5): one chunk per lane and nothing else -- no producer wave, no LDS
-// ring.  Each lane loads and realigns its own block, expands the schedule in a 16-word
-// register window and runs the 64 rounds: ~1,400 VALU per block from one wave (the
-// producer / consumer pair issues about as many, split over two waves on two SIMDs at
-// one wave per SIMD, the consumer's half saturated and the producer's ~65 % busy).
-// Without the 69.6 KiB ring a CU holds as many of these waves as registers allow, so in
-// a launch that fills the GPU the work spreads over every SIMD; a lone solo chain is
-// ~1.5x slower per block than the consumer's, so only chunks well below the longest take
-// this tier (k_len_base's need[2], launch_sha256).
-// ---------------------------------------------------------------------------
-#define SOLO_RND(a, b, c, d, e, f, g, h, t)                                                        \
-    {                                                                                              \
-        uint32_t wt;                                                                               \
-        if ((t) < 16) {                                                                            \
-            wt = w[(t)&15];                                                                        \
-        } else {                                                                                   \
-            wt = add3(w[(t)&15], SHA_s0(w[((t) - 15) & 15]), w[((t) - 7) & 15]) + SHA_s1(w[((t) - 2) & 15]); \
-            w[(t)&15] = wt;                                                                        \
-        }                                                                                          \
-        const uint32_t t1 = add3(h, wt + SHA_K[t], ch(e, f, g)) + SHA_S1(e);                       \
-        d += t1;                                                                                   \
-        h = add3(t1, SHA_S0(a), maj(a, b, c));                                                     \
-    }
-#define SOLO_8RND(t)                              \
-    SOLO_RND(a, b, c, d, e, f, g, h, (t) + 0);    \
-    SOLO_RND(h, a, b, c, d, e, f, g, (t) + 1);    \
-    SOLO_RND(g, h, a, b, c, d, e, f, (t) + 2);    \
-    SOLO_RND(f, g, h, a, b, c, d, e, (t) + 3);    \
-    SOLO_RND(e, f, g, h, a, b, c, d, (t) + 4);    \
-    SOLO_RND(d, e, f, g, h, a, b, c, (t) + 5);    \
-    SOLO_RND(c, d, e, f, g, h, a, b, (t) + 6);    \
-    SOLO_RND(b, c, d, e, f, g, h, a, (t) + 7);
-
-__device__ __forceinline__ void sha_compress_solo(uint32_t st[8], uint32_t (&w)[16], bool active) {
-    uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
-    SOLO_8RND(0) SOLO_8RND(8) SOLO_8RND(16) SOLO_8RND(24) SOLO_8RND(32) SOLO_8RND(40) SOLO_8RND(48) SOLO_8RND(56)
-    // finished lanes keep their state (a select: the rounds always run under a full exec mask)
-    st[0] = active ? st[0] + a : st[0];
-    st[1] = active ? st[1] + b : st[1];
-    st[2] = active ? st[2] + c : st[2];
-    st[3] = active ? st[3] + d : st[3];
-    st[4] = active ? st[4] + e : st[4];
-    st[5] = active ? st[5] + f : st[5];
-    st[6] = active ? st[6] + g : st[6];
-    st[7] = active ? st[7] + h : st[7];
-}
-
-// Chunks [need[2], total) of the length order, one per lane.
-__global__ __launch_bounds__(256) void k_sha256_solo(const uint8_t *__restrict__ data, const uint64_t *__restrict__ abs,
-                                                    const DescRaw *__restrict__ desc,
-                                                    const uint64_t *__restrict__ total_p, uint64_t max_chunks,
-                                                    const uint32_t *__restrict__ order, uint8_t *__restrict__ hash_base,
-                                                    size_t stride, const uint32_t *__restrict__ need) {
-    uint64_t total = *total_p;
-    if (total > max_chunks) total = max_chunks;
-    const uint64_t first = (uint64_t)need[2] + (uint64_t)blockIdx.x * 256u;
-    if (first + (threadIdx.x & ~63u) >= total) return;  // whole wave idle (uniform)
-    const uint64_t gi = first + threadIdx.x;
-    const bool valid = gi < total;
-    const uint64_t ci = valid ? (uint64_t)order[gi] : 0;
-    const uint64_t len = valid ? desc[ci].length : 0;
-    const uint8_t *p = data + (valid ? abs[ci] : 0);
-    const uint64_t nb = len >> 6;
-    const uint32_t rem = (uint32_t)(len & 63u);
-    const uint32_t nbt = valid ? (uint32_t)(nb + (rem < 56 ? 1 : 2)) : 0u;
-    const uint32_t NB = __builtin_amdgcn_readfirstlane(wave_max_u32(nbt));
-    const uint32_t shift = (uint32_t)((uintptr_t)p & 3u);
-    const uint32_t *base = reinterpret_cast<const uint32_t *>(p - shift);
-    const uint32_t sel = perm_sel(shift);
-    uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
-    for (uint32_t k = 0; k < NB; ++k) {
-        uint32_t w[16];
-        if (k < nb) {
-            const uint32_t *q = base + 16ull * k;
-            uint32_t dw[17];
-#pragma unroll
-            for (int i = 0; i < 16; ++i) dw[i] = q[i];
-            dw[16] = q[shift ? 16 : 15];  // (as sha_produce: shift 0 ignores it)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_perm(dw[i + 1], dw[i], sel);
-        } else {
-            sha_pad_words(w, p, base, sel, len, k);
-        }
-        sha_compress_solo(st, w, k < nbt);
-    }
-    if (valid) {
-        uint4 *o = reinterpret_cast<uint4 *>(hash_base + ci * stride);
-        o[0] = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]), __builtin_bswap32(st[2]),
-                          __builtin_bswap32(st[3]));
-        o[1] = make_uint4(__builtin_bswap32(st[4]), __builtin_bswap32(st[5]), __builtin_bswap32(st[6]),
-                          __builtin_bswap32(st[7]));
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Length order.  A wave lives as long as its longest chunk, and a batch's digest
 // stage as long as its longest chunk, so lanes are handed chunks in descending
 // block count: a counting sort on SHA_NBKT buckets of (blocks >> shift), each
@@ -973,13 +876,13 @@ __global__ __launch_bounds__(256) void k_len_hist(const DescRaw *__restrict__ de
 // (DESIGN.md §4 "Latency tiers"): the longest chunk still sets the batch's digest time, and
 // the other chunks take 1/8 and 1/2 of the SIMD time a quad would give them.
 __global__ __launch_bounds__(SHA_NBKT) void k_len_base(uint32_t *__restrict__ bkt, uint32_t *__restrict__ need,
-                                                      uint32_t quad_pm, uint32_t pair_pm, uint32_t solo_pm) {
+                                                      uint32_t quad_pm, uint32_t pair_pm) {
     __shared__ uint32_t wsum[SHA_NBKT / 64];
-    __shared__ uint32_t s_first, s_need[3];
+    __shared__ uint32_t s_first, s_need[2];
     const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
     if (t == 0) {
         s_first = SHA_NBKT;
-        s_need[0] = s_need[1] = s_need[2] = 0;
+        s_need[0] = s_need[1] = 0;
     }
     const uint32_t v = bkt[t];
     uint32_t x = v;
@@ -1001,14 +904,10 @@ __global__ __launch_bounds__(SHA_NBKT) void k_len_base(uint32_t *__restrict__ bk
     const uint32_t bmax = SHA_NBKT - 1u - min(s_first, SHA_NBKT - 1u), bv = SHA_NBKT - 1u - t;
     if (bv * 1000u > bmax * quad_pm) atomicMax(&s_need[0], off + x);
     if (bv * 1000u > bmax * pair_pm) atomicMax(&s_need[1], off + x);
-    // need[2] (solo tier on): the chunks longer than solo_pm stay in k_sha256, the rest go
-    // to k_sha256_solo; at least the quads and pairs stay
-    if (bv * 1000u > bmax * solo_pm) atomicMax(&s_need[2], off + x);
     __syncthreads();
     if (t == 0) {
         need[0] = max(s_need[0], 1u);
         need[1] = max(s_need[1], s_need[0]);
-        need[2] = max(max(s_need[2], s_need[1]), 1u);
     }
 }
 
@@ -1048,13 +947,10 @@ size_t sha256_order_tmp_elems(uint64_t max_chunks) { return max_chunks + SHA_NBK
 // tier the grid holds).
 uint32_t g_sha_tier_quad_pm[2] = {850, 950};
 uint32_t g_sha_tier_pair_pm[2] = {600, 700};
-// Solo tier (k_sha256_solo): chunks up to solo_pm of the longest; 0 = off.  Test hook
-// cg_test_sha_solo.
-uint32_t g_sha_tier_solo_pm[2] = {0, 0};
 
 const uint32_t *launch_len_order(const void *d_desc, const uint64_t *d_total, uint64_t max_chunks, uint64_t max_len,
                                  uint32_t *d_order_tmp, hipStream_t st, uint32_t *d_need, uint32_t quad_pm,
-                                 uint32_t pair_pm, uint32_t solo_pm) {
+                                 uint32_t pair_pm) {
     if (!d_order_tmp || max_chunks == 0) return nullptr;
     uint32_t shift = 0;
     while ((((max_len + 72) >> 6) >> shift) >= SHA_NBKT - 1) ++shift;
@@ -1063,7 +959,7 @@ const uint32_t *launch_len_order(const void *d_desc, const uint64_t *d_total, ui
     (void)hipMemsetAsync(bkt, 0, SHA_NBKT * sizeof(uint32_t), st);
     hipLaunchKernelGGL(k_len_hist, dim3(nb), dim3(256), 0, st, (const DescRaw *)d_desc, d_total, max_chunks, shift,
                        bkt);
-    hipLaunchKernelGGL(k_len_base, dim3(1), dim3(SHA_NBKT), 0, st, bkt, d_need, quad_pm, pair_pm, solo_pm);
+    hipLaunchKernelGGL(k_len_base, dim3(1), dim3(SHA_NBKT), 0, st, bkt, d_need, quad_pm, pair_pm);
     hipLaunchKernelGGL(k_len_scatter, dim3(nb), dim3(256), 0, st, (const DescRaw *)d_desc, d_total, max_chunks,
                        shift, bkt, ord);
     return ord;
@@ -1136,16 +1032,10 @@ void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
     // latency tiers: k_len_base counts the chunks that need a quad / a pair into the two
     // words after the order (sha256_order_tmp_elems' slack)
     const uint32_t qpm = latency_tiers ? g_sha_tier_quad_pm[fill] : 0u, ppm = g_sha_tier_pair_pm[fill];
-    const uint32_t spm = g_sha_tier_solo_pm[fill];
     uint32_t *need = max_chunks > 8 && d_order_tmp && qpm ? d_order_tmp + SHA_NBKT + max_chunks : nullptr;
-    const uint32_t *order = max_chunks > 8 ? launch_len_order(d_desc, d_total, max_chunks, max_len, d_order_tmp, st,
-                                                              need, qpm, ppm, spm ? spm : 1000u)
-                                           : nullptr;
-    // solo tier: its own launch ahead of k_sha256 on the same stream (chunks [need[2], total))
-    const bool solo = order && need && spm;
-    if (solo)
-        hipLaunchKernelGGL(k_sha256_solo, dim3((uint32_t)((max_chunks + 255) / 256)), dim3(256), 0, st, d_data, d_abs,
-                           (const DescRaw *)d_desc, d_total, max_chunks, order, d_hash_base, hash_stride, need);
+    const uint32_t *order = max_chunks > 8
+                                ? launch_len_order(d_desc, d_total, max_chunks, max_len, d_order_tmp, st, need, qpm, ppm)
+                                : nullptr;
     // Latency-bound batches (no more workgroups than CUs): pad the LDS request past half
     // a CU's 160 KiB so no two workgroups share a CU, and a consumer wave never shares a
     // SIMD with another workgroup's wave (which costs it 20-90 % per round).
@@ -1157,7 +1047,7 @@ void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
     t_sha_tiers[3] = (uint32_t)pad;
     hipLaunchKernelGGL(k_sha256, dim3(nwg), dim3(128), pad, st, d_data, d_abs,
                        (const DescRaw *)d_desc, d_total, max_chunks, order, d_hash_base, hash_stride, g_sha_diag,
-                       g_sha_mode, nquad, npair, g_sha_spin_limit, d_err, order ? need : nullptr, solo);
+                       g_sha_mode, nquad, npair, g_sha_spin_limit, d_err, order ? need : nullptr);
 }
 
 // ---------------------------------------------------------------------------
@@ -1360,14 +1250,6 @@ static uint32_t set_sha_tiers(int k, uint32_t quad_pm, uint32_t pair_pm) {
     return old;
 }
 extern "C" uint32_t cg_test_sha_tiers(uint32_t quad_pm, uint32_t pair_pm) { return set_sha_tiers(0, quad_pm, pair_pm); }
-// Solo tier thresholds (per mille of the longest chunk; 0 = off) for launches that leave
-// the chip idle / fill it; returns the previous latency * 1000 + fill values.
-extern "C" uint32_t cg_test_sha_solo(uint32_t latency_pm, uint32_t fill_pm) {
-    const uint32_t old = cg::g_sha_tier_solo_pm[0] * 1000u + cg::g_sha_tier_solo_pm[1];
-    cg::g_sha_tier_solo_pm[0] = latency_pm > 999u ? 999u : latency_pm;
-    cg::g_sha_tier_solo_pm[1] = fill_pm > 999u ? 999u : fill_pm;
-    return old;
-}
 extern "C" uint32_t cg_test_sha_tiers_fill(uint32_t quad_pm, uint32_t pair_pm) {
     return set_sha_tiers(1, quad_pm, pair_pm);
 }

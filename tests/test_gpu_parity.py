@@ -570,40 +570,6 @@ def test_sha_latency_tiers_agree(ca, O, quad_pm, pair_pm):
         ca.lib.cg_test_sha_tiers_fill(prev_fill // 1000, prev_fill % 1000)
 
 
-@pytest.mark.parametrize("solo_pm", [400, 999, 1, 700], ids=["mid", "all_but_longest", "none", "at_pair"])
-def test_sha_solo_tier_agree(ca, O, solo_pm):
-    """Solo tier (k_sha256_solo: one chunk per lane, no producer, no LDS ring) for the
-    chunks up to solo_pm of the longest, k_sha256 for the rest, both regimes: hashlib's
-    digests over the span sweep and the oracle's descriptors through the pipeline."""
-    import torch
-
-    prev = ca.lib.cg_test_sha_solo(solo_pm, solo_pm)
-    try:
-        rng = np.random.default_rng(29)
-        data = rng.integers(0, 256, 3 << 20, dtype=np.uint8)
-        lens = list(range(0, 140)) + [511, 4097, 65537, 300_000, 600_001, 900_000, 1 << 20, 1_500_003, 2_000_001]
-        offs = [int(rng.integers(0, len(data) - n + 1)) for n in lens]
-        d = torch.from_numpy(np.concatenate([data, np.zeros(256, np.uint8)])).cuda()
-        o = torch.tensor(offs, dtype=torch.int64).cuda()
-        ln = torch.tensor(lens, dtype=torch.int64).cuda()
-        dig = torch.zeros(len(lens) * 32, dtype=torch.uint8, device="cuda")
-        assert ca.lib.cg_hash_spans_device(d.data_ptr(), o.data_ptr(), ln.data_ptr(), len(lens), SHA,
-                                           dig.data_ptr(), None) == 0
-        dig = dig.cpu().numpy().reshape(-1, 32)
-        for k, (a, n) in enumerate(zip(offs, lens)):
-            assert bytes(dig[k]) == hashlib.sha256(data[a:a + n].tobytes()).digest(), (solo_pm, n, a)
-        from chunker_amd.nar import synth_nars
-
-        sizes = [2 * 1024 * 1024 + 8 * k for k in range(6)] + [12344, 128, 4096 + 8]
-        nd, no = synth_nars(sizes, first_index=9)
-        nars = [nd[no[i]:no[i + 1]] for i in range(len(sizes))]
-        got = ca.chunk_batch(nars, 4096, 16384, 65536)
-        for i, nar in enumerate(nars):
-            assert_same(got[i], O.chunk_descriptors(nar, 4096, 16384, 65536, algo=SHA), f"nar{i}")
-    finally:
-        ca.lib.cg_test_sha_solo(prev // 1000, prev % 1000)
-
-
 @pytest.mark.slow
 def test_full_size_config2_batch(ca, O):
     """BASELINE config 2 at full size (256 x 4 MiB NARs, defaults, SHA-256): every
