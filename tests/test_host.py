@@ -109,3 +109,61 @@ def test_bench_default_depth(monkeypatch):
     assert bench.default_depth(1, G) == 6
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
     assert bench.default_depth(1, G) == 2 and bench.default_depth(1, 16 * G) == 2
+
+
+def test_batch_pipeline_order_depth_and_drain(monkeypatch):
+    """BatchPipeline's host logic with the engine call replaced: at most `depth` batches
+    queued, results in submission order, drain() empties it, the context exit waits for
+    whatever is left (and re-raises a batch's error only when nothing else is raising),
+    and the default depth follows default_depth for the first batch's size."""
+    import numpy as np
+
+    log = []
+
+    class FakeBatch:
+        def __init__(self, k, fail=False):
+            self.k, self.fail = k, fail
+
+        def wait(self):
+            log.append(("wait", self.k))
+            if self.fail:
+                raise ca.IoError("boom")
+            return np.array([0, self.k], np.uint64)
+
+    issued = []
+
+    def fake_async(d_data, offs, d_out, cap, mn, avg, mx, hash=None, stream=0, inputs_ready=0):
+        k = len(issued)
+        issued.append((d_data, inputs_ready))
+        log.append(("issue", k))
+        return FakeBatch(k, fail=(d_data == 666))
+
+    monkeypatch.setattr(chunking, "chunk_batch_device_async", fake_async)
+    offs = np.array([0, 1 << 20], np.uint64)
+    with chunking.BatchPipeline(3) as p:
+        got = []
+        for k in range(7):
+            got += p.submit(1, offs, 2, 3, inputs_ready=9, tag=f"b{k}")
+            assert len(p) <= 2
+        got += p.drain()
+        assert len(p) == 0
+    assert [t for t, _ in got] == [f"b{k}" for k in range(7)]
+    assert [int(f[1]) for _, f in got] == list(range(7))
+    # batch k is waited for only after batch k + 2 was issued (depth 3)
+    assert log.index(("wait", 0)) > log.index(("issue", 2))
+    assert all(r == 9 for _, r in issued)
+    # a failing batch raises from submit/drain; leaving the context waits for the rest
+    issued.clear()
+    log.clear()
+    with pytest.raises(ca.IoError):
+        with chunking.BatchPipeline(2) as p:
+            p.submit(666, offs, 2, 3)
+            p.submit(1, offs, 2, 3)  # waits for the failing first batch -> raises
+    assert ("wait", 1) in log  # the context exit still waited for the second one
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "16")
+    p = chunking.BatchPipeline()
+    p.submit(1, offs, 2, 3)
+    assert p.depth == 10
+    p.drain()
+    with pytest.raises(ca.InvalidOptionsError):
+        chunking.BatchPipeline(0)
