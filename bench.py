@@ -220,16 +220,13 @@ def main():
     synth_ev = torch.cuda.Event()
     synth_ev.record()
 
-    def issue(k):
+    def ready_event(k):  # the inputs-ready event of step k (its output array free again)
         ev = gathered_ev[k % depth]
         if ev is not None:
             bstream.wait_event(ev)  # (the digest writes the output array's hashes)
-        ready = 0 if args.no_overlap else (ev or synth_ev).cuda_event
-        return ca.chunk_batch_device_async(d_data.data_ptr(), offs, d_outs[k % depth].data_ptr(), gcap, *params,
-                                           hash=algo, stream=sptr, inputs_ready=ready)
+        return 0 if args.no_overlap else (ev or synth_ev).cuda_event
 
-    def complete(k, batch):
-        first = batch.wait()
+    def after_wait(k, first):
         if multi and nccl:  # descriptors + NAR index to rank 0 over RCCL (the path's only exchange)
             gathered[0] = gather_batch_async(d_outs[k % depth], first, gcap, gnars)
             ev = torch.cuda.Event()
@@ -239,25 +236,32 @@ def main():
             gathered[0] = gather_batch(d_outs[k % depth][: int(first[-1]) * 48].cpu(), first)
         return first
 
-    def step(k=0):  # one batch, waited for
-        return complete(k, issue(k))
+    def run(n, on_done=None, d=None, k0=0):
+        """Steps k0 .. k0 + n - 1 through the product's own pipeline (chunker_amd.BatchPipeline
+        over cg_chunk_batch_device_async_after + cg_batch_wait): up to `d` queued, step
+        k + d - 1 queued before step k is waited for, so the host side of each call --
+        validation, staging, launches, the wait -- overlaps the GPU's work instead of
+        idling it between batches (~65 us per step, 8 % of a config-3 step)."""
+        pipe = ca.BatchPipeline(d or depth, *params, hash=algo, stream=sptr)
+        t_issue = {}
+        last_first = [None]
 
-    def run(n, on_done=None):
-        """n steps, up to `depth` queued: step k + depth - 1 is queued before step k is
-        waited for, so the host side of each call -- validation, staging, launches, the
-        wait -- overlaps the GPU's work instead of idling it between batches (~65 us per
-        step, 8 % of a config-3 step)."""
-        q = deque()
-        first = None
-        for k in range(n + depth - 1):
-            if k < n:
-                q.append((k, time.perf_counter(), issue(k)))
-            if len(q) == depth or (k >= n and q):
-                kk, t_issue, b = q.popleft()
-                first = complete(kk, b)
+        def finished(done):
+            for k, first in done:
+                last_first[0] = after_wait(k, first)
                 if on_done:
-                    on_done(kk, time.perf_counter() - t_issue)
-        return first
+                    on_done(k - k0, time.perf_counter() - t_issue.pop(k))
+
+        for k in range(k0, k0 + n):
+            ready = ready_event(k)
+            t_issue[k] = time.perf_counter()
+            finished(pipe.submit(d_data.data_ptr(), offs, d_outs[k % depth].data_ptr(), gcap, inputs_ready=ready,
+                                 tag=k))
+        finished(pipe.drain())
+        return last_first[0]
+
+    def step(k=0):  # one batch, waited for
+        return run(1, d=1, k0=k)
 
     # warm-up in the timed loop's pattern (depth batches queued, so every workspace the pool
     # hands out is sized before the timed region)
