@@ -1242,9 +1242,9 @@ extern "C" uint32_t cg_test_sha_pair_fill(uint32_t v) {
 
 // Latency tiers: per-mille thresholds (quad, pair) of the longest chunk for launches that
 // leave the chip idle (cg_test_sha_tiers) and for GPU-filling ones (cg_test_sha_tiers_fill);
-// quad_pm 0 = off.  Each returns its previous quad_pm * 1000 + pair_pm.
+// quad_pm 0 = off.  Each returns its previous quad_pm << 16 | pair_pm.
 static uint32_t set_sha_tiers(int k, uint32_t quad_pm, uint32_t pair_pm) {
-    const uint32_t old = cg::g_sha_tier_quad_pm[k] * 1000u + cg::g_sha_tier_pair_pm[k];
+    const uint32_t old = cg::g_sha_tier_quad_pm[k] << 16 | cg::g_sha_tier_pair_pm[k];
     cg::g_sha_tier_quad_pm[k] = quad_pm > 1000u ? 1000u : quad_pm;
     cg::g_sha_tier_pair_pm[k] = pair_pm > cg::g_sha_tier_quad_pm[k] ? cg::g_sha_tier_quad_pm[k] : pair_pm;
     return old;

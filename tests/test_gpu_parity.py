@@ -566,8 +566,8 @@ def test_sha_latency_tiers_agree(ca, O, quad_pm, pair_pm):
         for i, nar in enumerate(nars):
             assert_same(got[i], O.chunk_descriptors(nar, 4096, 16384, 65536, algo=SHA), f"nar{i}")
     finally:
-        ca.lib.cg_test_sha_tiers(prev // 1000, prev % 1000)
-        ca.lib.cg_test_sha_tiers_fill(prev_fill // 1000, prev_fill % 1000)
+        ca.lib.cg_test_sha_tiers(prev >> 16, prev & 0xFFFF)
+        ca.lib.cg_test_sha_tiers_fill(prev_fill >> 16, prev_fill & 0xFFFF)
 
 
 @pytest.mark.slow
