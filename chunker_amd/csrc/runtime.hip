@@ -292,8 +292,8 @@ uint32_t seg_slots(const CdcParams &p) {
 //
 // What a member can wait for, beyond its own digest's chain: callers only merge past
 // coal_min() (the hardware queues less 4, at least 4) in the entry, so a lone caller and up
-// to that many concurrent ones never enter a group (they go solo and no leader counts them: test_lone_and_few_callers_never_wait_for_the
-// _window); a merged member waits at most kCoalWindow (3 ms) for its group to form plus the
+// to that many concurrent ones never enter a group (they go solo and no leader counts them:
+// test_lone_and_few_callers_never_wait_for_the_window); a merged member waits at most kCoalWindow (3 ms) for its group to form plus the
 // previous group's remaining chain on the one set (lease_set: <= one longest-chunk chain,
 // ~55-75 ms at the default 4 MiB max), i.e. its call returns within window + 2 chains + its
 // boundary stages.  bench.py's `concurrent` leg reports the measured per-call p50 / p99 of
@@ -489,7 +489,7 @@ static int launch_group(CoalSet *S, std::vector<CoalEntry *> &grp, std::shared_p
 // well as one merged launch (16 queues, K = 12: 169 GiB/s per batch, p99 73 ms); past it
 // the per-batch launches queue behind one another on shared queues (K = 16 / 24 / 32:
 // 127-133 / 134 / 137 per batch with p99 121-127 ms, against 170 / 182 / 227-241 merged;
-// profiles/r05_v28_*, r05_v29_*, r05_v30_*).  Round 4, before the tiers, merged from 8
+// profiles/r05_v29_v31_coalesce_threshold.txt).  Round 4, before the tiers, merged from 8
 // callers (profiles/r04_v18_*, r04_v19_*).  Leader window 3 ms: 10 ms gave K = 32 220-279.
 #ifndef CG_COAL_MIN
 #define CG_COAL_MIN 4
@@ -628,7 +628,6 @@ int ensure_pass_buffers(Workspace *ws, uint64_t total_len, size_t n_nars, uint64
     }
     return CG_OK;
 }
-
 
 // The persistent scan's queue: allocated and zeroed (on the batch's stream, ahead of its
 // first scan) once per workspace; every scan launch leaves it zeroed again.
