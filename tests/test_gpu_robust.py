@@ -184,6 +184,16 @@ def test_concurrent_sha_callers_share_one_digest(ca, O, coalesce):
             assert _same(descs[int(first[i]):int(first[i + 1])], ref), (t, i)
 
 
+def _merging_callers():
+    """More concurrent callers than the coalescer lets launch alone (runtime.hip coal_min:
+    the process's hardware queues less 4, at least 4): 12 at HIP's default 4 queues."""
+    try:
+        q = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+    except ValueError:
+        q = 4
+    return max(12, max(q - 4, 4) + 8)
+
+
 def _coal_stats(ca):
     out = (ctypes.c_uint64 * 4)()
     ca.lib.cg_coalesce_stats(out)
@@ -200,7 +210,7 @@ def test_lone_and_few_callers_never_wait_for_the_window(ca, O):
 
     old = ca.lib.cg_test_coalesce(1)
     try:
-        jobs = _coalesced_jobs(ca, 12, seed=21)
+        jobs = _coalesced_jobs(ca, _merging_callers(), seed=21)
         time.sleep(0.1)  # (callers that returned within the last 50 ms count as expected back)
         s0 = _coal_stats(ca)
         _, errors = _run_threads(ca, jobs[:1], reps=4)  # a lone caller
@@ -212,10 +222,10 @@ def test_lone_and_few_callers_never_wait_for_the_window(ca, O):
         assert not errors, errors
         s2 = _coal_stats(ca)
         assert s2 == s1, (s1, s2)
-        firsts, errors = _run_threads(ca, jobs, reps=2)  # 12 callers: merged groups
+        firsts, errors = _run_threads(ca, jobs, reps=2)  # 12+ callers: merged groups
         assert not errors, errors
         s3 = _coal_stats(ca)
-        assert s3[0] > s2[0] and 2 <= s3[1] - s2[1] <= 24, (s2, s3)
+        assert s3[0] > s2[0] and 2 <= s3[1] - s2[1] <= 2 * len(jobs), (s2, s3)
     finally:
         ca.lib.cg_test_coalesce(old)
     torch.cuda.synchronize()
@@ -247,7 +257,7 @@ def test_coalesced_spin_guard_reaches_every_member(ca):
     """A spin-guard expiry inside a merged digest fails every member's call with CG_E_IO
     (the merged launch's error word is copied into each member's), and the next round is
     exact again."""
-    jobs = _coalesced_jobs(ca, 12, seed=9)  # more callers than hardware queues: the merged path
+    jobs = _coalesced_jobs(ca, _merging_callers(), seed=9)  # past coal_min: the merged path
     old = ca.lib.cg_test_sha_spin_limit(0)
     try:
         _, errors = _run_threads(ca, jobs)
