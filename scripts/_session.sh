@@ -1,5 +1,11 @@
 cd "${GRAFT_REPO_ROOT:-.}"; export TMPDIR=/tmp; mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_robust.py -m gpu > gpurun_out/r05_v49_robust.log 2>&1 || { tail -30 gpurun_out/r05_v49_robust.log; exit 1; }
-tail -1 gpurun_out/r05_v49_robust.log
-GPU_MAX_HW_QUEUES=16 timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_robust.py -m gpu -k "lone or spin_guard_reaches" > gpurun_out/r05_v49_robust_q16.log 2>&1 || { tail -30 gpurun_out/r05_v49_robust_q16.log; exit 1; }
-tail -1 gpurun_out/r05_v49_robust_q16.log
+T=r05_v52
+out=gpurun_out/${T}_queues.txt
+: > $out
+for qd in 4:2 4:4 4:6 4:8 4:10 4:14 4:16 8:10 8:14 16:14 16:16; do
+    IFS=: read q d <<< "$qd"
+    f=gpurun_out/${T}_q${q}_d$d
+    timeout -k 10 240 python -u bench.py --config c2 --steps 20 --warmup 5 --hw-queues $q --depth $d --no-cpu-baseline \
+      --no-concurrent --drop-in '' --e2e '' --no-clock > $f.json 2> $f.err || { tail -5 $f.err; exit 1; }
+    python3 scripts/depth_row.py $f.json c2 "q$q d$d" | tee -a $out
+done
