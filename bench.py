@@ -88,7 +88,7 @@ def parse_args():
     ap.add_argument("--no-overlap", action="store_true",
                     help="queue each batch after everything on the stream (cg_chunk_batch_device_async): its "
                          "boundary stages wait for the previous batch's digest (A/B of the overlap)")
-    ap.add_argument("--depth", type=int, default=0, choices=range(0, 17), metavar="0..16",
+    ap.add_argument("--depth", type=int, default=0, choices=range(0, 33), metavar="0..32",
                     help="batches in flight from the one caller (each its own output array and workspace); "
                          "1 = each batch waited for before the next is queued; 0 = auto (default_depth)")
     ap.add_argument("--split-mode", type=int, default=2, choices=(1, 2),
