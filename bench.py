@@ -82,7 +82,7 @@ def parse_args():
     ap.add_argument("--drop-in-only", action="store_true", help="only the drop-in leg (profiling)")
     ap.add_argument("--drop-in-sizes", default="10,64,256,1024",
                     help="MiB per call of the drop-in leg's one-caller size sweep ('' = skip)")
-    ap.add_argument("--hw-queues", type=int, default=16, choices=range(0, 33), metavar="0..32",
+    ap.add_argument("--hw-queues", type=int, default=22, choices=range(0, 33), metavar="0..32",
                     help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's)")
     ap.add_argument("--no-clock", action="store_true", help="skip the digest clock measurement (scripts/sha_clock.py)")
     ap.add_argument("--no-overlap", action="store_true",
@@ -112,17 +112,17 @@ def parse_args():
 
 def default_depth(algo: int, batch_bytes: int) -> int:
     """Batches the one caller keeps in flight: chunker_amd.default_depth (DESIGN.md §7
-    "Batches in flight").  SHA-256 under 4 GiB a batch: 10 -- such a batch's digest is
+    "Batches in flight").  SHA-256 under 4 GiB a batch: 20 -- such a batch's digest is
     latency-bound, every chunk one serial chain (config 2's longest: 52,345 blocks = 53
     ms), and with the latency tiers its ~1,000 chains take ~18 workgroups, so the batches
-    queued behind it fill the chip (config 2, 20 steps: 18.1 one at a time, 169.5 GiB/s
-    with ten, per-batch p50 latency 55 -> 58.5 ms; profiles/r05_v24_v26_tiers_ab.txt,
-    r05_v19_v23_depth_ab.txt before the tiers).  From 4 GiB: 4 (configs 4 / 5: the digest
-    fills the chip by itself and the overlap hides the scan).  BLAKE3: 2 (its batches stay
-    in stream order; the second one queued covers the host's per-call work).  Held to
-    GPU_MAX_HW_QUEUES - 2: each batch in flight runs on a HIP stream of its own, and at
-    HIP's default 4 queues config 2 stays at 36 GiB/s whatever the depth
-    (profiles/r05_v23 in r05_v19_v23_depth_ab.txt)."""
+    queued behind it fill the chip: config 2 at 22 hardware queues 318.8-320.4 GiB/s with
+    twenty in flight at a per-batch p50 of 61.4-61.5 ms (55 alone; 18.1 one at a time;
+    309.7 over 200 steps) (profiles/r05_v57_v58_q22.txt, r05_v24_v26_tiers_ab.txt).  From
+    4 GiB: 4 (configs 4 / 5: the digest fills the chip by itself and the overlap hides the
+    scan).  BLAKE3: 2 (its batches stay in stream order; the second one queued covers the
+    host's per-call work).  Held to GPU_MAX_HW_QUEUES - 2: each batch in flight runs on a
+    HIP stream of its own, and batches sharing a hardware queue run one after another
+    (profiles/r05_v51_v52_queues_depth.txt)."""
     from chunker_amd.chunking import default_depth as rule
 
     return rule(algo, batch_bytes)
@@ -147,10 +147,11 @@ def main():
     # engine refuses to chunk with it unless opted in; the JSON says which table ran.
     os.environ.setdefault("CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR", "1")
     # HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default) and streams
-    # sharing one serialise, so concurrent callers need more: the deployment setting
-    # DESIGN.md §7 / INTEGRATION.md recommend (single-batch value unchanged; K = 8 / 32
-    # batches in flight 38 / 51 -> 92 / 95 GiB/s).  Set before anything initialises HIP;
-    # --hw-queues 0 keeps the environment's value.
+    # sharing one serialise, so batches in flight and concurrent callers need more: the
+    # deployment setting DESIGN.md §7 / INTEGRATION.md recommend, 22 -- twenty batches in
+    # flight plus the caller's streams; at 24 and more the queues are time-sliced and every
+    # leg of this bench slowed (profiles/r05_v57_v58_q22.txt, r05_v53_q32_depth.txt).  Set
+    # before anything initialises HIP; --hw-queues 0 keeps the environment's value.
     if args.hw_queues:
         os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
 

@@ -397,19 +397,21 @@ def chunk_batch_device_async(d_data_ptr: int, nar_offsets: np.ndarray, d_out_ptr
 
 def default_depth(hash: HashAlgorithm, batch_bytes: int) -> int:
     """Device batches one caller keeps in flight (DESIGN.md §7 "Batches in flight"):
-    SHA-256 under 4 GiB a batch 10 -- its digest is its longest chunk's serial chain on a
+    SHA-256 under 4 GiB a batch 20 -- its digest is its longest chunk's serial chain on a
     few workgroups (SHA-256 latency tiers), so the batches queued behind it fill the chip
-    (config 2: 18.1 GiB/s one at a time, 169.5 with ten, per-batch latency 55 -> 58.5 ms);
-    from 4 GiB 4 (the digest fills the chip; the overlap hides the scan); BLAKE3 2 (its
-    batches stay in stream order).  Every batch in flight holds a HIP stream, so the depth
-    is held to GPU_MAX_HW_QUEUES - 2 (HIP's default 4 queues: 2)."""
+    (config 2 at 22 hardware queues: 18.1 GiB/s one at a time, 319-320 with twenty at a
+    per-batch p50 of 61.5 ms against 55 alone; thirty slow every chain); from 4 GiB 4 (the
+    digest fills the chip; the overlap hides the scan); BLAKE3 2 (its batches stay in
+    stream order).  Every batch in flight holds a HIP stream and batches sharing a hardware
+    queue run one after another, so the depth is held to GPU_MAX_HW_QUEUES - 2 (HIP's
+    default 4 queues: 2; 16: 14; 22: 20)."""
     if HashAlgorithm(hash) != HashAlgorithm.Sha256:
         return 2
     try:
         hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
     except ValueError:
         hwq = 4
-    return max(2, min(10 if batch_bytes < (4 << 30) else 4, hwq - 2))
+    return max(2, min(20 if batch_bytes < (4 << 30) else 4, hwq - 2))
 
 
 class BatchPipeline:

@@ -91,7 +91,7 @@ def test_bench_cli_contract():
 
 
 def test_bench_default_depth(monkeypatch):
-    """bench.py's batches in flight: 10 for sub-4-GiB SHA-256 batches (latency-bound
+    """bench.py's batches in flight: 20 for sub-4-GiB SHA-256 batches (latency-bound
     digest), 4 from 4 GiB, 2 for BLAKE3, and never more than the hardware queues allow
     (each batch in flight holds a stream of its own)."""
     import sys
@@ -101,8 +101,12 @@ def test_bench_default_depth(monkeypatch):
     import bench
 
     G = bench.GIB
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "22")
+    assert bench.default_depth(1, G) == 20
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "32")
+    assert bench.default_depth(1, G) == 20
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", "16")
-    assert bench.default_depth(1, G) == 10
+    assert bench.default_depth(1, G) == 14
     assert bench.default_depth(1, 16 * G) == 4
     assert bench.default_depth(0, G) == 2
     monkeypatch.setenv("GPU_MAX_HW_QUEUES", "8")
@@ -160,10 +164,10 @@ def test_batch_pipeline_order_depth_and_drain(monkeypatch):
             p.submit(666, offs, 2, 3)
             p.submit(1, offs, 2, 3)  # waits for the failing first batch -> raises
     assert ("wait", 1) in log  # the context exit still waited for the second one
-    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "16")
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "22")
     p = chunking.BatchPipeline()
     p.submit(1, offs, 2, 3)
-    assert p.depth == 10
+    assert p.depth == 20
     p.drain()
     with pytest.raises(ca.InvalidOptionsError):
         chunking.BatchPipeline(0)
