@@ -82,8 +82,9 @@ def parse_args():
     ap.add_argument("--drop-in-only", action="store_true", help="only the drop-in leg (profiling)")
     ap.add_argument("--drop-in-sizes", default="10,64,256,1024",
                     help="MiB per call of the drop-in leg's one-caller size sweep ('' = skip)")
-    ap.add_argument("--hw-queues", type=int, default=22, choices=range(0, 33), metavar="0..32",
-                    help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's)")
+    ap.add_argument("--hw-queues", type=int, default=-1, choices=range(-1, 33), metavar="-1..32",
+                    help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's; -1: 22 for one "
+                         "rank, 28 for the ranks of an N > 1 run, whose RCCL communicator takes queues too)")
     ap.add_argument("--no-clock", action="store_true", help="skip the digest clock measurement (scripts/sha_clock.py)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="queue each batch after everything on the stream (cg_chunk_batch_device_async): its "
@@ -152,6 +153,15 @@ def main():
     # flight plus the caller's streams; at 24 and more the queues are time-sliced and every
     # leg of this bench slowed (profiles/r05_v57_v58_q22.txt, r05_v53_q32_depth.txt).  Set
     # before anything initialises HIP; --hw-queues 0 keeps the environment's value.
+    if args.hw_queues < 0:
+        # 22: twenty batches in flight plus the caller's streams, the most the GPU schedules
+        # without time-slicing its queues (24+ slowed every leg).  An N > 1 rank's RCCL
+        # communicator holds queues too: at 22 its twenty batches ran as two rounds (168-170
+        # GiB/s, per-gather or not); at 26-32 one round with chains ~22 % slower (225-228)
+        # (profiles/r05_v61_v65_rccl_queues.txt).
+        # (The gloo rehearsal puts several ranks on one GPU: 8 queues each.)
+        multi_rank = int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.dist_force
+        args.hw_queues = (8 if args.dist_backend == "gloo" else 28) if multi_rank else 22
     if args.hw_queues:
         os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
 
