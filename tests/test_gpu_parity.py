@@ -911,7 +911,7 @@ def test_async_after_inputs_ready_matches_sync(ca, O, mode):
     ca.lib.cg_test_split_mode(old_mode)
 
 
-@pytest.mark.parametrize("depth", [None, 1, 3], ids=["default", "one", "three"])
+@pytest.mark.parametrize("depth", [None, 1, 3, 20], ids=["default", "one", "three", "twenty"])
 def test_batch_pipeline_matches_sync(ca, O, depth):
     """chunker_amd.BatchPipeline (one thread, up to `depth` batches in flight, each after
     its own inputs-ready event, DESIGN.md §7 "Batches in flight"): twelve SHA-256 batches
@@ -931,6 +931,7 @@ def test_batch_pipeline_matches_sync(ca, O, depth):
     ref_first = ca.chunk_batch_device(d.data_ptr(), offs, ref_out.data_ptr(), cap, 16384, 65536, 262144)
     ref = ref_out.cpu().numpy()
     n_out = 4 if depth is None else depth + 1
+    nb = 12 if depth is None or depth < 12 else depth + 4
     outs = [torch.full((cap * 48,), 0xAB, dtype=torch.uint8, device="cuda") for _ in range(n_out)]
     ready = torch.cuda.Event()
     ready.record()
@@ -939,7 +940,7 @@ def test_batch_pipeline_matches_sync(ca, O, depth):
     free = list(range(n_out))
     busy = {}
     with ca.BatchPipeline(depth, 16384, 65536, 262144, stream=stream.cuda_stream) as pipe:
-        for k in range(12):
+        for k in range(nb):
             j = free.pop(0)
             busy[k] = j
             for tag, first in pipe.submit(d.data_ptr(), offs, outs[j].data_ptr(), cap, inputs_ready=ready.cuda_event,
@@ -952,7 +953,7 @@ def test_batch_pipeline_matches_sync(ca, O, depth):
                     free.append(busy.pop(tag))
         for tag, first in pipe.drain():
             results.append((tag, first, outs[busy[tag]].cpu().numpy()))
-    assert [t for t, _, _ in results] == list(range(12))
+    assert [t for t, _, _ in results] == list(range(nb))
     n = int(ref_first[-1])
     want = O.chunk_descriptors(data[offs[6]:offs[7]], 16384, 65536, 262144, algo=SHA)
     for k, first, got in results:
