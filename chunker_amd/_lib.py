@@ -18,7 +18,7 @@ import os as _os
 LIB_PATH = Path(_os.environ.get("CHUNKER_AMD_LIB") or Path(__file__).resolve().parent / "libchunker_amd.so")
 # diagnostics build (make -C chunker_amd/csrc diag): same ABI plus cg_diag_* kernels
 DIAG_LIB_PATH = Path(__file__).resolve().parent / "libchunker_amd_diag.so"
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # Opt-in that lifts the engine's fail-closed FastCDC table gate (include/chunker_gpu.h):
 # with the placeholder GEAR installed every chunking call refuses to run unless it is "1".
@@ -48,13 +48,15 @@ EXPORTS = (
     "cg_cas_ids_device", "cg_cas_id", "cg_node_put_batch_device", "cg_node_put", "cg_stream_new", "cg_stream_push",
     "cg_stream_finish", "cg_stream_take", "cg_stream_pending", "cg_stream_bytes_consumed", "cg_stream_free",
     "cg_last_sha_tiers", "cg_chunk_batch_device_async", "cg_batch_wait", "cg_chunk_batch_device_async_after",
+    "cg_pipeline_create", "cg_pipeline_submit", "cg_pipeline_flush", "cg_pipeline_stats", "cg_pipeline_destroy",
+    "cg_batch_event",
 )
 # test hooks the product library exports beyond the header (tier caps, spin-guard limit)
 TEST_HOOKS = ("cg_test_sha_quad_max", "cg_test_sha_split_max", "cg_test_sha_spin_limit", "cg_test_cas_pair_max",
               "cg_test_fail_alloc", "cg_test_sha_quad_fill", "cg_test_sha_pair_fill", "cg_test_scan_path", "cg_test_scan_kernel", "cg_test_coalesce", "cg_test_scan_grid",
               "cg_test_stream_group_cap", "cg_test_stream_max_lanes", "cg_test_stream_eager",
               "cg_test_b3_fused_plan", "cg_test_b3_packed", "cg_coalesce_stats",
-              "cg_test_split_mode", "cg_test_sha_tiers", "cg_test_sha_tiers_fill")
+              "cg_test_split_mode", "cg_test_sha_tiers", "cg_test_sha_tiers_fill", "cg_hw_queues")
 
 
 def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
@@ -92,6 +94,19 @@ def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
     L.cg_chunk_batch_device_async_after.restype = i
     L.cg_batch_wait.argtypes = [p, p]
     L.cg_batch_wait.restype = i
+    u32_ = ctypes.c_uint32
+    L.cg_pipeline_create.argtypes = [i, u32_, u32_, ctypes.POINTER(p)]
+    L.cg_pipeline_create.restype = i
+    L.cg_pipeline_submit.argtypes = [p, p, p, sz, u64, u64, u64, i, p, sz, p, ctypes.POINTER(p)]
+    L.cg_pipeline_submit.restype = i
+    L.cg_pipeline_flush.argtypes = [p]
+    L.cg_pipeline_flush.restype = i
+    L.cg_pipeline_stats.argtypes = [p, p]
+    L.cg_pipeline_stats.restype = i
+    L.cg_pipeline_destroy.argtypes = [p]
+    L.cg_pipeline_destroy.restype = None
+    L.cg_batch_event.argtypes = [p, ctypes.POINTER(p)]
+    L.cg_batch_event.restype = i
     L.cg_push_new.argtypes = [u64, u64, u64, i, ctypes.POINTER(i)]
     L.cg_push_new.restype = p
     L.cg_push_push.argtypes = [p, p, u64, p, sz, psz]
@@ -163,6 +178,8 @@ def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
         if hasattr(L, name):
             getattr(L, name).argtypes = [i]
             getattr(L, name).restype = i
+    L.cg_hw_queues.argtypes = []
+    L.cg_hw_queues.restype = i
     L.cg_test_split_mode.argtypes = [i]
     L.cg_test_split_mode.restype = i
     L.cg_coalesce_stats.argtypes = [p]

@@ -395,52 +395,116 @@ def chunk_batch_device_async(d_data_ptr: int, nar_offsets: np.ndarray, d_out_ptr
     return BatchInFlight(h.value, n)
 
 
-def default_depth(hash: HashAlgorithm, batch_bytes: int) -> int:
-    """Device batches one caller keeps in flight (DESIGN.md §7 "Batches in flight"):
-    SHA-256 under 4 GiB a batch 20 -- its digest is its longest chunk's serial chain on a
-    few workgroups (SHA-256 latency tiers), so the batches queued behind it fill the chip
-    (config 2 at 22 hardware queues: 18.1 GiB/s one at a time, 319-320 with twenty at a
-    per-batch p50 of 61.5 ms against 55 alone; thirty slow every chain); from 4 GiB 4 (the
-    digest fills the chip; the overlap hides the scan); BLAKE3 2 (its batches stay in
-    stream order).  Every batch in flight holds a HIP stream and batches sharing a hardware
-    queue run one after another, so the depth is held to GPU_MAX_HW_QUEUES - 2 (HIP's
-    default 4 queues: 2; 16: 14; 22: 20)."""
+def default_depth(hash: HashAlgorithm, batch_bytes: int, hw_queues: int | None = None) -> int:
+    """Batches one caller keeps in flight through the per-batch-stream path
+    (BatchPipeline(group=0), cg_chunk_batch_device_async_after): SHA-256
+    under 4 GiB a batch 20, from 4 GiB 4, BLAKE3 2 -- held to the hardware queues less 2
+    (`hw_queues` None = the GPU_MAX_HW_QUEUES the library saw when it was loaded, which is
+    what HIP applies), since every batch in flight holds a HIP stream and batches sharing a
+    hardware queue run one after another.  The digest pipeline (the default) needs no such
+    limit: default_group."""
     if HashAlgorithm(hash) != HashAlgorithm.Sha256:
         return 2
-    try:
-        hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
-    except ValueError:
-        hwq = 4
+    hwq = int(lib.cg_hw_queues()) if hw_queues is None else int(hw_queues)
     return max(2, min(20 if batch_bytes < (4 << 30) else 4, hwq - 2))
 
 
+def pipeline_create(device: int, group: int, lanes: int) -> int:
+    """cg_pipeline_create: a digest pipeline handle."""
+    h = ctypes.c_void_p()
+    _check(lib.cg_pipeline_create(device, group, lanes, ctypes.byref(h)))
+    return h.value
+
+
+def pipeline_submit(p: int, d_data_ptr: int, offs: np.ndarray, d_out_ptr: int, out_cap: int, o: "ChunkingOptions",
+                    hash: HashAlgorithm, inputs_ready: int = 0) -> BatchInFlight:
+    """cg_pipeline_submit: one device batch into the pipeline `p`."""
+    n = len(offs) - 1
+    h = ctypes.c_void_p()
+    _check(lib.cg_pipeline_submit(ctypes.c_void_p(p), ctypes.c_void_p(d_data_ptr), offs.ctypes.data, n, o.min_size,
+                                  o.avg_size, o.max_size, int(hash), ctypes.c_void_p(d_out_ptr), out_cap,
+                                  ctypes.c_void_p(inputs_ready or None), ctypes.byref(h)))
+    return BatchInFlight(h.value, n)
+
+
+def pipeline_flush(p: int) -> None:
+    _check(lib.cg_pipeline_flush(ctypes.c_void_p(p)))
+
+
+def pipeline_destroy(p: int) -> None:
+    lib.cg_pipeline_destroy(ctypes.c_void_p(p))
+
+
+PIPE_GROUP_BYTES = 16 << 30  # bytes of batches one merged SHA-256 digest launch takes (default_group)
+PIPE_LANES = 2               # merged digests in flight (cg_pipeline_create lanes)
+
+
+def default_group(hash: HashAlgorithm, batch_bytes: int) -> int:
+    """Batches per merged SHA-256 digest launch of the digest pipeline (cg_pipeline_create):
+    enough 1 GiB batches to fill the chip with their chains (a config-2 batch's digest is its
+    longest chunk's ~55 ms chain on ~18 workgroups), one for batches that fill it alone.
+    BLAKE3: 1 (not merged)."""
+    if HashAlgorithm(hash) != HashAlgorithm.Sha256:
+        return 1
+    return int(max(1, min(64, PIPE_GROUP_BYTES // max(int(batch_bytes), 1))))
+
+
 class BatchPipeline:
-    """Up to `depth` device batches in flight from one thread (an ingest worker draining
-    NAR batches): submit() queues a batch after its inputs-ready event only
-    (cg_chunk_batch_device_async_after) and, once `depth` are queued, waits for the oldest
-    and returns it; drain() waits for the rest.  Results come back in submission order as
-    (tag, nar_first).  The caller owns the buffers: a batch's input and output arrays must
-    stay untouched until its result has been returned (one output array per batch in
-    flight).  depth None = default_depth for the first batch's size."""
+    """Device batches in flight from one thread (an ingest worker draining NAR batches):
+    submit() queues a batch after its inputs-ready event only and, once `depth` are queued,
+    waits for the oldest and returns it; drain() waits for the rest.  Results come back in
+    submission order as (tag, nar_first).  The caller owns the buffers: a batch's input and
+    output arrays must stay untouched until its result has been returned (one output array
+    per batch in flight).
+
+    The product form is the digest pipeline (cg_pipeline_*): every batch's boundary stages
+    on one library stream, the SHA-256 digests of `group` consecutive batches merged into one
+    launch on one of `lanes` digest streams, each batch completing when its own chunks are
+    digested -- so the batches in flight need no hardware queue each.  depth None = (lanes +
+    1) x group, which keeps every lane busy while the next group forms.  group None =
+    default_group for the first batch's size; group=0 selects the round-5 per-batch-stream
+    path (cg_chunk_batch_device_async_after on `stream`, depth default_depth)."""
 
     def __init__(self, depth: int | None = None, min_size=None, avg_size=None, max_size=None,
-                 hash: HashAlgorithm = HashAlgorithm.Sha256, stream: int = 0):
+                 hash: HashAlgorithm = HashAlgorithm.Sha256, stream: int = 0, group: int | None = None,
+                 lanes: int | None = None, device: int = -1):
         if depth is not None and depth < 1:
             raise InvalidOptionsError(f"pipeline depth must be at least 1, got {depth}")
+        if group is not None and not 0 <= group <= 64:
+            raise InvalidOptionsError(f"pipeline group must be in 0..=64, got {group}")
         self.depth = depth
         self.options = ChunkingOptions.resolve(min_size, avg_size, max_size)
         self.hash = HashAlgorithm(hash)
         self.stream = stream
+        self.group = group
+        self.lanes = lanes or PIPE_LANES
+        self.device = device
+        self._p = None
+        self._opened = False
         self._q: deque = deque()
+
+    def _open(self, batch_bytes: int) -> None:
+        self._opened = True
+        if self.group is None:
+            self.group = default_group(self.hash, batch_bytes)
+        if self.group:
+            self._p = pipeline_create(self.device, self.group, self.lanes)
+            if self.depth is None:
+                self.depth = (self.lanes + 1) * self.group
+        elif self.depth is None:
+            self.depth = default_depth(self.hash, batch_bytes)
 
     def submit(self, d_data_ptr: int, nar_offsets: np.ndarray, d_out_ptr: int, out_cap: int,
                inputs_ready: int = 0, tag=None) -> list:
         offs = np.ascontiguousarray(nar_offsets, dtype=np.uint64)
-        if self.depth is None:
-            self.depth = default_depth(self.hash, int(offs[-1]) if len(offs) else 0)
+        if not self._opened:
+            self._open(int(offs[-1]) if len(offs) else 0)
         o = self.options
-        b = chunk_batch_device_async(d_data_ptr, offs, d_out_ptr, out_cap, o.min_size, o.avg_size, o.max_size,
-                                     hash=self.hash, stream=self.stream, inputs_ready=inputs_ready)
+        if self._p is not None:
+            b = pipeline_submit(self._p, d_data_ptr, offs, d_out_ptr, out_cap, o, self.hash, inputs_ready)
+        else:
+            b = chunk_batch_device_async(d_data_ptr, offs, d_out_ptr, out_cap, o.min_size, o.avg_size, o.max_size,
+                                         hash=self.hash, stream=self.stream, inputs_ready=inputs_ready)
         self._q.append((tag, b))
         done = []
         while len(self._q) >= self.depth:
@@ -448,12 +512,39 @@ class BatchPipeline:
             done.append((t, oldest.wait()))
         return done
 
+    def flush(self) -> None:
+        """Launch the digest of the batches queued since the last group (cg_pipeline_flush)."""
+        if self._p is not None:
+            pipeline_flush(self._p)
+
     def drain(self) -> list:
         done = []
+        self.flush()
         while self._q:
             t, b = self._q.popleft()
             done.append((t, b.wait()))
         return done
+
+    def stats(self) -> dict:
+        """Digest-pipeline counters (cg_pipeline_stats): merged groups and their batches, and
+        -- for groups launched while cg_set_profiling was on -- the digest kernel's time."""
+        if self._p is None:
+            return {}
+        out = (ctypes.c_double * 6)()
+        _check(lib.cg_pipeline_stats(ctypes.c_void_p(self._p), out))
+        return {"groups": int(out[0]), "batches": int(out[1]), "timed_groups": int(out[2]),
+                "digest_ms_sum": out[3], "digest_bytes_sum": out[4], "last_digest_ms": out[5]}
+
+    def close(self) -> None:
+        """Wait for everything queued, then free the pipeline's streams."""
+        try:
+            while self._q:
+                _, b = self._q.popleft()
+                b.wait()
+        finally:
+            if self._p is not None:
+                pipeline_destroy(self._p)
+                self._p = None
 
     def __len__(self) -> int:
         return len(self._q)
@@ -463,6 +554,10 @@ class BatchPipeline:
 
     def __exit__(self, *exc):
         # wait for everything queued, whatever happened (the workspaces go back to the pool)
+        try:
+            self.flush()
+        except ChunkingError:
+            pass
         while self._q:
             _, b = self._q.popleft()
             try:
@@ -470,7 +565,16 @@ class BatchPipeline:
             except ChunkingError:
                 if exc[0] is None:
                     raise
+        if self._p is not None:
+            pipeline_destroy(self._p)
+            self._p = None
         return False
+
+    def __del__(self):
+        if getattr(self, "_p", None) is not None:
+            self._q.clear()  # (each BatchInFlight waits for itself when collected)
+            pipeline_destroy(self._p)
+            self._p = None
 
 
 def batch_capacity(nar_offsets: np.ndarray, min_size=None) -> int:

@@ -162,18 +162,67 @@ bool launch_assemble(const uint64_t *d_nar_off, const uint64_t *d_cap_base, cons
                      uint64_t out_cap, uint64_t *d_chunk_abs, uint64_t *d_scan_tmp, hipStream_t st,
                      const B3PlanOut *b3, uint64_t *host_first, bool *wrote_host_first);
 
+// Per-member completion of a merged digest (the digest pipeline, pipeline.hip): chunk g of
+// the merged list belongs to member[g] and its digest goes to dst[g] (a device address)
+// instead of hash_base + g * stride.  Once a workgroup's digests are stored, one lane per
+// chunk counts its member down (remain[m]); the lane that takes it to zero writes the
+// member's host-mapped completion word *flag[m] = 1, or 2 if a spin guard fired on any of
+// the member's chunks (merr[m]).  So a member is done when its own longest chunk is, not
+// when the whole merged launch is.
+struct ShaNotify {
+    const uint64_t *dst = nullptr;
+    const uint32_t *member = nullptr;
+    uint32_t *remain = nullptr;
+    uint32_t *merr = nullptr;
+    uint32_t *const *flag = nullptr;
+};
+
 // d_order_tmp (sha256_order_tmp_elems(max_chunks) u32, or nullptr = identity order) holds
 // the longest-first lane order; max_len bounds every chunk length (bucket width);
 // `expected` estimates the chunk count (sizes the workgroup tiers).  d_err (one u32, zeroed
 // by the caller) becomes nonzero if a producer/consumer hand-off hit its spin guard.
+// `notify` (optional): per-member destinations and completion words (ShaNotify).
 void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
                    uint64_t max_chunks, uint64_t expected, uint64_t max_len, uint32_t *d_order_tmp,
                    uint8_t *d_hash_base, size_t hash_stride, uint32_t *d_err, hipStream_t st,
-                   bool latency_tiers = true);
+                   bool latency_tiers = true, const ShaNotify *notify = nullptr);
 size_t sha256_order_tmp_elems(uint64_t max_chunks);
 
-// Coalesced SHA-256 digest (runtime.hip's per-device coalescer): the chunks of up to
-// CG_COAL_MAX batches that are ready at the same time digested by ONE launch_sha256.
+// The digest pipeline's merged launch (pipeline.hip): up to CG_PIPE_MAX batches of one
+// caller, each after its boundary stages, digested by ONE k_sha256 with per-member
+// completion.  Member b's chunks are (data[b] + abs[b][i], out[b][i].length) for
+// i < min(*total[b], bound[b]); digests land in out[b][i].hash; flag[b] is the device
+// address of the member's host-mapped completion word.
+#define CG_PIPE_MAX 64
+struct PipeTable {
+    uint32_t n;
+    const uint8_t *data[CG_PIPE_MAX];
+    const uint64_t *abs[CG_PIPE_MAX];
+    DescRaw *out[CG_PIPE_MAX];
+    const uint64_t *total[CG_PIPE_MAX];
+    uint64_t bound[CG_PIPE_MAX];
+    uint32_t *flag[CG_PIPE_MAX];
+};
+// The merged arrays a PipeTable launch uses (bound_sum = sum of bound[b]).
+struct PipeBufs {
+    DescRaw *mdesc;      // bound_sum (lengths only)
+    uint64_t *mabs;      // bound_sum: chunk address - data[0]
+    uint64_t *mdst;      // bound_sum: digest destination
+    uint32_t *mmember;   // bound_sum
+    uint64_t *mtotal;    // 1
+    uint32_t *morder;    // sha256_order_tmp_elems(bound_sum)
+    uint32_t *remain;    // CG_PIPE_MAX
+    uint32_t *merr;      // CG_PIPE_MAX
+    uint32_t **mflag;    // CG_PIPE_MAX
+    uint32_t *err;       // 1: the launch's spin-guard word
+};
+// start / stop (optional): timing events around the digest kernel alone (after the merge)
+void launch_sha256_pipe(const PipeTable &t, uint64_t bound_sum, uint64_t expected, uint64_t max_len,
+                        const PipeBufs &b, hipStream_t st, hipEvent_t start = nullptr, hipEvent_t stop = nullptr);
+
+// Coalesced SHA-256 digest (runtime.hip's per-device coalescer of concurrent callers): the
+// chunks of up to CG_COAL_MAX batches that are ready at the same time digested by ONE
+// launch_sha256.
 // Member b's chunks are (data[b] + abs[b][i], out[b][i].length) for i < min(*total[b],
 // bound[b]); their digests land in out[b][i].hash and a spin-guard failure in *err[b].
 #define CG_COAL_MAX 32

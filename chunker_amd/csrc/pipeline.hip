@@ -1,0 +1,432 @@
+// pipeline.hip -- the digest pipeline (cg_pipeline_*, round 6): batches in flight from one
+// caller, their SHA-256 digests merged G at a time into ONE k_sha256 launch.
+//
+// A device batch's SHA-256 digest is bound by its longest chunk's serial chain (config 2:
+// ~55 ms for a 1 GiB batch) and, with the latency tiers, occupies only ~18 workgroups,
+// so one caller needs many batches in flight to fill the chip.  Round 5 bought that
+// concurrency with one HIP stream per batch in flight (cg_chunk_batch_device_async_after):
+// twenty batches needed GPU_MAX_HW_QUEUES=22, HIP's default 4 queues gave 36-60 GiB/s, and
+// an RCCL communicator in the same process took queues away (0.70 of the rate).  Here the
+// concurrency lives inside one launch instead:
+//   * every batch's boundary stages (scan, compaction, walk, assembly) run on the
+//     pipeline's one boundary stream, each after its own inputs-ready event;
+//   * the batches queued since the last digest form the open group; at G members (or
+//     when a member is waited for, or at cg_pipeline_flush) the group's chunk lists are
+//     merged (k_pipe_merge) and digested by one k_sha256 on one of the pipeline's L digest
+//     lanes (streams), so the next group's boundary stages and digest run beside it;
+//   * the digest kernel counts each member down as its chunks finish and raises the
+//     member's host-mapped completion word when its last chunk is stored (ShaNotify), so a
+//     batch completes when ITS longest chunk does, not when the merged launch ends, and a
+//     cg_batch_wait returns as soon as its own digests are in HBM.
+// The pipeline holds 1 + L streams however many batches are in flight.  They are created
+// with a CU mask covering the whole chip (CHUNKER_AMD_PIPE_STREAMS, below): such a stream
+// gets a hardware queue of its own instead of sharing the process's GPU_MAX_HW_QUEUES
+// pool.  BLAKE3 batches (a digest that fills the chip by itself) run whole on the
+// boundary stream, in submission order.
+// Replaces, across a caller's consecutive chunk_descriptors_with_hash calls, the
+// collect-then-hash sequence of src/chunking.rs:334-368.
+#include <chrono>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "runtime.h"
+
+namespace cgrt {
+
+struct PipeMember {
+    Workspace *ws = nullptr;
+    const uint8_t *d_data = nullptr;
+    cg_desc *d_out = nullptr;
+    const uint64_t *d_abs = nullptr, *d_total = nullptr;
+    uint64_t bound = 0, expected = 0, max_len = 0, bytes = 0;
+    volatile uint32_t *flag_host = nullptr;  // mapped: written by the digest kernel
+    uint32_t *flag_dev = nullptr;
+};
+
+struct PipeGroup {
+    std::vector<PipeMember> members;
+    hipEvent_t bdone = nullptr, done = nullptr, t0 = nullptr, t1 = nullptr;
+    bool launched = false, timed = false;
+    int rc = CG_OK;
+    std::string err;
+    uint64_t detail[3] = {0, 0, 0};
+    uint64_t bytes = 0;
+    cg_pipeline *owner = nullptr;  // while the group is open (a wait flushes it)
+    ~PipeGroup() {
+        for (hipEvent_t e : {bdone, done, t0, t1})
+            if (e) (void)hipEventDestroy(e);
+    }
+};
+
+struct PipeLane {
+    hipStream_t st = nullptr;
+    DevBuf mdesc, mabs, mdst, mmember, mtotal, morder, remain, merr, mflag, err;
+    std::shared_ptr<PipeGroup> last;
+};
+
+}  // namespace cgrt
+
+struct cg_pipeline {
+    int device = -1;
+    uint32_t group_max = 0, nlanes = 0;
+    hipStream_t bstream = nullptr;
+    std::vector<cgrt::PipeLane> lanes;
+    uint32_t next_lane = 0;
+    std::shared_ptr<cgrt::PipeGroup> open;
+    std::mutex mu;
+    // counters (cg_pipeline_stats)
+    uint64_t groups = 0, batches = 0, timed_groups = 0;
+    double digest_ms = 0, digest_bytes = 0, last_digest_ms = 0;
+    std::deque<std::shared_ptr<cgrt::PipeGroup>> timing;  // timed groups not yet read
+};
+
+namespace cgrt {
+
+// Stream kind of the pipeline's streams (CHUNKER_AMD_PIPE_STREAMS, read once):
+// "cumask" (default) = a CU mask over every CU, which HIP backs with a hardware queue of
+// its own; "high" = the high-priority pool; "plain" = ordinary streams (the shared pool).
+static int pipe_stream_kind() {
+    static const int k = [] {
+        const char *e = getenv("CHUNKER_AMD_PIPE_STREAMS");
+        if (e && !strcmp(e, "plain")) return 0;
+        if (e && !strcmp(e, "high")) return 1;
+        return 2;
+    }();
+    return k;
+}
+
+static int make_stream(hipStream_t *s) {
+    const int kind = pipe_stream_kind();
+    if (kind == 1) {
+        int lo = 0, hi = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIP_TRY(hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi));
+    } else if (kind == 2) {
+        int dev = 0;
+        HIP_TRY(hipGetDevice(&dev));
+        int ncu = 0;
+        HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+        std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0xffffffffu);
+        HIP_TRY(hipExtStreamCreateWithCUMask(s, (uint32_t)mask.size(), mask.data()));
+    } else {
+        HIP_TRY(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+    }
+    return CG_OK;
+}
+
+// The group's failure, as seen by each of its members' waits.
+static int group_fail(PipeGroup &g, int rc) {
+    g.rc = rc;
+    g.err = cg_last_error_message();
+    cg_last_error_detail(g.detail);
+    return rc;
+}
+
+// Launch the open group's merged digest on the next lane (pipeline lock held).
+static int flush_locked(cg_pipeline *p) {
+    std::shared_ptr<PipeGroup> g = std::move(p->open);
+    p->open.reset();
+    if (!g || g->members.empty()) return CG_OK;
+    g->owner = nullptr;
+    g->launched = true;
+    PipeLane &L = p->lanes[p->next_lane];
+    p->next_lane = (p->next_lane + 1) % p->nlanes;
+    auto launch = [&]() -> int {
+        HIP_TRY(hipEventRecord(g->bdone, p->bstream));
+        HIP_TRY(hipStreamWaitEvent(L.st, g->bdone, 0));
+        cg::PipeTable t{};
+        t.n = (uint32_t)g->members.size();
+        uint64_t bound = 0, expected = 0, max_len = 0;
+        for (uint32_t b = 0; b < t.n; ++b) {
+            const PipeMember &m = g->members[b];
+            t.data[b] = m.d_data;
+            t.abs[b] = m.d_abs;
+            t.out[b] = reinterpret_cast<DescRaw *>(m.d_out);
+            t.total[b] = m.d_total;
+            t.bound[b] = m.bound;
+            t.flag[b] = m.flag_dev;
+            bound += m.bound;
+            expected += m.expected;
+            max_len = std::max(max_len, m.max_len);
+        }
+        // growing a lane buffer frees the old one, which the lane's previous group may
+        // still read: wait for it first (only until the buffers have their steady size)
+        const uint64_t ord = cg::sha256_order_tmp_elems(bound) * 4;
+        const bool grow = L.mdesc.cap < (bound + 1) * sizeof(DescRaw) || L.morder.cap < ord || !L.remain.p;
+        if (grow && L.last) HIP_TRY(hipEventSynchronize(L.last->done));
+        int rc;
+        if ((rc = L.mdesc.ensure((bound + 1) * sizeof(DescRaw), "pipeline descriptors"))) return rc;
+        if ((rc = L.mabs.ensure((bound + 1) * 8, "pipeline addresses"))) return rc;
+        if ((rc = L.mdst.ensure((bound + 1) * 8, "pipeline destinations"))) return rc;
+        if ((rc = L.mmember.ensure((bound + 1) * 4, "pipeline members"))) return rc;
+        if ((rc = L.morder.ensure(ord, "pipeline order"))) return rc;
+        if ((rc = L.mtotal.ensure(64, "pipeline total"))) return rc;
+        if ((rc = L.remain.ensure(CG_PIPE_MAX * 4, "pipeline counters"))) return rc;
+        if ((rc = L.merr.ensure(CG_PIPE_MAX * 4, "pipeline counters"))) return rc;
+        if ((rc = L.mflag.ensure(CG_PIPE_MAX * 8, "pipeline flags"))) return rc;
+        if ((rc = L.err.ensure(64, "pipeline spin guard"))) return rc;
+        cg::PipeBufs pb{L.mdesc.as<DescRaw>(),  L.mabs.as<uint64_t>(),  L.mdst.as<uint64_t>(),
+                        L.mmember.as<uint32_t>(), L.mtotal.as<uint64_t>(), L.morder.as<uint32_t>(),
+                        L.remain.as<uint32_t>(), L.merr.as<uint32_t>(),  L.mflag.as<uint32_t *>(),
+                        L.err.as<uint32_t>()};
+        cg::launch_sha256_pipe(t, bound, expected, max_len, pb, L.st, g->timed ? g->t0 : nullptr,
+                               g->timed ? g->t1 : nullptr);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(g->done, L.st));
+        return CG_OK;
+    };
+    const int rc = launch();
+    if (rc) {
+        // whatever was queued may still read the members' buffers: drain before their
+        // waits release the workspaces
+        (void)hipStreamSynchronize(L.st);
+        (void)hipStreamSynchronize(p->bstream);
+        return group_fail(*g, rc);
+    }
+    L.last = g;
+    ++p->groups;
+    p->batches += g->members.size();
+    if (g->timed) p->timing.push_back(g);
+    return CG_OK;
+}
+
+// Fold the timing of groups that have completed into the counters (pipeline lock held).
+static void read_timing(cg_pipeline *p) {
+    while (!p->timing.empty()) {
+        std::shared_ptr<PipeGroup> g = p->timing.front();
+        if (hipEventQuery(g->done) != hipSuccess) break;
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, g->t0, g->t1) == hipSuccess) {
+            p->digest_ms += ms;
+            p->digest_bytes += (double)g->bytes;
+            p->last_digest_ms = ms;
+            ++p->timed_groups;
+        }
+        p->timing.pop_front();
+    }
+}
+
+int pipeline_wait(cg_batch *b, uint64_t *nar_first) {
+    std::unique_ptr<cg_batch> hold(b);
+    std::shared_ptr<PipeGroup> g = b->group;
+    WsGuard guard{b->ws};
+    int rc = CG_OK;
+    if (!g->launched) {  // the batch is in the open group: launch it now
+        cg_pipeline *p = g->owner;
+        DeviceScope scope;
+        if ((rc = scope.set(p->device))) return rc;
+        std::lock_guard<std::mutex> lk(p->mu);
+        if (!g->launched) rc = flush_locked(p);
+    }
+    if (g->rc) return fail_detail(g->rc, g->err, g->detail);
+    if (rc) return rc;
+    const PipeMember &m = g->members[b->member];
+    // the member's completion word (ShaNotify): yield for the first ~0.2 ms, then poll
+    // every 20 us; the group's end event catches a word that never arrives
+    const auto t0 = std::chrono::steady_clock::now();
+    uint32_t f = 0;
+    for (;;) {
+        f = __atomic_load_n(m.flag_host, __ATOMIC_ACQUIRE);
+        if (f) break;
+        if (hipEventQuery(g->done) == hipSuccess) {
+            f = __atomic_load_n(m.flag_host, __ATOMIC_ACQUIRE);
+            break;
+        }
+        if (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(200))
+            std::this_thread::yield();
+        else
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    if (f == 0) return fail(CG_E_IO, "digest pipeline: the merged digest ended without completing this batch");
+    if (f != 1)
+        return fail(CG_E_IO, "SHA-256 digest: a producer/consumer hand-off hit the kernel's spin guard; "
+                             "the digests of this call are invalid");
+    return finish_batch(b->ws, b->st, b->bl, nar_first);
+}
+
+}  // namespace cgrt
+
+using namespace cgrt;
+
+extern "C" {
+
+int cg_pipeline_create(int device, uint32_t group_batches, uint32_t lanes, cg_pipeline **out) {
+    clear_error();
+    if (!out) return fail(CG_E_IO, "null pipeline handle pointer");
+    *out = nullptr;
+    if (group_batches > CG_PIPE_MAX) {
+        char buf[96];
+        snprintf(buf, sizeof buf, "pipeline group must be at most %u batches, got %u", CG_PIPE_MAX, group_batches);
+        return fail(CG_E_INVALID_OPTIONS, buf);
+    }
+    if (lanes > 8) return fail(CG_E_INVALID_OPTIONS, "pipeline lanes must be at most 8");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return fail(CG_E_NO_DEVICE, "no HIP device visible: the chunker engine has no CPU fallback");
+    if (device < 0) {
+        int cur = 0;
+        HIP_TRY(hipGetDevice(&cur));
+        device = cur;
+    }
+    if (device >= n) return fail(CG_E_NO_DEVICE, "pipeline device index out of range");
+    DeviceScope scope;
+    int rc = scope.set(device);
+    if (rc) return rc;
+    std::unique_ptr<cg_pipeline> p(new cg_pipeline());
+    p->device = device;
+    p->group_max = group_batches ? group_batches : 16;
+    p->nlanes = lanes ? lanes : 2;
+    p->lanes.resize(p->nlanes);
+    if ((rc = make_stream(&p->bstream))) return rc;
+    for (auto &L : p->lanes)
+        if ((rc = make_stream(&L.st))) return rc;
+    *out = p.release();
+    return CG_OK;
+}
+
+int cg_pipeline_submit(cg_pipeline *p, const uint8_t *d_data, const uint64_t *nar_offsets, size_t n_nars,
+                       uint64_t min_size, uint64_t avg_size, uint64_t max_size, int algo, cg_desc *d_out,
+                       size_t out_cap, void *inputs_ready, cg_batch **batch) {
+    clear_error();
+    if (!p || !batch) return fail(CG_E_IO, "null pipeline or batch handle pointer");
+    *batch = nullptr;
+    if (algo != CG_BLAKE3 && algo != CG_SHA256) return fail(CG_E_INVALID_OPTIONS, "unknown hash algorithm");
+    Opts o;
+    int rc = resolve(min_size, avg_size, max_size, &o, nullptr, 0);
+    if (rc) return rc;
+    if (n_nars && nar_offsets[0] != 0)
+        return fail_bounds(nar_offsets[n_nars], nar_offsets[0], 0, "device batch offsets must start at 0");
+    if ((rc = check_tables())) return rc;
+    DeviceScope scope;
+    if ((rc = scope.set(p->device))) return rc;
+    Workspace *ws = nullptr;
+    if ((rc = acquire(&ws))) return rc;
+    std::lock_guard<std::mutex> lk(p->mu);
+    auto undo = [&](int code) {
+        (void)hipStreamSynchronize(p->bstream);
+        release(ws);
+        return code;
+    };
+    if (inputs_ready && hipStreamWaitEvent(p->bstream, static_cast<hipEvent_t>(inputs_ready), 0) != hipSuccess)
+        return undo(fail(CG_E_IO, "hipStreamWaitEvent(inputs_ready) failed"));
+    BatchLaunch bl;
+    if (algo == CG_BLAKE3) {  // the whole batch on the boundary stream, in submission order
+        if ((rc = launch_batch(ws, d_data, nar_offsets, n_nars, o, algo, d_out, out_cap, p->bstream, nullptr,
+                               nullptr, true, &bl)))
+            return undo(rc);
+        *batch = new cg_batch{ws, p->bstream, bl, nullptr, 0, p->device};
+        return CG_OK;
+    }
+    if ((rc = ws->done_flag.ensure(64, /*mapped=*/true))) return undo(rc);
+    __atomic_store_n(ws->done_flag.as<uint32_t>(), 0u, __ATOMIC_RELEASE);
+    if ((rc = launch_batch(ws, d_data, nar_offsets, n_nars, o, algo, d_out, out_cap, p->bstream, nullptr, nullptr,
+                           /*digest=*/false, &bl)))
+        return undo(rc);
+    // the digest's sizes, as launch_batch's own digest would take them
+    uint64_t total_cap = 0;
+    for (size_t i = 0; i < n_nars; ++i) total_cap += capacity_of(nar_offsets[i + 1] - nar_offsets[i], o.min);
+    const uint64_t total_len = n_nars ? nar_offsets[n_nars] : 0;
+    PipeMember m;
+    m.ws = ws;
+    m.d_data = d_data;
+    m.d_out = d_out;
+    m.d_abs = ws->chunk_abs.as<uint64_t>();
+    m.d_total = ws->nar_first.as<uint64_t>() + n_nars;
+    m.bound = std::min<uint64_t>(total_cap, out_cap);
+    m.expected = std::min<uint64_t>(m.bound, total_len / (o.min + o.avg) + n_nars);
+    m.max_len = o.max;
+    m.bytes = total_len;
+    m.flag_host = ws->done_flag.as<uint32_t>();
+    m.flag_dev = static_cast<uint32_t *>(ws->done_flag.dev);
+    if (!p->open) {
+        auto g = std::make_shared<PipeGroup>();
+        g->timed = g_profiling.load() != 0;
+        if (hipEventCreateWithFlags(&g->bdone, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&g->done, hipEventDisableTiming) != hipSuccess ||
+            (g->timed && (hipEventCreate(&g->t0) != hipSuccess || hipEventCreate(&g->t1) != hipSuccess)))
+            return undo(fail(CG_E_IO, "hipEventCreate failed"));
+        g->owner = p;
+        p->open = g;
+    }
+    std::shared_ptr<PipeGroup> g = p->open;
+    g->members.push_back(m);
+    g->bytes += total_len;
+    *batch = new cg_batch{ws, p->bstream, bl, g, (uint32_t)(g->members.size() - 1), p->device};
+    if (g->members.size() >= p->group_max) flush_locked(p);  // a failure reaches every member's wait
+    return CG_OK;
+}
+
+int cg_pipeline_flush(cg_pipeline *p) {
+    clear_error();
+    if (!p) return fail(CG_E_IO, "null pipeline handle");
+    DeviceScope scope;
+    int rc = scope.set(p->device);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(p->mu);
+    return flush_locked(p);
+}
+
+int cg_batch_event(cg_batch *batch, void **event) {
+    clear_error();
+    if (!batch || !event) return fail(CG_E_IO, "null batch handle or event pointer");
+    *event = nullptr;
+    if (!batch->group) {
+        *event = batch->bl.done;
+        return CG_OK;
+    }
+    std::shared_ptr<PipeGroup> g = batch->group;
+    if (!g->launched) {
+        cg_pipeline *p = g->owner;
+        DeviceScope scope;
+        int rc = scope.set(p->device);
+        if (rc) return rc;
+        std::lock_guard<std::mutex> lk(p->mu);
+        if (!g->launched) flush_locked(p);
+    }
+    if (g->rc) return fail_detail(g->rc, g->err, g->detail);
+    *event = g->done;
+    return CG_OK;
+}
+
+int cg_pipeline_stats(cg_pipeline *p, double out[6]) {
+    clear_error();
+    if (!p || !out) return fail(CG_E_IO, "null pipeline handle or output");
+    std::lock_guard<std::mutex> lk(p->mu);
+    read_timing(p);
+    out[0] = (double)p->groups;
+    out[1] = (double)p->batches;
+    out[2] = (double)p->timed_groups;
+    out[3] = p->digest_ms;
+    out[4] = p->digest_bytes;
+    out[5] = p->last_digest_ms;
+    return CG_OK;
+}
+
+void cg_pipeline_destroy(cg_pipeline *p) {
+    if (!p) return;
+    {
+        DeviceScope scope;
+        (void)scope.set(p->device);
+        std::lock_guard<std::mutex> lk(p->mu);
+        (void)flush_locked(p);  // a batch still in the open group gets its digest
+        for (auto &L : p->lanes)
+            if (L.st) (void)hipStreamSynchronize(L.st);
+        if (p->bstream) (void)hipStreamSynchronize(p->bstream);
+        p->timing.clear();
+        for (auto &L : p->lanes) {
+            L.last.reset();
+            for (DevBuf *d : {&L.mdesc, &L.mabs, &L.mdst, &L.mmember, &L.mtotal, &L.morder, &L.remain, &L.merr,
+                              &L.mflag, &L.err})
+                d->release();
+            if (L.st) (void)hipStreamDestroy(L.st);
+        }
+        if (p->bstream) (void)hipStreamDestroy(p->bstream);
+    }
+    delete p;
+}
+
+}  // extern "C"

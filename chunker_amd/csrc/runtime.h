@@ -4,6 +4,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
 #include <memory>
 #include <mutex>
@@ -115,6 +116,7 @@ struct Workspace {
         scanq;  // scanq: the persistent scan's work queue (cg::ScanQueue), zeroed once
     bool scanq_zeroed = false;  // the zeroing memset of scanq has been queued
     PinBuf stage, err_stage, first_host;  // first_host: mapped, the assembly writes the NAR index there
+    PinBuf done_flag;  // mapped: a pipeline batch's completion word, written by its merged digest
     hipEvent_t ev[EV_N] = {};
     // CAS ids run on side_stream, concurrently with the digest: both stages are bound by
     // their longest chunk's serial chain, not by the chip, so they overlap for free.
@@ -226,4 +228,37 @@ struct CoalEntry {
 int coalesced_sha256(CoalEntry *e);
 bool coalesce_worth(int dev);
 
+// Which device a call runs on: the device set for the scope, the caller's restored after.
+struct DeviceScope {
+    int prev = -1;
+    int set(int dev) {
+        HIP_TRY(hipGetDevice(&prev));
+        if (prev != dev) HIP_TRY(hipSetDevice(dev));
+        return CG_OK;
+    }
+    ~DeviceScope() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+struct PipeGroup;  // pipeline.hip
+extern std::atomic<int> g_profiling;  // cg_set_profiling mode
+
 }  // namespace cgrt
+
+// An asynchronous batch (cg_chunk_batch_device_async, cg_pipeline_submit): its workspace
+// stays reserved, and its results unread, until cg_batch_wait.  A pipeline batch also
+// names its digest group and its index in it (pipeline.hip).
+struct cg_pipeline;
+struct cg_batch {
+    cgrt::Workspace *ws;
+    hipStream_t st;
+    cgrt::BatchLaunch bl;
+    std::shared_ptr<cgrt::PipeGroup> group;  // pipeline batches only
+    uint32_t member = 0;
+    int device = -1;
+};
+namespace cgrt {
+int pipeline_wait(cg_batch *b, uint64_t *nar_first);  // pipeline.hip
+}

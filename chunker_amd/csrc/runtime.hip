@@ -799,6 +799,10 @@ int launch_batch(Workspace *ws, const uint8_t *d_data, const uint64_t *h_nar_off
     if (inputs_ready && algo == CG_SHA256) {
         bs = ws->stream;
         HIP_TRY(hipStreamWaitEvent(bs, inputs_ready, 0));
+    } else if (inputs_ready) {
+        // BLAKE3: stream order AND the event (its input may be written on another stream,
+        // e.g. a copy stream, that `st` knows nothing of)
+        HIP_TRY(hipStreamWaitEvent(st, inputs_ready, 0));
     }
     if ((rc = ensure_scan_queue(ws, bs))) return rc;
     // nar_off (n+1) then cap_base (n+1): one block, one copy (s_cap follows s_off in staging)
@@ -1177,14 +1181,6 @@ using namespace cgrt;
 // The retained bytes live in HBM: each push copies only its new bytes H2D, straight
 // from the caller's buffer, after the device-resident tail (no host-side copy of
 // the stream); after a drain the tail moves to the front of the other buffer.
-// An asynchronous batch (cg_chunk_batch_device_async): its workspace stays reserved, and
-// its results unread, until cg_batch_wait.
-struct cg_batch {
-    cgrt::Workspace *ws;
-    hipStream_t st;
-    cgrt::BatchLaunch bl;
-};
-
 struct cg_push {
     Opts o;
     int algo;
@@ -1451,13 +1447,14 @@ int cg_chunk_batch_device_async_after(const uint8_t *d_data, const uint64_t *nar
         release(ws);
         return rc;
     }
-    *batch = new cg_batch{ws, st, bl};
+    *batch = new cg_batch{ws, st, bl, nullptr, 0, ws->device};
     return CG_OK;
 }
 
 int cg_batch_wait(cg_batch *batch, uint64_t *nar_first) {
     clear_error();
     if (!batch) return fail(CG_E_IO, "null batch handle");
+    if (batch->group) return pipeline_wait(batch, nar_first);  // frees the handle
     const int rc = finish_batch(batch->ws, batch->st, batch->bl, nar_first);
     release(batch->ws);
     delete batch;

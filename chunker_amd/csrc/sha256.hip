@@ -708,7 +708,8 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
                                                uint8_t *__restrict__ hash_base, size_t stride,
                                                unsigned long long *__restrict__ diag, uint32_t mode,
                                                uint32_t nquad, uint32_t npair, uint32_t spin_limit,
-                                               uint32_t *__restrict__ err, const uint32_t *__restrict__ need) {
+                                               uint32_t *__restrict__ err, const uint32_t *__restrict__ need,
+                                               ShaNotify nt) {
     unsigned long long t_start = diag ? __builtin_amdgcn_s_memtime() : 0ull, t_spin = 0;
     const unsigned long long rt_start = diag ? __builtin_amdgcn_s_memrealtime() : 0ull;
     if (need) {  // latency tiers (k_len_base): no more lanes per chunk than its length needs
@@ -786,9 +787,11 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
             split_consumer<false>(sW, row, hi, lane, NB, NBmin, nbt, &s_ready, &s_done, st, &t_spin, diag != nullptr);
         if (diag && lane == 0) sha_diag_consumer(diag, t_spin, t_start, rt_start);
         if (valid && (!quad || (lane & 3u) == 0)) {  // hi: H0..H3 (bytes 0-15), lo: H4..H7 (bytes 16-31)
-            uint4 *o = reinterpret_cast<uint4 *>(hash_base + ci * stride + (hi ? 0 : 16));
+            uint8_t *hb = nt.dst ? reinterpret_cast<uint8_t *>(nt.dst[ci]) : hash_base + ci * stride;
+            uint4 *o = reinterpret_cast<uint4 *>(hb + (hi ? 0 : 16));
             *o = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]), __builtin_bswap32(st[2]),
                             __builtin_bswap32(st[3]));
+            if (nt.remain) __threadfence();  // visible device-wide before the member is counted down
         }
     } else {
         uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
@@ -825,17 +828,31 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
         }
         if (diag && lane == 0) sha_diag_consumer(diag, t_spin, t_start, rt_start);
         if (valid) {
-            uint4 *o = reinterpret_cast<uint4 *>(hash_base + ci * stride);
+            uint4 *o = reinterpret_cast<uint4 *>(nt.dst ? reinterpret_cast<uint8_t *>(nt.dst[ci]) : hash_base + ci * stride);
             o[0] = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]), __builtin_bswap32(st[2]),
                               __builtin_bswap32(st[3]));
             o[1] = make_uint4(__builtin_bswap32(st[4]), __builtin_bswap32(st[5]), __builtin_bswap32(st[6]),
                               __builtin_bswap32(st[7]));
+            if (nt.remain) __threadfence();  // visible device-wide before the member is counted down
         }
     }
     // both waves are past their last wait: report an expired spin guard (vector store)
     __syncthreads();
-    if (threadIdx.x == 0 && __hip_atomic_load(&s_sync[SY_TIMEOUT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
-        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool timed_out = __hip_atomic_load(&s_sync[SY_TIMEOUT], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+    if (threadIdx.x == 0 && timed_out) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // per-member completion (ShaNotify): one consumer lane per chunk -- the one-lane tier's
+    // own lane, a split chunk's hi lane that stored H0..H3 -- counts its member down once
+    // every digest of this workgroup is stored and fenced; the last one out raises the
+    // member's host-mapped completion word (system scope, vector store)
+    if (nt.remain && !producer && valid && (!split || (hi && (!quad || (lane & 3u) == 0)))) {
+        const uint32_t m = nt.member[ci];
+        if (timed_out) __hip_atomic_fetch_or(&nt.merr[m], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__hip_atomic_fetch_sub(&nt.remain[m], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == 1u) {
+            const uint32_t e = __hip_atomic_load(&nt.merr[m], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+            __threadfence_system();
+            __hip_atomic_store(nt.flag[m], e ? 2u : 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1023,7 +1040,7 @@ thread_local uint32_t t_sha_tiers[4];
 void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_desc, const uint64_t *d_total,
                    uint64_t max_chunks, uint64_t expected, uint64_t max_len, uint32_t *d_order_tmp,
                    uint8_t *d_hash_base, size_t hash_stride, uint32_t *d_err, hipStream_t st,
-                   bool latency_tiers) {
+                   bool latency_tiers, const ShaNotify *notify) {
     if (max_chunks == 0) return;
     uint32_t nquad = 0, npair = 0;
     bool fill = false;
@@ -1047,7 +1064,8 @@ void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
     t_sha_tiers[3] = (uint32_t)pad;
     hipLaunchKernelGGL(k_sha256, dim3(nwg), dim3(128), pad, st, d_data, d_abs,
                        (const DescRaw *)d_desc, d_total, max_chunks, order, d_hash_base, hash_stride, g_sha_diag,
-                       g_sha_mode, nquad, npair, g_sha_spin_limit, d_err, order ? need : nullptr);
+                       g_sha_mode, nquad, npair, g_sha_spin_limit, d_err, order ? need : nullptr,
+                       notify ? *notify : ShaNotify{});
 }
 
 // ---------------------------------------------------------------------------
@@ -1123,6 +1141,97 @@ void launch_sha256_coalesced(const CoalTable &t, uint64_t bound_sum, uint64_t ex
     launch_sha256(t.data[0], mabs, mdesc, mtotal, bound_sum, expected, max_len, morder_tmp,
                   reinterpret_cast<uint8_t *>(mdesc) + offsetof(DescRaw, hash), sizeof(DescRaw), merr, st);
     hipLaunchKernelGGL(k_coal_scatter, dim3(grid), dim3(256), 0, st, t, mdesc, merr);
+}
+
+// ---------------------------------------------------------------------------
+// The digest pipeline's merged launch (pipeline.hip, round 6).  One caller's queued
+// batches are digested G at a time by ONE k_sha256, so the batches in flight no longer
+// need a HIP stream -- a hardware queue -- each: the chip is filled by the merged launch's
+// workgroups, not by concurrent launches.  k_pipe_merge builds the merged chunk list
+// (lengths, addresses relative to member 0's base, digest destinations inside each
+// member's own descriptors, member index) and arms the per-member counters; k_sha256 then
+// signals each member as soon as its last chunk is digested (ShaNotify).
+// ---------------------------------------------------------------------------
+// Member prefix of the chunk counts (n <= CG_PIPE_MAX = one wave): pre[b] = chunks of
+// members 0..b-1, pre[n] = all.
+__device__ __forceinline__ void pipe_prefix(const PipeTable &t, uint64_t *pre) {
+    static_assert(CG_PIPE_MAX <= 64, "one wave scans the member counts");
+    if (threadIdx.x < 64) {
+        const uint32_t b = threadIdx.x;
+        uint64_t c = 0;
+        if (b < t.n) {
+            c = *t.total[b];
+            if (c > t.bound[b]) c = t.bound[b];
+        }
+        uint64_t x = c;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint64_t y = __shfl_up(x, d, 64);
+            if (b >= d) x += y;
+        }
+        if (b < t.n) pre[b] = x - c;
+        if (b == t.n - 1) pre[t.n] = x;
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t pipe_member(const uint64_t *pre, uint32_t n, uint64_t g) {
+    uint32_t lo = 0, hi = n - 1;  // the last b with pre[b] <= g
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (pre[mid] <= g) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(256) void k_pipe_merge(PipeTable t, PipeBufs m) {
+    __shared__ uint64_t pre[CG_PIPE_MAX + 1];
+    pipe_prefix(t, pre);
+    const uint64_t total = pre[t.n];
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) {
+            *m.mtotal = total;
+            *m.err = 0;
+        }
+        if (threadIdx.x < t.n) {
+            const uint32_t b = threadIdx.x;
+            const uint32_t c = (uint32_t)(pre[b + 1] - pre[b]);
+            m.remain[b] = c;
+            m.merr[b] = 0;
+            m.mflag[b] = t.flag[b];
+            // a member without chunks (empty NARs only) is complete now
+            if (c == 0) __hip_atomic_store(t.flag[b], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    const uint64_t base = (uint64_t)t.data[0];
+    for (uint64_t g = (uint64_t)blockIdx.x * 256 + threadIdx.x; g < total; g += (uint64_t)gridDim.x * 256) {
+        const uint32_t b = pipe_member(pre, t.n, g);
+        const uint64_t i = g - pre[b];
+        m.mdesc[g].length = t.out[b][i].length;
+        m.mabs[g] = (uint64_t)t.data[b] + t.abs[b][i] - base;  // data[0] + mabs[g] = the chunk's address
+        m.mdst[g] = (uint64_t)t.out[b][i].hash;
+        m.mmember[g] = b;
+    }
+}
+
+void launch_sha256_pipe(const PipeTable &t, uint64_t bound_sum, uint64_t expected, uint64_t max_len,
+                        const PipeBufs &b, hipStream_t st, hipEvent_t start, hipEvent_t stop) {
+    if (t.n == 0) return;
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((bound_sum + 255) / 256, 1024));
+    hipLaunchKernelGGL(k_pipe_merge, dim3(grid), dim3(256), 0, st, t, b);
+    if (start) (void)hipEventRecord(start, st);
+    if (bound_sum) {
+        ShaNotify nt;
+        nt.dst = b.mdst;
+        nt.member = b.mmember;
+        nt.remain = b.remain;
+        nt.merr = b.merr;
+        nt.flag = b.mflag;
+        launch_sha256(t.data[0], b.mabs, b.mdesc, b.mtotal, bound_sum, expected, max_len, b.morder, nullptr, 0, b.err,
+                      st, true, &nt);
+    }
+    if (stop) (void)hipEventRecord(stop, st);
 }
 
 #ifdef CG_DIAG

@@ -404,6 +404,10 @@ const int g_hw_queues_at_load = [] {
 
 extern "C" {
 
+// Test/tuning query (not in the header): the hardware-queue count above, which the
+// Python depth rule (chunking.default_depth) uses instead of the environment's current value.
+int cg_hw_queues(void) { return g_hw_queues_at_load; }
+
 cg_stream *cg_stream_new(uint64_t min_size, uint64_t avg_size, uint64_t max_size, int algo, uint64_t slice_bytes,
                          uint64_t inflight_bytes, int *status) {
     clear_error();

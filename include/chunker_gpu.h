@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define CG_ABI_VERSION 2u
+#define CG_ABI_VERSION 3u
 
 /* Status codes.  1..5 map 1:1 onto ChunkingError (src/chunking.rs:33-51) so the
  * host shim can rebuild the exact Display strings. */
@@ -129,6 +129,41 @@ int cg_chunk_batch_device_async_after(const uint8_t *d_data, const uint64_t *nar
                                       uint64_t min_size, uint64_t avg_size, uint64_t max_size, int algo,
                                       cg_desc *d_out, size_t out_cap, void *stream, void *inputs_ready,
                                       cg_batch **batch);
+
+/* Digest pipeline: many device batches in flight from one caller without a HIP stream
+ * (hardware queue) per batch.  Replaces, across a caller's consecutive
+ * chunk_descriptors_with_hash calls, the collect-then-hash sequence of
+ * src/chunking.rs:334-368: every batch's candidate scan, cut walk and descriptor assembly
+ * run on the pipeline's boundary stream, each after its own `inputs_ready` event (a
+ * hipEvent_t recorded after the last write to d_data and the last use of d_out; NULL = no
+ * wait); the SHA-256 digests of up to `group_batches` consecutive batches (0 = 16, at most
+ * 64) are then computed by ONE merged launch on one of `lanes` digest streams (0 = 2, at
+ * most 8), so the next group's boundary stages and digest run beside it.  A group is
+ * launched when it is full, when one of its batches is waited for (cg_batch_wait,
+ * cg_batch_event) or by cg_pipeline_flush.  Each batch completes as soon as its own chunks
+ * are digested (the digest kernel signals it), not when its whole group does.  BLAKE3
+ * batches run whole on the boundary stream, in submission order.  The pipeline uses
+ * 1 + lanes streams on `device` (-1 = the current device; the caller's current device is
+ * left unchanged by every pipeline call), each with a hardware queue of its own, whatever
+ * GPU_MAX_HW_QUEUES is.  A batch is waited for with cg_batch_wait exactly once, as for
+ * cg_chunk_batch_device_async; results, errors and nar_first are the same as those of
+ * cg_chunk_batch_device on the same inputs.  A pipeline is single-owner; its batches may
+ * be waited for from any thread, also after cg_pipeline_destroy (which launches a still
+ * open group and waits for the pipeline's streams). */
+typedef struct cg_pipeline cg_pipeline;
+int cg_pipeline_create(int device, uint32_t group_batches, uint32_t lanes, cg_pipeline **out);
+int cg_pipeline_submit(cg_pipeline *p, const uint8_t *d_data, const uint64_t *nar_offsets, size_t n_nars,
+                       uint64_t min_size, uint64_t avg_size, uint64_t max_size, int algo, cg_desc *d_out,
+                       size_t out_cap, void *inputs_ready, cg_batch **batch);
+int cg_pipeline_flush(cg_pipeline *p);
+/* out = {groups launched, batches in them, groups timed, their digest-kernel ms (sum), their
+ * bytes (sum), the last timed group's ms}; groups are timed while cg_set_profiling is on. */
+int cg_pipeline_stats(cg_pipeline *p, double out[6]);
+void cg_pipeline_destroy(cg_pipeline *p);
+/* A hipEvent_t that completes once the batch's results are in HBM (for a pipeline batch:
+ * the end of its group's merged digest), so device work can be ordered after it without a
+ * host wait; launches the batch's group if it is still open.  Valid until cg_batch_wait. */
+int cg_batch_event(cg_batch *batch, void **event);
 
 /* PushChunker (src/chunking.rs:753-829) over drain_finalized_chunks (:541-673).
  * push/finish write the chunks that became final; `out_cap` must be at least

@@ -127,7 +127,7 @@ static READY: OnceLock<Result<(), String>> = OnceLock::new();
 pub fn available() -> bool {
     READY
         .get_or_init(|| unsafe {
-            if cg_abi_version() != 2 {
+            if cg_abi_version() != 3 {
                 return Err("chunker_amd ABI version".into());
             }
             check(cg_set_cdc_tables(&tables::GEAR, &tables::MASKS)).map_err(|e| format!("{e:?}"))?;

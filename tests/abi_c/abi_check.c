@@ -29,7 +29,7 @@ _Static_assert(offsetof(cg_desc, offset) == 0, "offset at 0");
 _Static_assert(offsetof(cg_desc, length) == 8, "length at 8");
 _Static_assert(offsetof(cg_desc, hash) == 16, "hash at 16");
 _Static_assert(sizeof(((cg_desc *)0)->hash) == 32, "32-byte digest");
-_Static_assert(CG_ABI_VERSION == 2u, "ABI version 2");
+_Static_assert(CG_ABI_VERSION == 3u, "ABI version 3");
 _Static_assert(CG_OK == 0 && CG_E_BOUNDS == 1 && CG_E_IO == 2 && CG_E_ZERO_LENGTH_CHUNK == 3 &&
                    CG_E_INVALID_OPTIONS == 4 && CG_E_BUFFER_LIMIT == 5 && CG_E_CAPACITY == 6 &&
                    CG_E_NO_DEVICE == 7 && CG_E_TABLES == 8,
@@ -115,6 +115,17 @@ static int nodevice(void) {
                   CG_E_NO_DEVICE &&
               b == NULL,
           "async batch after an event");
+    cg_pipeline *pl = (cg_pipeline *)1;
+    CHECK(cg_pipeline_create(-1, 16, 2, &pl) == CG_E_NO_DEVICE && pl == NULL, "pipeline create");
+    CHECK(cg_pipeline_create(0, 65, 2, &pl) == CG_E_INVALID_OPTIONS, "pipeline group above 64");
+    CHECK(cg_pipeline_submit(NULL, data, boffs, 1, 0, 0, 0, CG_SHA256, out, 64, NULL, &b) == CG_E_IO,
+          "pipeline submit without a pipeline");
+    CHECK(cg_pipeline_flush(NULL) == CG_E_IO, "pipeline flush without a pipeline");
+    double ps[6];
+    CHECK(cg_pipeline_stats(NULL, ps) == CG_E_IO, "pipeline stats without a pipeline");
+    cg_pipeline_destroy(NULL);
+    void *ev = NULL;
+    CHECK(cg_batch_event(NULL, &ev) == CG_E_IO, "batch event without a batch");
     cg_push *p = cg_push_new(0, 0, 0, CG_SHA256, &st);
     if (p) {
         CHECK(cg_push_push(p, data, sizeof data, out, 64, &n) == CG_E_NO_DEVICE, "push");

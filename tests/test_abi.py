@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol(ca):
     assert set(syms) == set(_lib.EXPORTS)
     for s in _lib.TEST_HOOKS:
         assert hasattr(ca.lib, s), f"missing test hook {s}"
-    assert ca.lib.cg_abi_version() == _lib.ABI_VERSION == 2
+    assert ca.lib.cg_abi_version() == _lib.ABI_VERSION == 3
 
 
 def test_product_library_has_no_diagnostic_kernels(ca):

@@ -90,29 +90,21 @@ def test_bench_cli_contract():
         assert flag in r.stdout, flag
 
 
-def test_bench_default_depth(monkeypatch):
-    """bench.py's batches in flight: 20 for sub-4-GiB SHA-256 batches (latency-bound
-    digest), 4 from 4 GiB, 2 for BLAKE3, and never more than the hardware queues allow
-    (each batch in flight holds a stream of its own)."""
-    import sys
-    from pathlib import Path
-
-    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
-    import bench
-
-    G = bench.GIB
-    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "22")
-    assert bench.default_depth(1, G) == 20
-    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "32")
-    assert bench.default_depth(1, G) == 20
-    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "16")
-    assert bench.default_depth(1, G) == 14
-    assert bench.default_depth(1, 16 * G) == 4
-    assert bench.default_depth(0, G) == 2
-    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "8")
-    assert bench.default_depth(1, G) == 6
-    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
-    assert bench.default_depth(1, G) == 2 and bench.default_depth(1, 16 * G) == 2
+def test_default_depth_and_group():
+    """Per-batch-stream path (group=0): 20 batches in flight for sub-4-GiB SHA-256 batches,
+    4 from 4 GiB, 2 for BLAKE3, never more than the hardware queues less 2 (each batch in
+    flight holds a stream of its own); the queue count defaults to what the library saw at
+    load (cg_hw_queues), not the environment's current value.  Digest pipeline: 16 GiB of
+    batches per merged SHA-256 launch (1 GiB -> 16, 16 GiB -> 1), BLAKE3 unmerged."""
+    G = 1 << 30
+    dd = chunking.default_depth
+    assert dd(1, G, 22) == 20 and dd(1, G, 32) == 20 and dd(1, G, 16) == 14
+    assert dd(1, 16 * G, 16) == 4 and dd(0, G, 16) == 2 and dd(1, G, 8) == 6
+    assert dd(1, G, 4) == 2 and dd(1, 16 * G, 4) == 2
+    assert dd(1, G) == dd(1, G, ca.lib.cg_hw_queues())
+    dg = chunking.default_group
+    assert dg(1, G) == 16 and dg(1, 4 * G) == 4 and dg(1, 16 * G) == 1 and dg(1, 64 << 20) == 64
+    assert dg(0, G) == 1
 
 
 def test_batch_pipeline_order_depth_and_drain(monkeypatch):
@@ -144,7 +136,7 @@ def test_batch_pipeline_order_depth_and_drain(monkeypatch):
 
     monkeypatch.setattr(chunking, "chunk_batch_device_async", fake_async)
     offs = np.array([0, 1 << 20], np.uint64)
-    with chunking.BatchPipeline(3) as p:
+    with chunking.BatchPipeline(3, group=0) as p:
         got = []
         for k in range(7):
             got += p.submit(1, offs, 2, 3, inputs_ready=9, tag=f"b{k}")
@@ -160,14 +152,61 @@ def test_batch_pipeline_order_depth_and_drain(monkeypatch):
     issued.clear()
     log.clear()
     with pytest.raises(ca.IoError):
-        with chunking.BatchPipeline(2) as p:
+        with chunking.BatchPipeline(2, group=0) as p:
             p.submit(666, offs, 2, 3)
             p.submit(1, offs, 2, 3)  # waits for the failing first batch -> raises
     assert ("wait", 1) in log  # the context exit still waited for the second one
-    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "22")
-    p = chunking.BatchPipeline()
+    monkeypatch.setattr(chunking.lib, "cg_hw_queues", lambda: 22)
+    p = chunking.BatchPipeline(group=0)
     p.submit(1, offs, 2, 3)
     assert p.depth == 20
     p.drain()
     with pytest.raises(ca.InvalidOptionsError):
         chunking.BatchPipeline(0)
+    with pytest.raises(ca.InvalidOptionsError):
+        chunking.BatchPipeline(group=65)
+
+
+def test_batch_pipeline_digest_pipeline_host_logic(monkeypatch):
+    """BatchPipeline over the digest pipeline (cg_pipeline_*) with the engine calls
+    replaced: one pipeline created at the first submit with default_group / the lanes,
+    depth (lanes + 1) x group by default, every batch submitted to it in order with its
+    inputs-ready event, results in submission order, drain() flushes the open group before
+    waiting, and leaving the context destroys the pipeline after every wait."""
+    import numpy as np
+
+    log = []
+
+    class FakeBatch:
+        def __init__(self, k):
+            self.k = k
+
+        def wait(self):
+            log.append(("wait", self.k))
+            return np.array([0, self.k], np.uint64)
+
+    monkeypatch.setattr(chunking, "pipeline_create", lambda dev, g, l: log.append(("create", dev, g, l)) or 77)
+    monkeypatch.setattr(chunking, "pipeline_flush", lambda p: log.append(("flush", p)))
+    monkeypatch.setattr(chunking, "pipeline_destroy", lambda p: log.append(("destroy", p)))
+    sub = []
+
+    def fake_submit(p, d, offs, o, cap, opts, hash, ready=0):
+        assert p == 77
+        sub.append((d, ready))
+        log.append(("submit", len(sub) - 1))
+        return FakeBatch(len(sub) - 1)
+
+    monkeypatch.setattr(chunking, "pipeline_submit", fake_submit)
+    offs = np.array([0, 1 << 30], np.uint64)  # 1 GiB batches: default group 16
+    with chunking.BatchPipeline(lanes=2) as p:
+        got = []
+        for k in range(50):
+            got += p.submit(k, offs, 2, 3, inputs_ready=9, tag=k)
+        assert p.group == 16 and p.depth == 48 and len(p) == 47
+        got += p.drain()
+    assert log[0] == ("create", -1, 16, 2)
+    assert [t for t, _ in got] == list(range(50))
+    assert all(r == 9 for _, r in sub) and [d for d, _ in sub] == list(range(50))
+    assert log.index(("flush", 77)) < log.index(("wait", 3))  # drain flushes first
+    assert log[-1] == ("destroy", 77)
+    assert log.index(("wait", 0)) > log.index(("submit", 47))
