@@ -82,16 +82,25 @@ def parse_args():
     ap.add_argument("--drop-in-only", action="store_true", help="only the drop-in leg (profiling)")
     ap.add_argument("--drop-in-sizes", default="10,64,256,1024",
                     help="MiB per call of the drop-in leg's one-caller size sweep ('' = skip)")
-    ap.add_argument("--hw-queues", type=int, default=-1, choices=range(-1, 33), metavar="-1..32",
-                    help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's; -1: 22 for one "
-                         "rank, 28 for the ranks of an N > 1 run, whose RCCL communicator takes queues too)")
+    ap.add_argument("--hw-queues", type=int, default=0, choices=range(0, 33), metavar="0..32",
+                    help="GPU_MAX_HW_QUEUES for this process (0: leave the environment's, HIP's default 4: the "
+                         "digest pipeline needs no more)")
+    ap.add_argument("--group", type=int, default=-1, choices=range(-1, 65), metavar="-1..64",
+                    help="batches per merged SHA-256 digest launch of the digest pipeline (cg_pipeline_*; -1: "
+                         "chunker_amd.default_group; 0: the round-5 per-batch-stream path, "
+                         "cg_chunk_batch_device_async_after)")
+    ap.add_argument("--lanes", type=int, default=0, choices=range(0, 9), metavar="0..8",
+                    help="merged digests in flight (cg_pipeline_create lanes; 0: chunker_amd.PIPE_LANES)")
+    ap.add_argument("--no-stage-profile", action="store_true",
+                    help="skip the per-stage single steps (so a kernel trace holds only the pipeline's launches)")
     ap.add_argument("--no-clock", action="store_true", help="skip the digest clock measurement (scripts/sha_clock.py)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="queue each batch after everything on the stream (cg_chunk_batch_device_async): its "
                          "boundary stages wait for the previous batch's digest (A/B of the overlap)")
-    ap.add_argument("--depth", type=int, default=0, choices=range(0, 33), metavar="0..32",
-                    help="batches in flight from the one caller (each its own output array and workspace); "
-                         "1 = each batch waited for before the next is queued; 0 = auto (default_depth)")
+    ap.add_argument("--depth", type=int, default=0, choices=range(0, 257), metavar="0..256",
+                    help="batches in flight from the one caller (each its own input batch, output array and "
+                         "workspace); 1 = each batch waited for before the next is queued; 0 = auto: (lanes + 1) x "
+                         "group for the digest pipeline, default_depth for --group 0")
     ap.add_argument("--split-mode", type=int, default=2, choices=(1, 2),
                     help="overlapped batches: 1 = boundary stages on the library stream, digests in stream order; "
                          "2 = the whole batch on the library stream (digests of consecutive batches overlap too)")
@@ -129,6 +138,13 @@ def default_depth(algo: int, batch_bytes: int) -> int:
     return rule(algo, batch_bytes)
 
 
+def timed_group(lib_default: int, steps: int) -> int:
+    """The divisor of `steps` nearest the library's default group (ties: the larger), so the
+    timed steps are whole merged groups: 20 steps -> 20 (library default 24)."""
+    divs = [g for g in range(1, min(steps, 64) + 1) if steps % g == 0] or [1]
+    return min(divs, key=lambda g: (abs(g - lib_default), -g))
+
+
 def launch_ranks(n: int) -> int:
     """Start n ranks as one child torchrun process (127.0.0.1 rendezvous) and return
     its exit code.  Nothing here initialises HIP: the GPUs belong to the children."""
@@ -147,21 +163,9 @@ def main():
     # The installed GEAR table is the labelled placeholder (tables/README.md) and the
     # engine refuses to chunk with it unless opted in; the JSON says which table ran.
     os.environ.setdefault("CHUNKER_AMD_ALLOW_PLACEHOLDER_GEAR", "1")
-    # HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default) and streams
-    # sharing one serialise, so batches in flight and concurrent callers need more: the
-    # deployment setting DESIGN.md §7 / INTEGRATION.md recommend, 22 -- twenty batches in
-    # flight plus the caller's streams; at 24 and more the queues are time-sliced and every
-    # leg of this bench slowed (profiles/r05_v57_v58_q22.txt, r05_v53_q32_depth.txt).  Set
-    # before anything initialises HIP; --hw-queues 0 keeps the environment's value.
-    if args.hw_queues < 0:
-        # 22: twenty batches in flight plus the caller's streams, the most the GPU schedules
-        # without time-slicing its queues (24+ slowed every leg).  An N > 1 rank's RCCL
-        # communicator holds queues too: at 22 its twenty batches ran as two rounds (168-170
-        # GiB/s, per-gather or not); at 26-32 one round with chains ~22 % slower (225-228)
-        # (profiles/r05_v61_v65_rccl_queues.txt).
-        # (The gloo rehearsal puts several ranks on one GPU: 8 queues each.)
-        multi_rank = int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.dist_force
-        args.hw_queues = (8 if args.dist_backend == "gloo" else 28) if multi_rank else 22
+    # The digest pipeline holds 1 + lanes streams however many batches are in flight, so
+    # HIP's default 4 hardware queues suffice (round 5's per-batch streams needed 22).
+    # --hw-queues N sets GPU_MAX_HW_QUEUES before anything initialises HIP (A/B only).
     if args.hw_queues:
         os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
 
@@ -205,39 +209,57 @@ def main():
         return
     mine = shard_nars(n_per * world, world, rank)
     sizes = np.full(len(mine), nar_bytes, np.uint64)
-    d_data, offs = synth_nars_device(sizes, zeros=args.zeros, first_index=mine.start)
+    batch_bytes = int(sizes.sum())
+    # The product pipeline (chunker_amd.BatchPipeline): the digest pipeline with `group`
+    # batches per merged SHA-256 launch and `lanes` merged launches in flight, depth (lanes +
+    # 1) x group batches queued from this one caller (every lane busy while the next group
+    # forms); --group 0 = the round-5 per-batch-stream path.
+    # (the timed region must span whole groups: steps complete in bursts as each group's
+    # members finish, so the default group is the divisor of --steps nearest the library's
+    # default -- 20 for the driver's 20 steps)
+    group = args.group if args.group >= 0 else timed_group(ca.chunking.default_group(algo, batch_bytes), args.steps)
+    lanes = args.lanes or ca.chunking.PIPE_LANES
+    depth = args.depth or ((lanes + 1) * group if group else default_depth(algo, batch_bytes))
+    # Distinct inputs: every in-flight slot owns its own batch of NARs (global NAR indices
+    # slot * n_per * world + this rank's shard, the reference's per-NAR seeds,
+    # crates/node/src/lib.rs:191-203) and output array.  Slot k % depth is reused by step k
+    # only after step k - depth was returned (BatchPipeline keeps at most `depth` queued).
+    t_syn = time.perf_counter()
+    d_ins, offs = [], None
+    for slot in range(depth):
+        d, offs = synth_nars_device(sizes, zeros=args.zeros, first_index=slot * n_per * world + mine.start)
+        d_ins.append(d)
+    torch.cuda.synchronize()
+    synth_s = time.perf_counter() - t_syn
     total_bytes = int(offs[-1])
     cap = ca.chunking.batch_capacity(offs, params[0])
     # RCCL gather: fixed per-rank sizes agreed once here, so a step's gather needs no count
     # exchange and no host sync (chunker_amd.dist.gather_batch_async)
     gcap, gnars = gather_shape(cap, len(mine)) if multi and nccl else (cap, len(mine))
-    # `depth` output arrays, used in turn: while step k's descriptors are gathered, steps
-    # k + 1 .. k + depth - 1 write the others
-    depth = args.depth or default_depth(algo, int(offs[-1]))
     d_outs = [torch.empty(gcap * 48, dtype=torch.uint8, device="cuda") for _ in range(depth)]
-    # The batches run on a stream of their own.  The gather of step k is queued on torch's
-    # current stream (RCCL's stream waits for that one), which holds none of the batches, so
-    # it runs while step k + 1's kernels do instead of queueing behind them; an event after
-    # it holds back step k + depth, the next writer of the same output array.
+    # The gather of step k is queued on torch's current stream (RCCL's stream waits for that
+    # one) once step k is back on the host; an event after it is the inputs-ready event of
+    # step k + depth, the next writer of the same output array, so the pipeline's boundary
+    # stream waits for the gather and nothing else.
     bstream = torch.cuda.Stream()
     sptr = bstream.cuda_stream
     gathered_ev = [None] * depth
     gathered = [None]
-    # Inputs-ready events (cg_chunk_batch_device_async_after): a batch's boundary stages
-    # (scan, walk, assembly) wait only for its input and output array to be free -- the NARs
-    # were written once, before the timed region; an output array is free once its previous
-    # gather has run -- so they run under the previous batch's digest on bstream, and only
-    # the digests follow one another there.  --no-overlap: after everything on bstream.
     synth_ev = torch.cuda.Event()
     synth_ev.record()
 
     def ready_event(k):  # the inputs-ready event of step k (its output array free again)
         ev = gathered_ev[k % depth]
-        if ev is not None:
-            bstream.wait_event(ev)  # (the digest writes the output array's hashes)
-        return 0 if args.no_overlap else (ev or synth_ev).cuda_event
+        if args.no_overlap:
+            if ev is not None:
+                bstream.wait_event(ev)
+            return 0
+        return (ev or synth_ev).cuda_event
+
+    slot_first = {}
 
     def after_wait(k, first):
+        slot_first[k % depth] = first
         if multi and nccl:  # descriptors + NAR index to rank 0 over RCCL (the path's only exchange)
             gathered[0] = gather_batch_async(d_outs[k % depth], first, gcap, gnars)
             ev = torch.cuda.Event()
@@ -247,50 +269,57 @@ def main():
             gathered[0] = gather_batch(d_outs[k % depth][: int(first[-1]) * 48].cpu(), first)
         return first
 
-    def run(n, on_done=None, d=None, k0=0):
-        """Steps k0 .. k0 + n - 1 through the product's own pipeline (chunker_amd.BatchPipeline
-        over cg_chunk_batch_device_async_after + cg_batch_wait): up to `d` queued, step
-        k + d - 1 queued before step k is waited for, so the host side of each call --
-        validation, staging, launches, the wait -- overlaps the GPU's work instead of
-        idling it between batches (~65 us per step, 8 % of a config-3 step)."""
-        pipe = ca.BatchPipeline(d or depth, *params, hash=algo, stream=sptr)
-        t_issue = {}
-        last_first = [None]
+    pipe = ca.BatchPipeline(depth, *params, hash=algo, stream=sptr, group=group, lanes=lanes)
+    t_issue = {}
+    last = {"k": None, "first": None}
+    nxt = [0]  # next step index
 
-        def finished(done):
-            for k, first in done:
-                last_first[0] = after_wait(k, first)
-                if on_done:
-                    on_done(k - k0, time.perf_counter() - t_issue.pop(k))
+    def submit_next(on_done=None):
+        k = nxt[0]
+        nxt[0] += 1
+        ready = ready_event(k)
+        t_issue[k] = time.perf_counter()
+        got = pipe.submit(d_ins[k % depth].data_ptr(), offs, d_outs[k % depth].data_ptr(), gcap,
+                          inputs_ready=ready, tag=k)
+        for kk, first in got:
+            last["k"], last["first"] = kk, after_wait(kk, first)
+            if on_done:
+                on_done(kk, time.perf_counter() - t_issue[kk])
+        return len(got)
 
-        for k in range(k0, k0 + n):
-            ready = ready_event(k)
-            t_issue[k] = time.perf_counter()
-            finished(pipe.submit(d_data.data_ptr(), offs, d_outs[k % depth].data_ptr(), gcap, inputs_ready=ready,
-                                 tag=k))
-        finished(pipe.drain())
-        return last_first[0]
+    def drain(on_done=None):
+        for kk, first in pipe.drain():
+            last["k"], last["first"] = kk, after_wait(kk, first)
+            if on_done:
+                on_done(kk, time.perf_counter() - t_issue[kk])
 
-    def step(k=0):  # one batch, waited for
-        return run(1, d=1, k0=k)
+    # warm-up: max(W, depth) + 1 steps rounded up to whole groups, so every workspace the
+    # pool hands out and every lane buffer is sized before the timed region
+    n_warm = max(args.warmup, depth) + 1
+    if group:
+        n_warm = -(-n_warm // group) * group
+    for _ in range(n_warm):
+        submit_next()
+    drain()
 
-    # warm-up in the timed loop's pattern (depth batches queued, so every workspace the pool
-    # hands out is sized before the timed region)
-    run(max(args.warmup, depth) + 1)
-    # Digest-stage device time: the two HIP events the library records around the digest
-    # on the stream the kernels run on (cg_set_profiling(2)), live inside the timed region
-    # (each step already ends in a stream sync for the NAR->chunk index, so reading them
-    # adds only host bookkeeping).  A timing event between two kernels holds the second
-    # back by ~6 us, so the other stages are timed on PROFILE_STEPS untimed steps before
-    # the timed region (cg_set_profiling(1), every stage boundary an event).
-    def profile_stages(k_out):
-        """Every stage timed (cg_set_profiling(1)) on PROFILE_STEPS single steps, then the
-        scan stage right after a 2 GiB write (the 256 MB MALL holds none of the batch): the
-        cold-HBM rate, reported beside the warm one (the previous digest just read the batch)."""
+    # Stage profile (every stage boundary a HIP event, cg_set_profiling(1)) on PROFILE_STEPS
+    # single batches through the per-batch path (its digest is one batch's launch), then the
+    # scan stage right after a 2 GiB write (the 256 MB MALL holds none of the batch): the
+    # cold-HBM rate beside the warm one.  A timing event between two kernels holds the second
+    # back by ~6 us, so the timed region records only the pipeline's events around each
+    # merged digest (cg_set_profiling(2)).
+    buf = (np.ctypeslib.ctypes.c_double * 5)()
+
+    def single(k_slot):
+        with ca.BatchPipeline(1, *params, hash=algo, stream=sptr, group=0) as one:
+            one.submit(d_ins[k_slot].data_ptr(), offs, d_outs[k_slot].data_ptr(), gcap)
+            one.drain()
+
+    def profile_stages():
         ca.lib.cg_set_profiling(1)
         prof = np.zeros((PROFILE_STEPS, 5))
         for k in range(PROFILE_STEPS):
-            step(k_out)
+            single(k % depth)
             ca.lib.cg_last_stage_times(buf, 5)
             prof[k] = list(buf)
         cold = np.zeros(PROFILE_STEPS)
@@ -298,53 +327,115 @@ def main():
         for k in range(PROFILE_STEPS):
             scratch.fill_(k)
             torch.cuda.synchronize()
-            step(k_out)
+            single(k % depth)
             ca.lib.cg_last_stage_times(buf, 5)
             cold[k] = buf[0]
         del scratch
         ca.lib.cg_set_profiling(0)
         return prof, cold
 
-    # The stage profile runs before the timed region (after the warm-up): run after a deep
-    # pipelined region every stage's events read 20-200 % longer (scan 0.239-0.253 vs
-    # 0.198 ms, compact 0.057 vs 0.017; profiles/r05_v33_profile_order.txt) -- the events'
-    # timestamps, not the kernels: the same single steps before it match one batch at a time.
-    buf = (np.ctypeslib.ctypes.c_double * 5)()
-    if not args.profile_after:
-        pre_prof = profile_stages(0)
+    floor = None
+    if args.no_stage_profile:
+        prof, cold = np.full((1, 5), np.nan), np.full(1, np.nan)
+    else:
+        prof, cold = profile_stages()
+        if algo == 1:  # the single batch's digest against its longest chunk's chain (its own launch's tiers)
+            k_s = (PROFILE_STEPS - 1) % depth
+            n_s = int(ca.chunking.batch_capacity(offs, params[0]))
+            d_s = d_outs[k_s][: n_s * 48].cpu().numpy().view(ca.DESC_DTYPE)
+            d_s = d_s[d_s["length"] > 0]
+            clk = sha_clock(args) if world == 1 and not args.no_clock else None
+            floor = sha_chain_floor(ca, d_s, float(np.mean(prof[:, 4])), clk)
     ca.lib.cg_set_profiling(2)
-    stage = np.zeros((max(args.steps, 1), 5))
+    st0 = pipe.stats()
     torch.cuda.synchronize()
     if multi:
         dist.barrier()
-    t0 = time.perf_counter()
+    # Fill (untimed): depth - 1 steps queued, the pipeline's groups forming and launching;
+    # then settle (untimed): at least `depth` more steps submitted and completed one for one,
+    # as in every step of a long run, ending at the completion of a whole group.  The timed
+    # region then counts completions in steady state, from one group's
+    # end to another's.
+    t_fill = time.perf_counter()
+    done0 = nxt[0]  # steps completed so far (the warm-up drained)
+    while nxt[0] - done0 < depth - 1:
+        submit_next()
+    fill_ms = (time.perf_counter() - t_fill) * 1e3
+    t_settle = time.perf_counter()
+    settled = [0]
 
-    latency = np.zeros(max(args.steps, 1))
+    def count(kk, waited):
+        settled[0] += 1
 
-    def record(k, waited):
-        ca.lib.cg_last_stage_times(buf, 5)
-        stage[k] = list(buf)
-        latency[k] = waited
-
-    first = run(args.steps, record)
-    last = (args.steps - 1) % depth
-    torch.cuda.synchronize()  # every stream: the batches' and the last gather
+    while settled[0] < depth or (group and (last["k"] + 1) % group):
+        submit_next(count)
+    settle_ms = (time.perf_counter() - t_settle) * 1e3
+    # t0: the caller's own streams are idle (torch's current stream and the gather's), the
+    # ranks aligned; the pipeline holds depth - 1 batches in flight, as it does at every
+    # step of a long run
+    torch.cuda.current_stream().synchronize()
+    bstream.synchronize()
     if multi:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    prof, cold = profile_stages(last) if args.profile_after else pre_prof
+    t0 = time.perf_counter()
+    latency = []
+    done = [0]
+
+    def record(kk, waited):
+        done[0] += 1
+        latency.append(waited)
+
+    while done[0] < args.steps:  # EXACTLY `steps` batches completed inside the timed region
+        submit_next(record)
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    done_timed = done[0]
+    # A longer steady window right after (untimed for `value`): 3 x lanes whole groups, so
+    # the lanes' phase (a single group-to-group window of `steps` steps reads +-10 %) averages
+    # out; reported beside `value`.
+    n_long = 3 * lanes * group if group else 0
+    long_rate = None
+    if n_long:
+        done_l = [0]
+
+        def count_l(kk, waited):
+            done_l[0] += 1
+
+        tl = time.perf_counter()
+        while done_l[0] < n_long:
+            submit_next(count_l)
+        long_rate = done_l[0] * total_bytes * world / (time.perf_counter() - tl) / GIB
+    if multi:
+        dist.barrier()
+    # drain (untimed): the depth - 1 batches still in flight
+    t_dr = time.perf_counter()
+    drain()
+    torch.cuda.synchronize()  # every stream: the batches' and the last gather
+    drain_ms = (time.perf_counter() - t_dr) * 1e3
+    st1 = pipe.stats()
+    pipe.close()
+    ca.lib.cg_set_profiling(0)
     if multi:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if nccl else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    first = last["first"]
+    k_last = last["k"] % depth
     n_chunks = int(first[-1])
-    stages_ms = dict(zip(["scan", "compact", "walk", "assemble", "digest"], prof.mean(axis=0).round(4)))
-    stages_ms["digest_timed"] = round(float(stage[: max(args.steps, 1), 4].mean()), 4)
+    stages_ms = dict(zip(["scan", "compact", "walk", "assemble", "digest"], np.nanmean(prof, axis=0).round(4)))
+    # merged digest launches timed by the pipeline's events (cg_set_profiling(2)): the timed
+    # region's groups and the drain's
+    g_n = st1.get("timed_groups", 0) - st0.get("timed_groups", 0)
+    g_ms = st1.get("digest_ms_sum", 0.0) - st0.get("digest_ms_sum", 0.0)
+    g_bytes = st1.get("digest_bytes_sum", 0.0) - st0.get("digest_bytes_sum", 0.0)
+    launch_ms = g_ms / g_n if g_n else float("nan")
+    launch_bytes = g_bytes / g_n if g_n else float("nan")
+    stages_ms["digest_launch"] = round(launch_ms, 4)
 
     # parity spot check on the last step: descriptors cover every NAR exactly -- this
     # rank's own batch, and at N > 1 the whole batch as gathered on rank 0 (global NAR
     # order, every NAR of every rank tiled contiguously)
-    descs = d_outs[last][: n_chunks * 48].cpu().numpy().view(ca.DESC_DTYPE)
+    descs = d_outs[k_last][: n_chunks * 48].cpu().numpy().view(ca.DESC_DTYPE)
     check_gathered_batch(descs, first, sizes)
     gather_check = None
     if multi and rank == 0:
@@ -357,20 +448,34 @@ def main():
         assert gather_check["rank0_prefix_equal"], "rank 0's own descriptors differ inside the gathered batch"
 
     total_all = total_bytes * world
-    value = total_all * args.steps / elapsed / GIB
-    dig_ms = stages_ms["digest_timed"]
+    value = total_all * done_timed / elapsed / GIB
     scan_ms = stages_ms["scan"]
+    if group and algo == 1 and g_n:
+        # dominant kernel = the merged digest: algorithmic bytes per launch = every NAR byte of
+        # its `group` batches once; duration = the pipeline's HIP events around k_sha256 on
+        # the lane stream it ran on
+        ach = launch_bytes / (launch_ms * 1e-3) / 1e9
+        kname, knote = "k_sha256", (f"merged digest launch of the digest pipeline ({group} batches per launch, {lanes} "
+                                    "lanes): algorithmic bytes = every NAR byte of the launch's batches once, / the "
+                                    "mean launch duration (HIP events on the lane stream around k_sha256, the timed "
+                                    f"region's and the drain's {g_n} launches)")
+    else:
+        dig_ms = stages_ms["digest"]
+        ach = total_bytes / (dig_ms * 1e-3) / 1e9
+        kname = "k_sha256" if algo == 1 else "k_b3_leaves+k_b3_fold+k_b3_top"
+        knote = (f"digest stage of one batch (HIP events around the digest, {PROFILE_STEPS} untimed single steps): "
+                 "algorithmic bytes = every NAR byte once")
     roofline = {
-        "kernel": "k_sha256" if algo == 1 else "k_b3_leaves+k_b3_fold+k_b3_top",
+        "kernel": kname,
         "bound": "hbm",
-        "achieved": round(total_bytes / (dig_ms * 1e-3) / 1e9, 2),
+        "achieved": round(ach, 2),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
-        "frac": round(total_bytes / (dig_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+        "frac": round(ach / HBM_PEAK_GBS, 5),
         "traffic": None,
-        "note": "digest stage: algorithmic bytes = every NAR byte once, / mean digest-stage duration over the "
-                "timed steps (HIP events around the digest only); scan stage (scan_kernel) from "
-                f"{PROFILE_STEPS} untimed single steps with every stage timed, before the timed region",
+        "note": knote,
+        "launch": {"bytes": round(launch_bytes) if g_n else None, "ms": round(launch_ms, 3) if g_n else None,
+                   "launches_timed": g_n},
         "scan_kernel": {"kernel": scan_kernel_name(ca, params[1], total_bytes),
                         "achieved": round(total_bytes / (scan_ms * 1e-3) / 1e9, 2),
                         "frac": round(total_bytes / (scan_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -382,17 +487,12 @@ def main():
                                              f"(median of {PROFILE_STEPS}); the warm figure above follows the "
                                              "previous step's digest, which just read the batch"}},
     }
-    # With batches overlapped (cg_chunk_batch_device_async_after, two in flight) the digest
-    # launches of consecutive steps run side by side: per launch the fraction above is
-    # unchanged, and the whole job's digest throughput is every step's bytes / the timed
-    # wall time (= `value` in GB/s).
-    roofline["aggregate"] = {"achieved": round(total_bytes * args.steps / elapsed / 1e9, 2),
-                             "frac": round(total_bytes * args.steps / elapsed / 1e9 / HBM_PEAK_GBS, 5),
-                             "launches_in_flight": 1 if args.no_overlap or algo != 1 else depth,
+    roofline["aggregate"] = {"achieved": round(total_bytes * done_timed / elapsed / 1e9, 2),
+                             "frac": round(total_bytes * done_timed / elapsed / 1e9 / HBM_PEAK_GBS, 5),
+                             "batches_in_flight": depth,
                              "note": "this rank's algorithmic bytes of all timed steps / the timed wall time"}
-    if algo == 1:
-        clk = sha_clock(args) if world == 1 and not args.no_clock else None
-        roofline["latency_floor"] = sha_chain_floor(ca, descs, dig_ms, clk)
+    if floor is not None:
+        roofline["latency_floor"] = floor
     # (the batch path assembles the leaf map, so its leaf kernel is k_b3_leaves; k_b3_groups
     # is the three-kernel form's, counted when a summary holds it instead)
     dig_kernels = ["k_sha256"] if algo == 1 else ["k_b3_leaves", "k_b3_groups", "k_b3_fold", "k_b3_top"]
@@ -402,23 +502,27 @@ def main():
         roofline["scan_kernel"]["traffic"] = pmc_traffic(args.config, [roofline["scan_kernel"]["kernel"]])[0]
         roofline["traffic_source"] = src
 
+    # slot 0's batch (global NARs 0 .. n_per - 1 at rank 0): the e2e leg's host batch
+    n0 = int(slot_first[0][-1])
+    descs0 = d_outs[0][: n0 * 48].cpu().numpy().view(ca.DESC_DTYPE)
     cpu = None
     conc = None
     drop = None
+    del d_ins, d_outs
+    torch.cuda.empty_cache()
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, n_per, nar_bytes, params, algo)
-    if world == 1 and args.drop_in:  # (before the concurrent leg: its 32 streams share the hardware queues)
+    if world == 1 and args.drop_in:
         drop = drop_in_rates(ca, args)
     if world == 1 and not args.no_concurrent:
-        del d_outs, d_data
-        torch.cuda.empty_cache()
         conc = concurrent_rates(ca, torch, args, n_per, nar_bytes, params, algo)
         if args.e2e:
-            conc["e2e"] = e2e_rates(ca, torch, args, n_per, nar_bytes, params, algo, descs)
+            conc["e2e"] = e2e_rates(ca, torch, args, n_per, nar_bytes, params, algo, descs0)
 
     if rank == 0:
         gear = "placeholder" if ca.lib.cg_gear_is_placeholder() else (
             "fastcdc-4.0.1 (selftest passed)" if ca.tables_verified() else "installed, unverified")
+        lat = np.array(latency) * 1e3
         line = {
             "metric": "device-resident GiB/s FastCDC+SHA-256 over synthetic NARs, 1/2/4/8 MI355X"
             if algo == 1 else "device-resident GiB/s FastCDC+BLAKE3 over synthetic NARs",
@@ -426,20 +530,33 @@ def main():
             "unit": "GiB/s",
             "n_gpus": world,
             "steps": args.steps,
-            "steps_queued": depth,
-            "overlap": "none" if args.no_overlap or depth == 1 else (
-                "none (BLAKE3 batches stay in stream order)" if algo == 0 else
-                "boundary stages" if args.split_mode == 1 else f"whole batch: {depth} batches in flight"),
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            # what one batch waits, queued -> results on the host, with `depth` in flight
-            "batch_latency_ms": {"p50": round(float(np.percentile(latency[: args.steps], 50)) * 1e3, 3),
-                                 "p99": round(float(np.percentile(latency[: args.steps], 99)) * 1e3, 3)},
+            "ms_per_step": round(elapsed / done_timed * 1e3, 3),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (xorshift64 NAR payloads)" if not args.zeros else "synthetic (all-zero NAR payloads)",
+            "data": ("synthetic (xorshift64 NAR payloads)" if not args.zeros else "synthetic (all-zero NAR payloads)"),
+            "inputs": f"distinct: {depth} input batches resident in HBM, one per batch in flight",
+            "timed": (f"steady: before t0 the pipeline was filled ({depth - 1} batches in flight) and settled "
+                      f"({settled[0]} steps, each one submitted and one completed, ending at a group's end); exactly "
+                      f"{done_timed} batches completed between t0 and t1 ({done_timed // max(group, 1)} whole groups of "
+                      f"{group}; t0 after a barrier with the caller's streams idle, t1 at the last completion returned "
+                      "to the host); fill, settle and drain untimed, reported"),
+            "pipeline": {"kind": "digest pipeline (cg_pipeline_*)" if group else
+                         "per-batch streams (cg_chunk_batch_device_async_after)",
+                         "group": group, "lanes": lanes if group else None, "depth": depth,
+                         "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "4 (HIP default)"),
+                         "fill_ms": round(fill_ms, 2), "settle_steps": settled[0], "settle_ms": round(settle_ms, 2),
+                         "settle_GiBps": round(settled[0] * total_bytes * world / (settle_ms * 1e-3) / GIB, 3),
+                         "drain_ms": round(drain_ms, 2),
+                         "steady_window": {"steps": n_long, "GiBps": round(long_rate, 3) if long_rate else None,
+                                           "note": "the steps right after the timed ones, group end to group end "
+                                                   "(this rank; not part of `value`)"},
+                         "synth_s": round(synth_s, 1)},
+            "batch_latency_ms": {"p50": round(float(np.percentile(lat, 50)), 3),
+                                 "p99": round(float(np.percentile(lat, 99)), 3),
+                                 "note": "submit -> results on the host, per batch, timed region"},
             "config": {"workload": desc, "nars_per_gpu": len(mine), "nar_bytes": nar_bytes,
                        "params": list(params), "parallelism": f"nar-shard x{world}",
                        **({"dist_backend": args.dist_backend} if multi else {})},
@@ -619,60 +736,53 @@ def e2e_rates(ca, torch, args, n_per, nar_bytes, params, algo, want):
                 f"e2e batch {k}: descriptors differ from the device-resident run"
         res[f"K{K}"] = round(K * reps * nbytes / dt / GIB, 3)
     if algo == 1:
-        res["one_caller_overlapped"] = e2e_one_caller(ca, torch, bufs, offs, nbytes, cap, n_per, params, algo, want,
-                                                      args.depth or default_depth(algo, nbytes))
+        res["one_caller_overlapped"] = e2e_one_caller(ca, torch, bufs, offs, nbytes, cap, params, algo, want, args)
     return res
 
 
-def e2e_one_caller(ca, torch, bufs, offs, nbytes, cap, n_per, params, algo, want, depth=2):
-    """Host to host from ONE caller thread with `depth` batches in flight (bench.py's
-    default_depth for the config): batch k's pinned H2D copy runs on a copy stream, its
-    inputs-ready event orders the batch (cg_chunk_batch_device_async_after), so the copy and
-    the batch overlap the batches before it; the descriptors come back D2H after its wait.
-    `depth` device input and output buffers are used in turn; batch k + depth is issued only
-    after batch k was waited for and its descriptors copied out.  GiB/s = reps x batch
-    bytes / wall time, reps = max(8, 2 x depth)."""
+def e2e_one_caller(ca, torch, bufs, offs, nbytes, cap, params, algo, want, args):
+    """Host to host from ONE caller thread through the product pipeline
+    (chunker_amd.BatchPipeline, the digest pipeline at its default group / lanes): batch k's
+    pinned H2D copy runs on a copy stream and its event is the batch's inputs-ready event,
+    so the copies overlap the batches before them; the descriptors come back D2H after each
+    batch is returned.  `depth` device input and output buffers are used in turn.  GiB/s =
+    reps x batch bytes / wall time, fill and drain included, reps = 3 x depth."""
     host = bufs[0][0]
-    reps = max(8, 2 * depth)
+    group = args.group if args.group >= 0 else ca.chunking.default_group(algo, nbytes)
+    lanes = args.lanes or ca.chunking.PIPE_LANES
+    depth = args.depth or ((lanes + 1) * group if group else default_depth(algo, nbytes))
+    reps = 3 * depth
     dins = [torch.empty(nbytes + 256, dtype=torch.uint8, device="cuda") for _ in range(depth)]
     douts = [torch.empty(cap * 48, dtype=torch.uint8, device="cuda") for _ in range(depth)]
-    outs = [np.zeros(cap * 48, np.uint8) for _ in range(depth)]
+    out = np.zeros(cap * 48, np.uint8)
     copy = torch.cuda.Stream()
-    bstream = torch.cuda.Stream()
-
-    def issue(k):
-        j = k % depth
-        with torch.cuda.stream(copy):
-            dins[j][:nbytes].copy_(host, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
-        return ca.chunk_batch_device_async(dins[j].data_ptr(), offs, douts[j].data_ptr(), cap, *params, hash=algo,
-                                           stream=bstream.cuda_stream, inputs_ready=ev.cuda_event), ev
-
-    def complete(k, h):
-        first = h[0].wait()
-        n = int(first[-1])
-        j = k % depth
-        outs[j][: n * 48] = douts[j][: n * 48].cpu().numpy()
-        return n
-
+    n = 0
     for timed in (False, True):
         count = reps if timed else depth
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        q = deque()
-        for k in range(count + depth - 1):
-            if k < count:
-                q.append((k, issue(k)))
-            if len(q) == depth or (k >= count and q):
-                kk, h = q.popleft()
-                n = complete(kk, h)
+        with ca.BatchPipeline(depth, *params, hash=algo, group=group, lanes=lanes) as pipe:
+            def take(done):
+                nonlocal n
+                for k, first in done:
+                    n = int(first[-1])
+                    out[: n * 48] = douts[k % depth][: n * 48].cpu().numpy()
+
+            for k in range(count):
+                j = k % depth
+                with torch.cuda.stream(copy):
+                    dins[j][:nbytes].copy_(host, non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record()
+                take(pipe.submit(dins[j].data_ptr(), offs, douts[j].data_ptr(), cap, inputs_ready=ev.cuda_event,
+                                 tag=k))
+            take(pipe.drain())
         dt = time.perf_counter() - t0
-    assert n == len(want) and np.array_equal(outs[(count - 1) % depth][: n * 48], want.view(np.uint8)), \
+    assert n == len(want) and np.array_equal(out[: n * 48], want.view(np.uint8)), \
         "e2e one caller: descriptors differ from the device-resident run"
-    return {"GiBps": round(reps * nbytes / dt / GIB, 3), "reps": reps, "depth": depth,
-            "shape": f"one thread, {depth} batches in flight: pinned H2D on a copy stream -> inputs-ready event -> "
-                     "cg_chunk_batch_device_async_after -> wait -> descriptors D2H"}
+    return {"GiBps": round(reps * nbytes / dt / GIB, 3), "reps": reps, "depth": depth, "group": group,
+            "shape": f"one thread, up to {depth} batches in flight: pinned H2D on a copy stream -> inputs-ready event "
+                     "-> digest pipeline -> wait -> descriptors D2H (fill and drain inside the timed region)"}
 
 
 def drop_in_rates(ca, args):

@@ -49,7 +49,7 @@ EXPORTS = (
     "cg_stream_finish", "cg_stream_take", "cg_stream_pending", "cg_stream_bytes_consumed", "cg_stream_free",
     "cg_last_sha_tiers", "cg_chunk_batch_device_async", "cg_batch_wait", "cg_chunk_batch_device_async_after",
     "cg_pipeline_create", "cg_pipeline_submit", "cg_pipeline_flush", "cg_pipeline_stats", "cg_pipeline_destroy",
-    "cg_batch_event",
+    "cg_batch_event", "cg_multi_create", "cg_multi_submit", "cg_multi_wait", "cg_multi_flush", "cg_multi_destroy",
 )
 # test hooks the product library exports beyond the header (tier caps, spin-guard limit)
 TEST_HOOKS = ("cg_test_sha_quad_max", "cg_test_sha_split_max", "cg_test_sha_spin_limit", "cg_test_cas_pair_max",
@@ -107,6 +107,16 @@ def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
     L.cg_pipeline_destroy.restype = None
     L.cg_batch_event.argtypes = [p, ctypes.POINTER(p)]
     L.cg_batch_event.restype = i
+    L.cg_multi_create.argtypes = [p, sz, u32_, u32_, ctypes.POINTER(p)]
+    L.cg_multi_create.restype = i
+    L.cg_multi_submit.argtypes = [p, p, p, p, u64, u64, u64, i, p, sz, p, ctypes.POINTER(p)]
+    L.cg_multi_submit.restype = i
+    L.cg_multi_wait.argtypes = [p, p]
+    L.cg_multi_wait.restype = i
+    L.cg_multi_flush.argtypes = [p]
+    L.cg_multi_flush.restype = i
+    L.cg_multi_destroy.argtypes = [p]
+    L.cg_multi_destroy.restype = None
     L.cg_push_new.argtypes = [u64, u64, u64, i, ctypes.POINTER(i)]
     L.cg_push_new.restype = p
     L.cg_push_push.argtypes = [p, p, u64, p, sz, psz]

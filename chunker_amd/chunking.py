@@ -435,7 +435,7 @@ def pipeline_destroy(p: int) -> None:
     lib.cg_pipeline_destroy(ctypes.c_void_p(p))
 
 
-PIPE_GROUP_BYTES = 16 << 30  # bytes of batches one merged SHA-256 digest launch takes (default_group)
+PIPE_GROUP_BYTES = 24 << 30  # bytes of batches one merged SHA-256 digest launch takes (default_group)
 PIPE_LANES = 2               # merged digests in flight (cg_pipeline_create lanes)
 
 
@@ -575,6 +575,95 @@ class BatchPipeline:
             self._q.clear()  # (each BatchInFlight waits for itself when collected)
             pipeline_destroy(self._p)
             self._p = None
+
+
+class MultiDevicePipeline:
+    """One host process driving several GPUs (cg_multi_*): each step is a batch of NARs
+    sharded one-file-per-GPU -- shard k already in device k's HBM -- and chunked by device
+    k's digest pipeline; the descriptors are gathered into one array on devices[0] over xGMI
+    peer copies, with the global NAR index on the host (north_star's 8-GPU split for the
+    reference's single node-bin process).  submit()/drain() behave as BatchPipeline's: up to
+    `depth` steps in flight, results (tag, nar_first) in submission order.  A device may be
+    listed more than once (a rehearsal of the split on one GPU)."""
+
+    def __init__(self, devices, min_size=None, avg_size=None, max_size=None,
+                 hash: HashAlgorithm = HashAlgorithm.Sha256, group: int | None = None, lanes: int | None = None,
+                 depth: int | None = None):
+        if depth is not None and depth < 1:
+            raise InvalidOptionsError(f"pipeline depth must be at least 1, got {depth}")
+        self.devices = [int(d) for d in devices]
+        self.options = ChunkingOptions.resolve(min_size, avg_size, max_size)
+        self.hash = HashAlgorithm(hash)
+        self.group, self.lanes, self.depth = group, lanes or PIPE_LANES, depth
+        self._m = None
+        self._q: deque = deque()
+
+    def _open(self, shard_bytes: int) -> None:
+        if self.group is None:
+            self.group = default_group(self.hash, shard_bytes)
+        if self.depth is None:
+            self.depth = (self.lanes + 1) * max(self.group, 1)
+        devs = (ctypes.c_int * len(self.devices))(*self.devices)
+        h = ctypes.c_void_p()
+        _check(lib.cg_multi_create(devs, len(self.devices), max(self.group, 1), self.lanes, ctypes.byref(h)))
+        self._m = h.value
+
+    def submit(self, shards, d_out_ptr: int, out_cap: int, inputs_ready=None, tag=None) -> list:
+        """shards: one (device pointer, nar_offsets starting at 0) per device, in NAR order."""
+        if len(shards) != len(self.devices):
+            raise InvalidOptionsError(f"{len(shards)} shards for {len(self.devices)} devices")
+        offs = [np.ascontiguousarray(o, dtype=np.uint64) for _, o in shards]
+        if self._m is None:
+            self._open(max(int(o[-1]) if len(o) else 0 for o in offs))
+        nd = len(shards)
+        d = (ctypes.c_void_p * nd)(*[ctypes.c_void_p(p) for p, _ in shards])
+        op = (ctypes.c_void_p * nd)(*[ctypes.c_void_p(o.ctypes.data) for o in offs])
+        nn = (ctypes.c_size_t * nd)(*[len(o) - 1 for o in offs])
+        ev = (ctypes.c_void_p * nd)(*[ctypes.c_void_p(e or None) for e in (inputs_ready or [0] * nd)])
+        o = self.options
+        h = ctypes.c_void_p()
+        _check(lib.cg_multi_submit(ctypes.c_void_p(self._m), d, op, nn, o.min_size, o.avg_size, o.max_size,
+                                   int(self.hash), ctypes.c_void_p(d_out_ptr), out_cap, ev, ctypes.byref(h)))
+        self._q.append((tag, h.value, sum(len(x) - 1 for x in offs), offs))
+        done = []
+        while len(self._q) >= self.depth:
+            done.append(self._wait_oldest())
+        return done
+
+    def _wait_oldest(self):
+        t, h, n, _ = self._q.popleft()
+        first = np.zeros(n + 1, np.uint64)
+        _check(lib.cg_multi_wait(ctypes.c_void_p(h), first.ctypes.data))
+        return t, first
+
+    def drain(self) -> list:
+        if self._m is not None:
+            _check(lib.cg_multi_flush(ctypes.c_void_p(self._m)))
+        done = []
+        while self._q:
+            done.append(self._wait_oldest())
+        return done
+
+    def close(self) -> None:
+        try:
+            while self._q:
+                _, h, _, _ = self._q.popleft()
+                lib.cg_multi_wait(ctypes.c_void_p(h), None)
+        finally:
+            if self._m is not None:
+                lib.cg_multi_destroy(ctypes.c_void_p(self._m))
+                self._m = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False
+
+    def __del__(self):
+        if getattr(self, "_m", None) is not None:
+            self.close()
 
 
 def batch_capacity(nar_offsets: np.ndarray, min_size=None) -> int:

@@ -18,10 +18,15 @@
 //     member's host-mapped completion word when its last chunk is stored (ShaNotify), so a
 //     batch completes when ITS longest chunk does, not when the merged launch ends, and a
 //     cg_batch_wait returns as soon as its own digests are in HBM.
-// The pipeline holds 1 + L streams however many batches are in flight.  They are created
-// with a CU mask covering the whole chip (CHUNKER_AMD_PIPE_STREAMS, below): such a stream
-// gets a hardware queue of its own instead of sharing the process's GPU_MAX_HW_QUEUES
-// pool.  BLAKE3 batches (a digest that fills the chip by itself) run whole on the
+// The pipeline holds 1 + L streams however many batches are in flight.  They are
+// non-blocking high-priority streams (CHUNKER_AMD_PIPE_STREAMS, below): HIP keeps a pool
+// of hardware queues per priority, so they do not share a queue with the process's
+// ordinary streams however many of those are busy (scripts/micro/queue_probe.hip,
+// profiles/r06_v4_queue_probe.txt: three such streams ran three 40 ms kernels side by side
+// beside 16 busy ordinary streams at GPU_MAX_HW_QUEUES=4, where three ordinary streams took
+// 5x as long).  A full-CU-mask stream also gets a queue of its own, but HIP creates it as a
+// blocking stream (it then synchronises with the legacy null stream, which torch and other
+// callers use).  BLAKE3 batches (a digest that fills the chip by itself) run whole on the
 // boundary stream, in submission order.
 // Replaces, across a caller's consecutive chunk_descriptors_with_hash calls, the
 // collect-then-hash sequence of src/chunking.rs:334-368.
@@ -86,15 +91,16 @@ struct cg_pipeline {
 
 namespace cgrt {
 
-// Stream kind of the pipeline's streams (CHUNKER_AMD_PIPE_STREAMS, read once):
-// "cumask" (default) = a CU mask over every CU, which HIP backs with a hardware queue of
-// its own; "high" = the high-priority pool; "plain" = ordinary streams (the shared pool).
+// Stream kind of the pipeline's streams (CHUNKER_AMD_PIPE_STREAMS, read once): "high"
+// (default) = non-blocking, high priority (HIP's high-priority queue pool); "cumask" = a CU
+// mask over every CU (a queue of its own, but a blocking stream); "plain" = ordinary
+// non-blocking streams (the shared pool; A/B only).
 static int pipe_stream_kind() {
     static const int k = [] {
         const char *e = getenv("CHUNKER_AMD_PIPE_STREAMS");
         if (e && !strcmp(e, "plain")) return 0;
-        if (e && !strcmp(e, "high")) return 1;
-        return 2;
+        if (e && !strcmp(e, "cumask")) return 2;
+        return 1;
     }();
     return k;
 }
@@ -427,6 +433,234 @@ void cg_pipeline_destroy(cg_pipeline *p) {
         if (p->bstream) (void)hipStreamDestroy(p->bstream);
     }
     delete p;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Multi-device batches (cg_multi_*, round 6): north_star's split -- a batch of NARs
+// shards one-file-per-GPU across the GPUs of one node, the chunk descriptors gathered to
+// one GPU -- behind the C ABI, so a single host process (the reference's node-bin,
+// crates/node-bin/src/main.rs:1-25, calling Node::put per PUT, crates/node/src/lib.rs:114-132)
+// can drive every GPU.  Each device runs its own digest pipeline on its shard (no data-path
+// exchange: FastCDC state never crosses files); the wait gathers the shards' descriptors
+// into the caller's array on devices[0] with peer copies over xGMI (hipMemcpyPeerAsync on
+// a stream of devices[0]) and concatenates the NAR index on the host.
+// ---------------------------------------------------------------------------
+namespace cgrt {
+
+struct MultiShard {
+    cg_batch *b = nullptr;
+    DevBuf *scratch = nullptr;  // descriptors of a shard on devices[k], k > 0 (pooled)
+    size_t n_nars = 0;
+    bool direct = false;        // shard 0: written straight into the caller's array
+};
+
+}  // namespace cgrt
+
+struct cg_multi {
+    std::vector<int> devices;
+    std::vector<cg_pipeline *> pipes;
+    hipStream_t gather = nullptr;  // on devices[0]
+    std::mutex mu;
+    std::vector<std::vector<std::unique_ptr<cgrt::DevBuf>>> pool;  // free scratch per shard index
+};
+
+struct cg_multi_batch {
+    cg_multi *m;
+    std::vector<cgrt::MultiShard> shards;
+    cg_desc *d_out;
+    size_t out_cap;
+};
+
+namespace cgrt {
+
+static void multi_release(cg_multi_batch *mb) {
+    cg_multi *m = mb->m;
+    std::lock_guard<std::mutex> lk(m->mu);
+    for (size_t k = 0; k < mb->shards.size(); ++k)
+        if (mb->shards[k].scratch) m->pool[k].emplace_back(mb->shards[k].scratch);
+}
+
+}  // namespace cgrt
+
+extern "C" {
+
+int cg_multi_create(const int *devices, size_t n_dev, uint32_t group_batches, uint32_t lanes, cg_multi **out) {
+    clear_error();
+    if (!out || !devices || n_dev == 0) return fail(CG_E_IO, "cg_multi_create: null handle pointer or no devices");
+    *out = nullptr;
+    if (n_dev > 64) return fail(CG_E_INVALID_OPTIONS, "cg_multi_create: at most 64 devices");
+    std::unique_ptr<cg_multi> m(new cg_multi());
+    m->devices.assign(devices, devices + n_dev);
+    m->pool.resize(n_dev);
+    auto fail_all = [&](int rc) {
+        for (cg_pipeline *p : m->pipes) cg_pipeline_destroy(p);
+        m->pipes.clear();
+        return rc;
+    };
+    for (size_t k = 0; k < n_dev; ++k) {
+        cg_pipeline *p = nullptr;
+        int rc = cg_pipeline_create(devices[k], group_batches, lanes, &p);
+        if (rc) return fail_all(rc);
+        m->pipes.push_back(p);
+    }
+    DeviceScope scope;
+    int rc = scope.set(devices[0]);
+    if (rc) return fail_all(rc);
+    // peer access to every other device's HBM (already enabled / same device: fine; without
+    // it hipMemcpyPeerAsync still copies, staged by the runtime)
+    for (size_t k = 1; k < n_dev; ++k)
+        if (devices[k] != devices[0]) {
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, devices[0], devices[k]) == hipSuccess && can) {
+                const hipError_t e = hipDeviceEnablePeerAccess(devices[k], 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return fail_all(hip_fail(e, "peer access"));
+                (void)hipGetLastError();
+            }
+        }
+    if (hipStreamCreateWithFlags(&m->gather, hipStreamNonBlocking) != hipSuccess)
+        return fail_all(fail(CG_E_IO, "cg_multi_create: gather stream"));
+    *out = m.release();
+    return CG_OK;
+}
+
+int cg_multi_submit(cg_multi *m, const uint8_t *const *d_data, const uint64_t *const *nar_offsets, const size_t *n_nars,
+                    uint64_t min_size, uint64_t avg_size, uint64_t max_size, int algo, cg_desc *d_out, size_t out_cap,
+                    void *const *inputs_ready, cg_multi_batch **batch) {
+    clear_error();
+    if (!m || !batch || !d_data || !nar_offsets || !n_nars) return fail(CG_E_IO, "cg_multi_submit: null argument");
+    *batch = nullptr;
+    Opts o;
+    int rc = resolve(min_size, avg_size, max_size, &o, nullptr, 0);
+    if (rc) return rc;
+    const size_t nd = m->devices.size();
+    std::unique_ptr<cg_multi_batch> mb(new cg_multi_batch{m, std::vector<MultiShard>(nd), d_out, out_cap});
+    auto undo = [&](int code) {
+        // shards already submitted: wait for them (their workspaces go back), keep the error
+        std::string msg = cg_last_error_message();
+        uint64_t det[3];
+        cg_last_error_detail(det);
+        for (auto &s : mb->shards)
+            if (s.b) (void)cg_batch_wait(s.b, nullptr);
+        multi_release(mb.get());
+        return fail_detail(code, msg, det);
+    };
+    for (size_t k = 0; k < nd; ++k) {
+        MultiShard &s = mb->shards[k];
+        s.n_nars = n_nars[k];
+        uint64_t cap = 0;
+        for (size_t i = 0; i < n_nars[k]; ++i) cap += capacity_of(nar_offsets[k][i + 1] - nar_offsets[k][i], o.min);
+        cg_desc *dst = nullptr;
+        size_t dst_cap = (size_t)cap;
+        if (k == 0) {
+            s.direct = true;
+            dst = d_out;
+            dst_cap = std::min<size_t>(out_cap, (size_t)cap);
+        } else {
+            {
+                std::lock_guard<std::mutex> lk(m->mu);
+                if (!m->pool[k].empty()) {
+                    s.scratch = m->pool[k].back().release();
+                    m->pool[k].pop_back();
+                }
+            }
+            if (!s.scratch) s.scratch = new DevBuf();
+            DeviceScope scope;
+            if ((rc = scope.set(m->devices[k])) ||
+                (rc = s.scratch->ensure((cap + 1) * sizeof(cg_desc), "multi-device shard descriptors")))
+                return undo(rc);
+            dst = s.scratch->as<cg_desc>();
+        }
+        if ((rc = cg_pipeline_submit(m->pipes[k], d_data[k], nar_offsets[k], n_nars[k], min_size, avg_size, max_size,
+                                     algo, dst, dst_cap, inputs_ready ? inputs_ready[k] : nullptr, &s.b)))
+            return undo(rc);
+    }
+    *batch = mb.release();
+    return CG_OK;
+}
+
+int cg_multi_wait(cg_multi_batch *batch, uint64_t *nar_first) {
+    clear_error();
+    if (!batch) return fail(CG_E_IO, "null multi-device batch handle");
+    std::unique_ptr<cg_multi_batch> mb(batch);
+    cg_multi *m = mb->m;
+    int rc = CG_OK;
+    std::string err;  // the first failure (each later cg_batch_wait clears the thread's error)
+    uint64_t det[3] = {0, 0, 0};
+    auto keep = [&](int r) {
+        if (r && !rc) {
+            rc = r;
+            err = cg_last_error_message();
+            cg_last_error_detail(det);
+        }
+    };
+    uint64_t base_nar = 0, base_desc = 0;
+    std::vector<uint64_t> first;
+    // every shard is waited for (and its workspace returned) whatever fails
+    for (size_t k = 0; k < mb->shards.size(); ++k) {
+        MultiShard &s = mb->shards[k];
+        first.assign(s.n_nars + 1, 0);
+        keep(cg_batch_wait(s.b, first.data()));
+        s.b = nullptr;
+        if (rc) continue;
+        const uint64_t n = first[s.n_nars];
+        if (base_desc + n > mb->out_cap) {
+            keep(fail(CG_E_CAPACITY, "descriptor output array too small"));
+            continue;
+        }
+        if (!s.direct && n) {
+            DeviceScope scope;
+            keep(scope.set(m->devices[0]));
+            if (rc) continue;
+            const hipError_t e = hipMemcpyPeerAsync(mb->d_out + base_desc, m->devices[0], s.scratch->p, m->devices[k],
+                                                    n * sizeof(cg_desc), m->gather);
+            if (e != hipSuccess) keep(hip_fail(e, "hipMemcpyPeerAsync (descriptor gather)"));
+        }
+        if (nar_first)
+            for (size_t i = 0; i < s.n_nars; ++i) nar_first[base_nar + i] = base_desc + first[i];
+        base_nar += s.n_nars;
+        base_desc += n;
+    }
+    if (nar_first && !rc) nar_first[base_nar] = base_desc;
+    {
+        DeviceScope scope;
+        if (scope.set(m->devices[0]) == CG_OK) {
+            const hipError_t e = hipStreamSynchronize(m->gather);
+            if (e != hipSuccess) keep(hip_fail(e, "descriptor gather"));
+        }
+    }
+    multi_release(mb.get());
+    return rc ? fail_detail(rc, err, det) : CG_OK;
+}
+
+int cg_multi_flush(cg_multi *m) {
+    clear_error();
+    if (!m) return fail(CG_E_IO, "null multi-device handle");
+    for (cg_pipeline *p : m->pipes) {
+        const int rc = cg_pipeline_flush(p);
+        if (rc) return rc;
+    }
+    return CG_OK;
+}
+
+void cg_multi_destroy(cg_multi *m) {
+    if (!m) return;
+    for (cg_pipeline *p : m->pipes) cg_pipeline_destroy(p);
+    {
+        DeviceScope scope;
+        (void)scope.set(m->devices[0]);
+        if (m->gather) {
+            (void)hipStreamSynchronize(m->gather);
+            (void)hipStreamDestroy(m->gather);
+        }
+        for (size_t k = 0; k < m->pool.size(); ++k) {
+            DeviceScope s2;
+            (void)s2.set(m->devices[k]);
+            for (auto &b : m->pool[k]) b->release();
+        }
+    }
+    delete m;
 }
 
 }  // extern "C"

@@ -143,9 +143,10 @@ int cg_chunk_batch_device_async_after(const uint8_t *d_data, const uint64_t *nar
  * cg_batch_event) or by cg_pipeline_flush.  Each batch completes as soon as its own chunks
  * are digested (the digest kernel signals it), not when its whole group does.  BLAKE3
  * batches run whole on the boundary stream, in submission order.  The pipeline uses
- * 1 + lanes streams on `device` (-1 = the current device; the caller's current device is
- * left unchanged by every pipeline call), each with a hardware queue of its own, whatever
- * GPU_MAX_HW_QUEUES is.  A batch is waited for with cg_batch_wait exactly once, as for
+ * 1 + lanes non-blocking high-priority streams on `device` (-1 = the current device; the
+ * caller's current device is left unchanged by every pipeline call), which HIP keeps off
+ * the hardware queues of the process's ordinary streams whatever GPU_MAX_HW_QUEUES is.
+ * A batch is waited for with cg_batch_wait exactly once, as for
  * cg_chunk_batch_device_async; results, errors and nar_first are the same as those of
  * cg_chunk_batch_device on the same inputs.  A pipeline is single-owner; its batches may
  * be waited for from any thread, also after cg_pipeline_destroy (which launches a still
@@ -164,6 +165,30 @@ void cg_pipeline_destroy(cg_pipeline *p);
  * the end of its group's merged digest), so device work can be ordered after it without a
  * host wait; launches the batch's group if it is still open.  Valid until cg_batch_wait. */
 int cg_batch_event(cg_batch *batch, void **event);
+
+/* Multi-device batches: north_star's split of a batch of NARs one-file-per-GPU across the
+ * GPUs of one node, with the descriptors gathered to one GPU, for a single host process
+ * (the reference's node-bin, crates/node-bin/src/main.rs:1-25, whose Node::put calls
+ * chunk_data per PUT, crates/node/src/lib.rs:114-132).  A cg_multi holds one digest
+ * pipeline per entry of `devices` (cg_pipeline_create(devices[k], group_batches, lanes));
+ * a device may be listed more than once.  cg_multi_submit queues shard k -- n_nars[k] NARs
+ * at nar_offsets[k] (host array starting at 0) in d_data[k], device memory on devices[k],
+ * after inputs_ready[k] (may be NULL, or hold NULLs) -- on device k's pipeline; there is no
+ * exchange on the data path (FastCDC state never crosses files).  cg_multi_wait waits for
+ * every shard and gathers their descriptors, shard after shard, into d_out (device memory
+ * on devices[0], out_cap descriptors) with peer copies over xGMI, and writes the global NAR
+ * index nar_first (sum of n_nars + 1 entries, may be NULL): the same result as one
+ * cg_chunk_batch_device call over all shards' NARs in order.  Every handle is waited for
+ * exactly once; cg_multi_flush launches every device's open group. */
+typedef struct cg_multi cg_multi;
+typedef struct cg_multi_batch cg_multi_batch;
+int cg_multi_create(const int *devices, size_t n_dev, uint32_t group_batches, uint32_t lanes, cg_multi **out);
+int cg_multi_submit(cg_multi *m, const uint8_t *const *d_data, const uint64_t *const *nar_offsets,
+                    const size_t *n_nars, uint64_t min_size, uint64_t avg_size, uint64_t max_size, int algo,
+                    cg_desc *d_out, size_t out_cap, void *const *inputs_ready, cg_multi_batch **batch);
+int cg_multi_wait(cg_multi_batch *batch, uint64_t *nar_first);
+int cg_multi_flush(cg_multi *m);
+void cg_multi_destroy(cg_multi *m);
 
 /* PushChunker (src/chunking.rs:753-829) over drain_finalized_chunks (:541-673).
  * push/finish write the chunks that became final; `out_cap` must be at least

@@ -9,7 +9,7 @@
 // and reports the wall time: ~ms = the test streams ran side by side, ~n x ms = they
 // shared a queue.
 // kinds: 0 ordinary, 1 high priority, 2 low priority, 3 full CU mask.
-// usage: queue_probe <kind> <n> <fillers> <ms>
+// usage: queue_probe <kind> <n> <fillers> <ms> [busy]
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
@@ -67,14 +67,21 @@ int main(int argc, char **argv) {
     for (auto &s : fill) hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s, 1000ull, d);
     CK(hipDeviceSynchronize());
     const unsigned long long ticks = (unsigned long long)(ms * 1e5);
+    // busy = 1: every filler runs a spin of the same length at the same time, so a test
+    // stream sharing a hardware queue with a filler finishes a spin later
+    const int busy = argc > 5 ? atoi(argv[5]) : 0;
     for (int r = 0; r < 3; ++r) {
+        if (busy)
+            for (auto &s : fill) hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s, ticks, d);
         const auto t0 = std::chrono::steady_clock::now();
         for (auto &s : test) hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, s, ticks, d);
-        CK(hipDeviceSynchronize());
+        for (auto &s : test) CK(hipStreamSynchronize(s));
         const double wall = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-        printf("{\"kind\": %d, \"n\": %d, \"fillers\": %d, \"spin_ms\": %.1f, \"wall_ms\": %.2f, \"ratio\": %.2f, "
-               "\"prio_range\": [%d, %d]}\n",
-               kind, n, fillers, ms, wall, wall / ms, lo, hi);
+        CK(hipDeviceSynchronize());
+        const double all = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        printf("{\"kind\": %d, \"n\": %d, \"fillers\": %d, \"busy\": %d, \"spin_ms\": %.1f, \"test_ms\": %.2f, "
+               "\"ratio\": %.2f, \"all_ms\": %.2f, \"prio_range\": [%d, %d]}\n",
+               kind, n, fillers, busy, ms, wall, wall / ms, all, lo, hi);
     }
     return 0;
 }

@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--steps", type=int, default=48)
     ap.add_argument("--slots", type=int, default=0, help="distinct input batches (0 = the largest depth)")
     ap.add_argument("--check", action="store_true")
+    ap.add_argument("--profile", action="store_true", help="time each merged digest kernel (cg_set_profiling(2))")
     ap.add_argument("--legacy", type=int, default=0, help="also time the round-5 async_after path at this depth")
     args = ap.parse_args()
 
@@ -65,7 +66,7 @@ def main():
     total = int(offs[-1])
     res = {"config": args.config, "slots": slots, "synth_s": round(synth_s, 1),
            "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "4(default)"),
-           "pipe_streams": os.environ.get("CHUNKER_AMD_PIPE_STREAMS", "cumask"), "runs": []}
+           "pipe_streams": os.environ.get("CHUNKER_AMD_PIPE_STREAMS", "high"), "runs": []}
 
     def run(pipe, n, t_issue, lat, firsts):
         for k in range(n):
@@ -76,6 +77,8 @@ def main():
                 firsts[tag % slots] = first
         return pipe
 
+    if args.profile:
+        ca.lib.cg_set_profiling(2)
     for g, l, depth in sweep:
         if depth > slots:
             continue
@@ -108,6 +111,9 @@ def main():
             firsts[tag % slots] = first
         drain_s = time.perf_counter() - t_dr
         st = pipe.stats()
+        if st.get("timed_groups"):
+            st["digest_ms_mean"] = round(st["digest_ms_sum"] / st["timed_groups"], 3)
+            st["digest_GiB_mean"] = round(st["digest_bytes_sum"] / st["timed_groups"] / 2**30, 2)
         row = {"group": g, "lanes": l, "depth": depth, "GiBps": round(done * total / el / 2**30, 2),
                "steps": done, "ms": round(el * 1e3, 2), "fill_ms": round(fill_s * 1e3, 2),
                "drain_ms": round(drain_s * 1e3, 2),

@@ -126,6 +126,19 @@ static int nodevice(void) {
     cg_pipeline_destroy(NULL);
     void *ev = NULL;
     CHECK(cg_batch_event(NULL, &ev) == CG_E_IO, "batch event without a batch");
+    const int devs[2] = {0, 0};
+    cg_multi *mu = (cg_multi *)1;
+    CHECK(cg_multi_create(devs, 2, 16, 2, &mu) == CG_E_NO_DEVICE && mu == NULL, "multi create");
+    CHECK(cg_multi_create(devs, 0, 16, 2, &mu) == CG_E_IO, "multi create without devices");
+    const uint8_t *shard_data[1] = {data};
+    const uint64_t *shard_offs[1] = {boffs};
+    const size_t shard_n[1] = {1};
+    cg_multi_batch *mb = NULL;
+    CHECK(cg_multi_submit(NULL, shard_data, shard_offs, shard_n, 0, 0, 0, CG_SHA256, out, 64, NULL, &mb) == CG_E_IO,
+          "multi submit without a handle");
+    CHECK(cg_multi_wait(NULL, first) == CG_E_IO, "multi wait without a batch");
+    CHECK(cg_multi_flush(NULL) == CG_E_IO, "multi flush without a handle");
+    cg_multi_destroy(NULL);
     cg_push *p = cg_push_new(0, 0, 0, CG_SHA256, &st);
     if (p) {
         CHECK(cg_push_push(p, data, sizeof data, out, 64, &n) == CG_E_NO_DEVICE, "push");

@@ -868,57 +868,62 @@ def test_async_after_inputs_ready_matches_sync(ca, O, mode):
     copy = torch.cuda.Stream()
     batches = []
     old_mode = ca.lib.cg_test_split_mode(mode)  # 2: the digests of queued batches overlap too
-    for seed, algo in ((11, SHA), (12, B3), (13, SHA), (14, SHA), (15, B3)):
-        sizes = [4 << 20] * 12 + [8 * seed + 4096, 300_008]
-        data, offs = synth_nars(sizes, first_index=1000 * seed)
-        cap = ca.chunking.batch_capacity(offs, 16384)
-        ref = torch.from_numpy(data).cuda()
-        ref_out = torch.zeros(cap * 48, dtype=torch.uint8, device="cuda")
-        ref_first = ca.chunk_batch_device(ref.data_ptr(), offs, ref_out.data_ptr(), cap, 16384, 65536, 262144,
-                                          hash=algo, stream=torch.cuda.current_stream().cuda_stream)
-        del ref
-        batches.append((torch.from_numpy(data).pin_memory(), offs, cap, algo, ref_out.cpu().numpy(), ref_first, data))
-    torch.cuda.synchronize()
-    devs = [torch.empty(len(b[6]) + 256, dtype=torch.uint8, device="cuda") for b in batches]
-    outs = [torch.full((b[2] * 48,), 0xAB, dtype=torch.uint8, device="cuda") for b in batches]
-    inflight = []
-    for k, b in enumerate(batches):
-        with torch.cuda.stream(copy):  # the input arrives on the copy stream
-            devs[k][: len(b[6])].copy_(b[0], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
-        inflight.append(ca.chunk_batch_device_async(devs[k].data_ptr(), b[1], outs[k].data_ptr(), b[2], 16384, 65536,
-                                                    262144, hash=b[3], stream=stream.cuda_stream,
-                                                    inputs_ready=ev.cuda_event))
-    # work queued on `stream` after the calls follows every batch (mode 2 joins each batch's
-    # end into it): copies queued now, before any wait, must see the finished descriptors
-    tails = [torch.empty_like(o) for o in outs]
-    with torch.cuda.stream(stream):
-        for t, o in zip(tails, outs):
-            t.copy_(o)
-    stream.synchronize()  # waits for the copies, which wait for every batch
-    for k, h in enumerate(inflight):
-        first = h.wait()
-        _, offs, cap, algo, ref_out, ref_first, data = batches[k]
-        assert torch.equal(tails[k], outs[k]), f"batch{k}: work queued after it on the stream ran early"
-        assert np.array_equal(first, ref_first), k
-        n = int(first[-1])
-        got = outs[k].cpu().numpy()
-        assert np.array_equal(got[: n * 48], ref_out[: n * 48]), k
-        descs = got.view(ca.DESC_DTYPE)
-        want = O.chunk_descriptors(data[offs[12]:offs[13]], 16384, 65536, 262144, algo=algo)
-        assert_same(descs[int(first[12]):int(first[13])], want, f"batch{k} nar12")
-    ca.lib.cg_test_split_mode(old_mode)
+    try:
+        for seed, algo in ((11, SHA), (12, B3), (13, SHA), (14, SHA), (15, B3)):
+            sizes = [4 << 20] * 12 + [8 * seed + 4096, 300_008]
+            data, offs = synth_nars(sizes, first_index=1000 * seed)
+            cap = ca.chunking.batch_capacity(offs, 16384)
+            ref = torch.from_numpy(data).cuda()
+            ref_out = torch.zeros(cap * 48, dtype=torch.uint8, device="cuda")
+            ref_first = ca.chunk_batch_device(ref.data_ptr(), offs, ref_out.data_ptr(), cap, 16384, 65536, 262144,
+                                              hash=algo, stream=torch.cuda.current_stream().cuda_stream)
+            del ref
+            batches.append((torch.from_numpy(data).pin_memory(), offs, cap, algo, ref_out.cpu().numpy(), ref_first, data))
+        torch.cuda.synchronize()
+        devs = [torch.empty(len(b[6]) + 256, dtype=torch.uint8, device="cuda") for b in batches]
+        outs = [torch.full((b[2] * 48,), 0xAB, dtype=torch.uint8, device="cuda") for b in batches]
+        inflight = []
+        for k, b in enumerate(batches):
+            with torch.cuda.stream(copy):  # the input arrives on the copy stream
+                devs[k][: len(b[6])].copy_(b[0], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+            inflight.append(ca.chunk_batch_device_async(devs[k].data_ptr(), b[1], outs[k].data_ptr(), b[2], 16384, 65536,
+                                                        262144, hash=b[3], stream=stream.cuda_stream,
+                                                        inputs_ready=ev.cuda_event))
+        # work queued on `stream` after the calls follows every batch (mode 2 joins each batch's
+        # end into it): copies queued now, before any wait, must see the finished descriptors
+        tails = [torch.empty_like(o) for o in outs]
+        with torch.cuda.stream(stream):
+            for t, o in zip(tails, outs):
+                t.copy_(o)
+        stream.synchronize()  # waits for the copies, which wait for every batch
+        for k, h in enumerate(inflight):
+            first = h.wait()
+            _, offs, cap, algo, ref_out, ref_first, data = batches[k]
+            assert torch.equal(tails[k], outs[k]), f"batch{k}: work queued after it on the stream ran early"
+            assert np.array_equal(first, ref_first), k
+            n = int(first[-1])
+            got = outs[k].cpu().numpy()
+            assert np.array_equal(got[: n * 48], ref_out[: n * 48]), k
+            descs = got.view(ca.DESC_DTYPE)
+            want = O.chunk_descriptors(data[offs[12]:offs[13]], 16384, 65536, 262144, algo=algo)
+            assert_same(descs[int(first[12]):int(first[13])], want, f"batch{k} nar12")
+    finally:
+        ca.lib.cg_test_split_mode(old_mode)
 
 
-@pytest.mark.parametrize("depth", [None, 1, 3, 20], ids=["default", "one", "three", "twenty"])
-def test_batch_pipeline_matches_sync(ca, O, depth):
+@pytest.mark.parametrize("depth,group", [(None, None), (1, None), (3, 2), (20, 4), (None, 0), (3, 0), (20, 0)],
+                         ids=["default", "one", "three_g2", "twenty_g4", "perbatch_default", "perbatch_three",
+                              "perbatch_twenty"])
+def test_batch_pipeline_matches_sync(ca, O, depth, group):
     """chunker_amd.BatchPipeline (one thread, up to `depth` batches in flight, each after
-    its own inputs-ready event, DESIGN.md §7 "Batches in flight"): twelve SHA-256 batches
-    through one pipeline (default depth: 2 at this process's 4 hardware queues; with fewer
-    output arrays than the depth the test drains early) come back in submission order, each
-    equal to the synchronous entry, with the oracle on a sampled NAR; the output arrays
-    rotate, each reused only after its batch was returned."""
+    its own inputs-ready event, DESIGN.md §7 "Batches in flight"), as the digest pipeline
+    (group None = default_group, or merged groups of 2 / 4) and as the round-5 per-batch
+    stream path (group 0; default depth 2 at this process's 4 hardware queues): twelve or
+    more SHA-256 batches (with fewer output arrays than the depth the test drains early)
+    come back in submission order, each equal to the synchronous entry, with the oracle on a
+    sampled NAR; the output arrays rotate, each reused only after its batch was returned."""
     import torch
 
     from chunker_amd.nar import synth_nars
@@ -939,7 +944,7 @@ def test_batch_pipeline_matches_sync(ca, O, depth):
     results = []
     free = list(range(n_out))
     busy = {}
-    with ca.BatchPipeline(depth, 16384, 65536, 262144, stream=stream.cuda_stream) as pipe:
+    with ca.BatchPipeline(depth, 16384, 65536, 262144, stream=stream.cuda_stream, group=group) as pipe:
         for k in range(nb):
             j = free.pop(0)
             busy[k] = j

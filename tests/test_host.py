@@ -90,6 +90,19 @@ def test_bench_cli_contract():
         assert flag in r.stdout, flag
 
 
+def test_bench_timed_group():
+    """bench.py's group: the divisor of --steps nearest the library default, so the timed
+    steps are whole merged groups."""
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    import bench
+
+    assert bench.timed_group(24, 20) == 20 and bench.timed_group(24, 48) == 24 and bench.timed_group(24, 5) == 5
+    assert bench.timed_group(1, 20) == 1 and bench.timed_group(24, 96) == 24 and bench.timed_group(16, 20) == 20
+
+
 def test_default_depth_and_group():
     """Per-batch-stream path (group=0): 20 batches in flight for sub-4-GiB SHA-256 batches,
     4 from 4 GiB, 2 for BLAKE3, never more than the hardware queues less 2 (each batch in
@@ -103,7 +116,7 @@ def test_default_depth_and_group():
     assert dd(1, G, 4) == 2 and dd(1, 16 * G, 4) == 2
     assert dd(1, G) == dd(1, G, ca.lib.cg_hw_queues())
     dg = chunking.default_group
-    assert dg(1, G) == 16 and dg(1, 4 * G) == 4 and dg(1, 16 * G) == 1 and dg(1, 64 << 20) == 64
+    assert dg(1, G) == 24 and dg(1, 4 * G) == 6 and dg(1, 16 * G) == 1 and dg(1, 64 << 20) == 64
     assert dg(0, G) == 1
 
 
@@ -197,16 +210,16 @@ def test_batch_pipeline_digest_pipeline_host_logic(monkeypatch):
         return FakeBatch(len(sub) - 1)
 
     monkeypatch.setattr(chunking, "pipeline_submit", fake_submit)
-    offs = np.array([0, 1 << 30], np.uint64)  # 1 GiB batches: default group 16
+    offs = np.array([0, 1 << 30], np.uint64)  # 1 GiB batches: default group 24
     with chunking.BatchPipeline(lanes=2) as p:
         got = []
-        for k in range(50):
+        for k in range(80):
             got += p.submit(k, offs, 2, 3, inputs_ready=9, tag=k)
-        assert p.group == 16 and p.depth == 48 and len(p) == 47
+        assert p.group == 24 and p.depth == 72 and len(p) == 71
         got += p.drain()
-    assert log[0] == ("create", -1, 16, 2)
-    assert [t for t, _ in got] == list(range(50))
-    assert all(r == 9 for _, r in sub) and [d for d, _ in sub] == list(range(50))
-    assert log.index(("flush", 77)) < log.index(("wait", 3))  # drain flushes first
+    assert log[0] == ("create", -1, 24, 2)
+    assert [t for t, _ in got] == list(range(80))
+    assert all(r == 9 for _, r in sub) and [d for d, _ in sub] == list(range(80))
+    assert log.index(("flush", 77)) < log.index(("wait", 9))  # drain flushes first
     assert log[-1] == ("destroy", 77)
-    assert log.index(("wait", 0)) > log.index(("submit", 47))
+    assert log.index(("wait", 0)) > log.index(("submit", 71))
