@@ -91,6 +91,9 @@ def parse_args():
                          "cg_chunk_batch_device_async_after)")
     ap.add_argument("--lanes", type=int, default=0, choices=range(0, 9), metavar="0..8",
                     help="merged digests in flight (cg_pipeline_create lanes; 0: chunker_amd.PIPE_LANES)")
+    ap.add_argument("--sha-occ", default="",
+                    help="SHA-256 workgroups per CU 'LATENCY,FILL' for launches with more workgroups than CUs "
+                         "(cg_test_sha_occupancy; '' = the library's)")
     ap.add_argument("--no-stage-profile", action="store_true",
                     help="skip the per-stage single steps (so a kernel trace holds only the pipeline's launches)")
     ap.add_argument("--no-clock", action="store_true", help="skip the digest clock measurement (scripts/sha_clock.py)")
@@ -196,6 +199,10 @@ def main():
     if args.no_coalesce:
         ca.lib.cg_test_coalesce(0)
     ca.lib.cg_test_split_mode(args.split_mode)
+    if args.sha_occ:
+        lat_occ, fill_occ = (int(v) for v in args.sha_occ.split(","))
+        ca.lib.cg_test_sha_occupancy(0, lat_occ)
+        ca.lib.cg_test_sha_occupancy(1, fill_occ)
     if args.sha_tiers:
         t = [int(v) for v in args.sha_tiers.split(",")]
         ca.lib.cg_test_sha_tiers(t[0], t[1])
@@ -547,6 +554,8 @@ def main():
                          "per-batch streams (cg_chunk_batch_device_async_after)",
                          "group": group, "lanes": lanes if group else None, "depth": depth,
                          "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "4 (HIP default)"),
+                         "sha_wgs_per_cu": [int(ca.lib.cg_test_sha_occupancy(k, ca.lib.cg_test_sha_occupancy(k, 1)))
+                                            for k in (0, 1)],
                          "fill_ms": round(fill_ms, 2), "settle_steps": settled[0], "settle_ms": round(settle_ms, 2),
                          "settle_GiBps": round(settled[0] * total_bytes * world / (settle_ms * 1e-3) / GIB, 3),
                          "drain_ms": round(drain_ms, 2),

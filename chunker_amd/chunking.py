@@ -446,7 +446,8 @@ def default_group(hash: HashAlgorithm, batch_bytes: int) -> int:
     BLAKE3: 1 (not merged)."""
     if HashAlgorithm(hash) != HashAlgorithm.Sha256:
         return 1
-    return int(max(1, min(64, PIPE_GROUP_BYTES // max(int(batch_bytes), 1))))
+    b = max(int(batch_bytes), 1)
+    return int(max(1, min(64, (PIPE_GROUP_BYTES + b // 2) // b)))
 
 
 class BatchPipeline:

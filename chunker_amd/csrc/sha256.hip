@@ -7,6 +7,8 @@
 // loaded as aligned dwords and realigned + byte-swapped with one v_perm_b32 per
 // word (chunk offsets are arbitrary bytes).  Rotates are v_alignbit_b32.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstddef>
 
 #include "common.h"
@@ -155,10 +157,30 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return v;
 }
 
-#ifndef CG_PC_RING
-#define CG_PC_RING 4u
+// LDS schedule ring.  Split (quad / pair) workgroups hold at most 32 chunk rows and use
+// PC_RING slots of 32 rows; one-lane workgroups hold 64 rows and use PC_RING1 slots of 64
+// rows (68 KiB: two workgroups per CU, one wave per SIMD).  Round 6
+// measured smaller one-lane rings for more workgroups per CU: a one-lane consumer holds
+// block k + 1's words in registers from the middle of block k on, so with early release
+// (SHA_EARLY: it frees both slots at the end of block k) three slots give the producer the
+// slack four give without it, at 51 KiB (three workgroups per CU), and two slots fit four.
+// None was faster: config 4 793 (3 slots, 3 per CU) / 800 (2 slots, 4 per CU) against 802
+// GiB/s (4 slots, 2 per CU), config 5 582 / 620 against 698-710, config 2's merged digest
+// 83-86 ms against 69.4 ms; at 2 per CU the 3-slot ring lost 20 % (c4 642)
+// (profiles/r06_v8_ring_occupancy.txt, PMC in r06_v9_pmc_c4_*.json).  So the product
+// keeps 4 slots; CG_PC_RING1 / CG_SHA_EARLY build the variants (scripts/build_variant.sh).
+#define PC_RING 4u  // split tiers: the producer runs up to PC_RING blocks ahead
+#ifndef CG_PC_RING1
+#define CG_PC_RING1 4u
 #endif
-#define PC_RING CG_PC_RING  // LDS schedule slots: the producer runs up to PC_RING blocks ahead
+#define PC_RING1 CG_PC_RING1  // one-lane tier
+#ifndef CG_SHA_EARLY
+#define CG_SHA_EARLY 0u
+#endif
+#define SHA_EARLY CG_SHA_EARLY  // one-lane consumer releases block k + 1's slot at the end of block k
+#define SPL_SLOT (32u * PC_ROW)
+#define ONE_SLOT (64u * PC_ROW)
+#define PC_LDS_WORDS (PC_RING * SPL_SLOT > PC_RING1 * ONE_SLOT ? PC_RING * SPL_SLOT : PC_RING1 * ONE_SLOT)
 
 // Spin guard: no legitimate wait for a ring slot lasts more than a few blocks
 // (~10^4 clocks); after `limit` sleeps (2^26 by default, ~2 s) a wait gives up so a
@@ -180,7 +202,7 @@ __device__ __forceinline__ bool spin_expired(const uint32_t *sync, uint32_t &it)
 }
 
 // Wait until `*ctr` moved past `k` (consumer: producer filled slot k) -- `ready`
-// form -- or until slot k is free (producer: consumer released k - PC_RING).
+// form -- or until slot k is free (producer: consumer released k - R, R = the ring's slots).
 __device__ __forceinline__ unsigned long long wait_ready(const uint32_t *ctr, uint32_t k, bool timed) {
     if (lds_load_acquire(ctr) > k) return 0;
     const unsigned long long t0 = timed ? __builtin_amdgcn_s_memtime() : 0ull;
@@ -190,12 +212,13 @@ __device__ __forceinline__ unsigned long long wait_ready(const uint32_t *ctr, ui
     }
     return timed ? __builtin_amdgcn_s_memtime() - t0 : 0ull;
 }
+template <uint32_t R>
 __device__ __forceinline__ unsigned long long wait_slot(const uint32_t *done, uint32_t k, bool timed) {
-    if ((int)(k - lds_load_acquire(done)) < (int)PC_RING) return 0;
+    if ((int)(k - lds_load_acquire(done)) < (int)R) return 0;
     const unsigned long long t0 = timed ? __builtin_amdgcn_s_memtime() : 0ull;
     const uint32_t *sync = done - SY_DONE;
     uint32_t it = 0;
-    while ((int)(k - lds_load_acquire(done)) >= (int)PC_RING && !spin_expired(sync, it)) {
+    while ((int)(k - lds_load_acquire(done)) >= (int)R && !spin_expired(sync, it)) {
     }
     return timed ? __builtin_amdgcn_s_memtime() - t0 : 0ull;
 }
@@ -246,9 +269,9 @@ __device__ __forceinline__ uint32_t perm_sel(uint32_t shift) {
 
 // Producer wave of a one-lane-per-chunk workgroup: for k = 0..NB-1 wait for a free
 // ring slot, load + realign + pad block k of this lane's chunk, expand its schedule
-// (W[t] + K[t], 64 words) into row `row` of slot k % PC_RING, publish.
+// (W[t] + K[t], 64 words) into row `row` of slot k % PC_RING1, publish.
 __device__ unsigned long long sha_produce(const uint8_t *p, uint64_t len, uint32_t nbt, uint32_t NB,
-                                          uint32_t (*sW)[64 * PC_ROW], uint32_t row, uint32_t lane,
+                                          uint32_t (*sW)[ONE_SLOT], uint32_t row, uint32_t lane,
                                           uint32_t *s_ready, const uint32_t *s_done, bool timed) {
     unsigned long long t_spin = 0;
     const uint64_t nb = len >> 6;
@@ -270,7 +293,7 @@ __device__ unsigned long long sha_produce(const uint8_t *p, uint64_t len, uint32
     };
     if (nb > 0) load_full(0);
     for (uint32_t k = 0; k < NB; ++k) {
-        t_spin += wait_slot(s_done, k, timed);
+        t_spin += wait_slot<PC_RING1>(s_done, k, timed);
         if (k < nbt) {
             uint32_t w[16];
             if (k < nb) {
@@ -283,7 +306,7 @@ __device__ unsigned long long sha_produce(const uint8_t *p, uint64_t len, uint32
             } else {
                 sha_pad_words(w, p, base, sel, len, k);
             }
-            sha_schedule_store(w, &sW[k % PC_RING][row * PC_ROW]);
+            sha_schedule_store(w, &sW[k % PC_RING1][row * PC_ROW]);
         }
         publish(s_ready, k, lane);
     }
@@ -554,7 +577,7 @@ __device__ __forceinline__ void sha_schedule_pair_store(const uint32_t R0[8], co
 }
 
 __device__ unsigned long long sha_produce_pair(const uint8_t *p, uint64_t len, uint32_t nbt, uint32_t NB,
-                                               uint32_t (*sW)[64 * PC_ROW], uint32_t row, bool hi, uint32_t lane,
+                                               uint32_t (*sW)[SPL_SLOT], uint32_t row, bool hi, uint32_t lane,
                                                uint32_t *s_ready, const uint32_t *s_done, bool timed) {
     unsigned long long t_spin = 0;
     const uint64_t nb = len >> 6;
@@ -580,7 +603,7 @@ __device__ unsigned long long sha_produce_pair(const uint8_t *p, uint64_t len, u
     uint32_t *const dst0 = &sW[0][row * PC_ROW + (hi ? 32u : 0u)];
     if (nb > 0) load_full(0);
     for (uint32_t k = 0; k < NB; ++k) {
-        t_spin += wait_slot(s_done, k, timed);
+        t_spin += wait_slot<PC_RING>(s_done, k, timed);
         if (k < nbt) {
             uint32_t R[8];
             if (k < nb) {
@@ -594,7 +617,7 @@ __device__ unsigned long long sha_produce_pair(const uint8_t *p, uint64_t len, u
 #pragma unroll
                 for (int i = 0; i < 8; ++i) R[i] = hi ? w[2 * i + 1] : w[2 * i];
             }
-            sha_schedule_pair_store(R, Kp, dst0 + (k % PC_RING) * (64 * PC_ROW));
+            sha_schedule_pair_store(R, Kp, dst0 + (k % PC_RING) * SPL_SLOT);
         }
         publish(s_ready, k, lane);
     }
@@ -605,7 +628,7 @@ __device__ unsigned long long sha_produce_pair(const uint8_t *p, uint64_t len, u
 // Consumer wave of a pair (QUAD = false: lo/hi = banks 0,2 / 1,3 of a DPP row, one
 // lane each) or quad (QUAD = true: the same banks, 4 lanes each) workgroup.
 template <bool QUAD>
-__device__ void split_consumer(uint32_t (*sW)[64 * PC_ROW], uint32_t row, bool hi, uint32_t lane, uint32_t NB,
+__device__ void split_consumer(uint32_t (*sW)[SPL_SLOT], uint32_t row, bool hi, uint32_t lane, uint32_t NB,
                                uint32_t NBmin, uint32_t nbt, uint32_t *s_ready, uint32_t *s_done, uint32_t st[4],
                                unsigned long long *t_spin, bool timed) {
     SplitLane c;
@@ -642,7 +665,7 @@ __device__ void split_consumer(uint32_t (*sW)[64 * PC_ROW], uint32_t row, bool h
     // k + 1 and k + 2 sit in ring slots (1, 2) and (3, 0) in turn: each row offset toggles
     // by one subtraction from a constant.
     static_assert(PC_RING == 4, "split_pair_main's slot toggling assumes a 4-slot ring");
-    constexpr uint32_t SLOT = 64 * PC_ROW;
+    constexpr uint32_t SLOT = SPL_SLOT;
     const uint32_t *ring = &sW[0][0];
     uint32_t oB = off + SLOT, oA = off + 2 * SLOT;
     const uint32_t cB = 2 * off + 4 * SLOT, cA = 2 * off + 2 * SLOT;
@@ -719,7 +742,9 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
         const uint32_t np = (rest + 31u) / 32u;
         if (np < npair) npair = np;
     }
-    __shared__ __attribute__((aligned(16))) uint32_t sW[PC_RING][64 * PC_ROW];
+    __shared__ __attribute__((aligned(16))) uint32_t sLDS[PC_LDS_WORDS];
+    uint32_t(*sW)[ONE_SLOT] = reinterpret_cast<uint32_t(*)[ONE_SLOT]>(sLDS);     // one-lane view
+    uint32_t(*sWs)[SPL_SLOT] = reinterpret_cast<uint32_t(*)[SPL_SLOT]>(sLDS);    // split view
     // hand-off words (SY_*): blocks filled by the producer / consumed by the consumer,
     // the spin guard's timeout flag and limit
     __shared__ uint32_t s_sync[SY_N];
@@ -770,7 +795,7 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
         if (mode == 1) {  // diag: no producer work, consumer rounds on stale schedules
             if (lane == 0) lds_store_release(&s_ready, 0xffffffffu);
         } else if (split) {
-            t_spin = sha_produce_pair(p, len, nbt, NB, sW, row, hi, lane, &s_ready, &s_done, diag != nullptr);
+            t_spin = sha_produce_pair(p, len, nbt, NB, sWs, row, hi, lane, &s_ready, &s_done, diag != nullptr);
         } else {
             t_spin = sha_produce(p, len, nbt, NB, sW, row, lane, &s_ready, &s_done, diag != nullptr);
         }
@@ -782,9 +807,9 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
     } else if (split) {
         uint32_t st[4];
         if (quad)
-            split_consumer<true>(sW, row, hi, lane, NB, NBmin, nbt, &s_ready, &s_done, st, &t_spin, diag != nullptr);
+            split_consumer<true>(sWs, row, hi, lane, NB, NBmin, nbt, &s_ready, &s_done, st, &t_spin, diag != nullptr);
         else
-            split_consumer<false>(sW, row, hi, lane, NB, NBmin, nbt, &s_ready, &s_done, st, &t_spin, diag != nullptr);
+            split_consumer<false>(sWs, row, hi, lane, NB, NBmin, nbt, &s_ready, &s_done, st, &t_spin, diag != nullptr);
         if (diag && lane == 0) sha_diag_consumer(diag, t_spin, t_start, rt_start);
         if (valid && (!quad || (lane & 3u) == 0)) {  // hi: H0..H3 (bytes 0-15), lo: H4..H7 (bytes 16-31)
             uint8_t *hb = nt.dst ? reinterpret_cast<uint8_t *>(nt.dst[ci]) : hash_base + ci * stride;
@@ -803,28 +828,30 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
         // Every lane runs every block's rounds (lanes whose chunk is done work on stale
         // words and keep their state by select): with part of the wave masked off, the
         // dependent round chain ran up to 1.7x slower per round on gfx950.
+        // after block k (and the wait that lands block k + 1's words in registers) both
+        // their slots are free: release k + 1 + SHA_EARLY
         uint32_t k = 0;
         for (; k + 1 < NBmin; k += 2) {  // blocks every valid lane's chunk has: no select
-            sha_rounds_pf<false>(st, wA, wB, &sW[(k + 1) % PC_RING][lane * PC_ROW], k + 1, k + 1 < NB && mode != 2,
+            sha_rounds_pf<false>(st, wA, wB, &sW[(k + 1) % PC_RING1][lane * PC_ROW], k + 1, k + 1 < NB && mode != 2,
                                  &s_ready, true);
             __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-            lds_store_release(&s_done, k + 1);
-            sha_rounds_pf<false>(st, wB, wA, &sW[(k + 2) % PC_RING][lane * PC_ROW], k + 2, k + 2 < NB && mode != 2,
+            lds_store_release(&s_done, k + 1 + SHA_EARLY);
+            sha_rounds_pf<false>(st, wB, wA, &sW[(k + 2) % PC_RING1][lane * PC_ROW], k + 2, k + 2 < NB && mode != 2,
                                  &s_ready, true);
             __builtin_amdgcn_s_waitcnt(0xc07f);
-            lds_store_release(&s_done, k + 2);
+            lds_store_release(&s_done, k + 2 + SHA_EARLY);
         }
         for (; k < NB; k += 2) {
             // block k from wA, block k+1's schedule prefetched into wB
-            sha_rounds_pf<true>(st, wA, wB, &sW[(k + 1) % PC_RING][lane * PC_ROW], k + 1, k + 1 < NB && mode != 2,
+            sha_rounds_pf<true>(st, wA, wB, &sW[(k + 1) % PC_RING1][lane * PC_ROW], k + 1, k + 1 < NB && mode != 2,
                           &s_ready, k < nbt);
             __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-            lds_store_release(&s_done, k + 1);
+            lds_store_release(&s_done, k + 1 + SHA_EARLY);
             if (k + 1 >= NB) break;
-            sha_rounds_pf<true>(st, wB, wA, &sW[(k + 2) % PC_RING][lane * PC_ROW], k + 2, k + 2 < NB && mode != 2,
+            sha_rounds_pf<true>(st, wB, wA, &sW[(k + 2) % PC_RING1][lane * PC_ROW], k + 2, k + 2 < NB && mode != 2,
                           &s_ready, k + 1 < nbt);
             __builtin_amdgcn_s_waitcnt(0xc07f);
-            lds_store_release(&s_done, k + 2);
+            lds_store_release(&s_done, k + 2 + SHA_EARLY);
         }
         if (diag && lane == 0) sha_diag_consumer(diag, t_spin, t_start, rt_start);
         if (valid) {
@@ -1033,6 +1060,29 @@ uint32_t sha256_grid(uint64_t max_chunks, uint64_t expected, uint32_t *nquad_out
     return (uint32_t)(nq + np + (rest + 63) / 64);
 }
 
+// Workgroups per CU of a launch with more workgroups than CUs: [0] latency-bound (the
+// chip mostly idle but for the chains: merged pipeline groups), [1] GPU-filling (config 4 /
+// 5 shapes).  The ring (34 KiB) admits 4; fewer leave each consumer a SIMD of its own for
+// longer.  CHUNKER_AMD_SHA_OCC="latency,fill" (read once; A/B) or cg_test_sha_occupancy.
+uint32_t g_sha_occ[2] = {0, 0};
+static uint32_t sha_wgs_per_cu(bool fill) {
+    static const bool init = [] {
+        uint32_t a = 4, b = 4;
+        if (const char *e = getenv("CHUNKER_AMD_SHA_OCC")) (void)sscanf(e, "%u,%u", &a, &b);
+        if (!g_sha_occ[0]) g_sha_occ[0] = std::min(std::max(a, 1u), 4u);
+        if (!g_sha_occ[1]) g_sha_occ[1] = std::min(std::max(b, 1u), 4u);
+        return true;
+    }();
+    (void)init;
+    return g_sha_occ[fill ? 1 : 0];
+}
+// Dynamic LDS that holds a CU to `n` workgroups: past 160 KiB / (n + 1) in all.
+static size_t lds_pad_for(uint32_t n) {
+    constexpr size_t ring_bytes = PC_LDS_WORDS * 4 + 64;  // (+ the hand-off words)
+    const size_t want = 163840 / (n + 1) + 1024;
+    return want > ring_bytes ? want - ring_bytes : 0;
+}
+
 // Shape of this thread's last digest launch (cg_last_sha_tiers): quad, pair and
 // one-lane workgroups, dynamic LDS pad bytes.
 thread_local uint32_t t_sha_tiers[4];
@@ -1055,9 +1105,11 @@ void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
                                 : nullptr;
     // Latency-bound batches (no more workgroups than CUs): pad the LDS request past half
     // a CU's 160 KiB so no two workgroups share a CU, and a consumer wave never shares a
-    // SIMD with another workgroup's wave (which costs it 20-90 % per round).
-    constexpr size_t ring_bytes = PC_RING * 64 * PC_ROW * 4;
-    const size_t pad = nwg <= 256 ? (ring_bytes < 81920 + 4096 ? 81920 + 4096 - ring_bytes : 0) : 0;
+    // SIMD with another workgroup's wave (which costs it 20-90 % per round).  Larger
+    // launches: at most sha_wgs_per_cu(fill) workgroups per CU (the ring's 34 KiB alone
+    // lets four in: two waves per SIMD).
+    const uint32_t per_cu = nwg <= 256 ? 1u : sha_wgs_per_cu(fill);
+    const size_t pad = lds_pad_for(per_cu);
     t_sha_tiers[0] = nquad;
     t_sha_tiers[1] = npair;
     t_sha_tiers[2] = nwg - nquad - npair;
@@ -1361,6 +1413,15 @@ static uint32_t set_sha_tiers(int k, uint32_t quad_pm, uint32_t pair_pm) {
 extern "C" uint32_t cg_test_sha_tiers(uint32_t quad_pm, uint32_t pair_pm) { return set_sha_tiers(0, quad_pm, pair_pm); }
 extern "C" uint32_t cg_test_sha_tiers_fill(uint32_t quad_pm, uint32_t pair_pm) {
     return set_sha_tiers(1, quad_pm, pair_pm);
+}
+
+// Test hook: workgroups per CU of latency-bound (which = 0) / GPU-filling (1) launches with
+// more workgroups than CUs (1..4); returns the previous value.
+extern "C" uint32_t cg_test_sha_occupancy(uint32_t which, uint32_t v) {
+    (void)cg::sha_wgs_per_cu(false);
+    const uint32_t k = which ? 1u : 0u, old = cg::g_sha_occ[k];
+    cg::g_sha_occ[k] = std::min(std::max(v, 1u), 4u);
+    return old;
 }
 
 extern "C" uint32_t cg_test_sha_quad_max(uint32_t v) {

@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--slots", type=int, default=0, help="distinct input batches (0 = the largest depth)")
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--profile", action="store_true", help="time each merged digest kernel (cg_set_profiling(2))")
+    ap.add_argument("--sha-occ", default="", help="LATENCY,FILL workgroups per CU (cg_test_sha_occupancy)")
     ap.add_argument("--legacy", type=int, default=0, help="also time the round-5 async_after path at this depth")
     args = ap.parse_args()
 
@@ -79,6 +80,11 @@ def main():
 
     if args.profile:
         ca.lib.cg_set_profiling(2)
+    if args.sha_occ:
+        a, b = (int(v) for v in args.sha_occ.split(","))
+        ca.lib.cg_test_sha_occupancy(0, a)
+        ca.lib.cg_test_sha_occupancy(1, b)
+        res["sha_occ"] = [a, b]
     for g, l, depth in sweep:
         if depth > slots:
             continue

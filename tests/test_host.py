@@ -116,7 +116,8 @@ def test_default_depth_and_group():
     assert dd(1, G, 4) == 2 and dd(1, 16 * G, 4) == 2
     assert dd(1, G) == dd(1, G, ca.lib.cg_hw_queues())
     dg = chunking.default_group
-    assert dg(1, G) == 24 and dg(1, 4 * G) == 6 and dg(1, 16 * G) == 1 and dg(1, 64 << 20) == 64
+    assert dg(1, G) == 24 and dg(1, 4 * G) == 6 and dg(1, 16 * G) == 2 and dg(1, 64 << 20) == 64
+    assert dg(1, 32 * G) == 1
     assert dg(0, G) == 1
 
 
