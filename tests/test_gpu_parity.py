@@ -434,6 +434,43 @@ def test_digest_spans_all_lengths(ca, O):
             assert bytes(dig[k]) == want, (algo, n, a)
 
 
+@pytest.mark.parametrize("fused,occ", [(1, 2), (1, 4), (0, 2), (1, 1)], ids=["fused_2cu", "fused_4cu", "pair_2cu",
+                                                                          "fused_1cu"])
+def test_sha_fill_launch_fused_tier(ca, fused, occ):
+    """A GPU-filling SHA-256 launch (40,000 spans: sha256_grid's fill tiers) with its
+    one-lane tier fused (sha_fused: one wave per 64 chunks, schedule in registers, no LDS)
+    or on the producer/consumer pair, at 1-4 workgroups per CU: every digest equals
+    hashlib's, for span lengths 0..5,000 at random unaligned offsets plus the padding
+    boundaries; the launch's one-lane workgroups hold 128 chunks when fused."""
+    import torch
+
+    rng = np.random.default_rng(77)
+    data = rng.integers(0, 256, 8 << 20, dtype=np.uint8)
+    n = 40_000
+    lens = rng.integers(0, 5001, n)
+    lens[:130] = np.arange(130)
+    lens[130:140] = [55, 56, 57, 63, 64, 65, 119, 120, 121, 128]
+    offs = np.array([int(rng.integers(0, len(data) - int(m) + 1)) for m in lens], np.int64)
+    d = torch.from_numpy(data).cuda()
+    o = torch.from_numpy(offs).cuda()
+    ln = torch.from_numpy(lens.astype(np.int64)).cuda()
+    old_f = ca.lib.cg_test_sha_fused(fused)
+    old_o = ca.lib.cg_test_sha_occupancy(1, occ)
+    try:
+        dig = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
+        assert ca.lib.cg_hash_spans_device(d.data_ptr(), o.data_ptr(), ln.data_ptr(), n, SHA, dig.data_ptr(), None) == 0
+        tiers = (ctypes.c_uint32 * 4)()
+        ca.lib.cg_last_sha_tiers(tiers)
+    finally:
+        ca.lib.cg_test_sha_fused(old_f)
+        ca.lib.cg_test_sha_occupancy(1, old_o)
+    nq, npair, nlane = int(tiers[0]), int(tiers[1]), int(tiers[2])
+    assert nlane * (128 if fused else 64) >= n - 8 * nq - 32 * npair > nlane * (128 if fused else 64) - (128 if fused else 64)
+    dig = dig.cpu().numpy().reshape(-1, 32)
+    bad = [k for k in range(n) if bytes(dig[k]) != hashlib.sha256(data[offs[k]:offs[k] + lens[k]].tobytes()).digest()]
+    assert not bad, (len(bad), bad[:8], [int(lens[k]) for k in bad[:8]])
+
+
 def _sha_kinds(ca, quad_max, pair_max):
     """Cap the quad and pair workgroups of the SHA-256 launch; returns the old caps."""
     return ca.lib.cg_test_sha_quad_max(quad_max), ca.lib.cg_test_sha_split_max(pair_max)
