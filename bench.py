@@ -94,8 +94,6 @@ def parse_args():
     ap.add_argument("--sha-occ", default="",
                     help="SHA-256 workgroups per CU 'LATENCY,FILL' for launches with more workgroups than CUs "
                          "(cg_test_sha_occupancy; '' = the library's)")
-    ap.add_argument("--sha-fused", type=int, default=-1, choices=(-1, 0, 1),
-                    help="fused one-lane SHA-256 tier in GPU-filling launches (cg_test_sha_fused; -1 = the library's)")
     ap.add_argument("--no-stage-profile", action="store_true",
                     help="skip the per-stage single steps (so a kernel trace holds only the pipeline's launches)")
     ap.add_argument("--no-clock", action="store_true", help="skip the digest clock measurement (scripts/sha_clock.py)")
@@ -150,6 +148,13 @@ def timed_group(lib_default: int, steps: int) -> int:
     return min(divs, key=lambda g: (abs(g - lib_default), -g))
 
 
+def peek_hook(hook, *which) -> int:
+    """The current setting of a set-and-return-previous test hook, left unchanged."""
+    old = int(hook(*which, 1))
+    hook(*which, old)
+    return old
+
+
 def launch_ranks(n: int) -> int:
     """Start n ranks as one child torchrun process (127.0.0.1 rendezvous) and return
     its exit code.  Nothing here initialises HIP: the GPUs belong to the children."""
@@ -201,8 +206,6 @@ def main():
     if args.no_coalesce:
         ca.lib.cg_test_coalesce(0)
     ca.lib.cg_test_split_mode(args.split_mode)
-    if args.sha_fused >= 0:
-        ca.lib.cg_test_sha_fused(args.sha_fused)
     if args.sha_occ:
         lat_occ, fill_occ = (int(v) for v in args.sha_occ.split(","))
         ca.lib.cg_test_sha_occupancy(0, lat_occ)
@@ -558,9 +561,7 @@ def main():
                          "per-batch streams (cg_chunk_batch_device_async_after)",
                          "group": group, "lanes": lanes if group else None, "depth": depth,
                          "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "4 (HIP default)"),
-                         "sha_wgs_per_cu": [int(ca.lib.cg_test_sha_occupancy(k, ca.lib.cg_test_sha_occupancy(k, 1)))
-                                            for k in (0, 1)],
-                         "sha_fused_fill": int(ca.lib.cg_test_sha_fused(ca.lib.cg_test_sha_fused(1))),
+                         "sha_wgs_per_cu": [peek_hook(ca.lib.cg_test_sha_occupancy, k) for k in (0, 1)],
                          "fill_ms": round(fill_ms, 2), "settle_steps": settled[0], "settle_ms": round(settle_ms, 2),
                          "settle_GiBps": round(settled[0] * total_bytes * world / (settle_ms * 1e-3) / GIB, 3),
                          "drain_ms": round(drain_ms, 2),

@@ -57,7 +57,7 @@ TEST_HOOKS = ("cg_test_sha_quad_max", "cg_test_sha_split_max", "cg_test_sha_spin
               "cg_test_stream_group_cap", "cg_test_stream_max_lanes", "cg_test_stream_eager",
               "cg_test_b3_fused_plan", "cg_test_b3_packed", "cg_coalesce_stats",
               "cg_test_split_mode", "cg_test_sha_tiers", "cg_test_sha_tiers_fill", "cg_hw_queues",
-              "cg_test_sha_occupancy", "cg_test_sha_fused")
+              "cg_test_sha_occupancy")
 
 
 def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
@@ -189,10 +189,9 @@ def _load(path: Path = LIB_PATH) -> ctypes.CDLL:
         if hasattr(L, name):
             getattr(L, name).argtypes = [i]
             getattr(L, name).restype = i
-    L.cg_test_sha_fused.argtypes = [u32]
-    L.cg_test_sha_fused.restype = u32
-    L.cg_test_sha_occupancy.argtypes = [u32, u32]
-    L.cg_test_sha_occupancy.restype = u32
+    if hasattr(L, "cg_test_sha_occupancy"):
+        L.cg_test_sha_occupancy.argtypes = [u32, u32]
+        L.cg_test_sha_occupancy.restype = u32
     L.cg_hw_queues.argtypes = []
     L.cg_hw_queues.restype = i
     L.cg_test_split_mode.argtypes = [i]

@@ -724,102 +724,11 @@ __device__ __forceinline__ void sha_diag_consumer(unsigned long long *diag, unsi
     diag[8 * blockIdx.x + 6] = wave_location();
 }
 
-// ---------------------------------------------------------------------------
-// Fused one-lane tier (round 6, GPU-filling launches only).  In a launch that fills the
-// chip the one-lane chunks are throughput work, not chains anyone waits for, and the
-// producer/consumer split costs throughput: the consumer's SIMD issues its 896 VALU per
-// block while the producer's SIMD sits ~35 % idle, and the 68 KiB ring holds a CU to two
-// workgroups (k_sha256 at ~58 % of the VALU issue peak on config 4, SQ_WAIT_ANY 21 % of
-// wave cycles, profiles/r06_v9_pmc_c4_prod.json).  Here ONE wave owns 64 chunks and does
-// everything -- dword loads realigned by v_perm_b32, padding, the message schedule in a
-// rolling 16-word register window, the 64 rounds -- with no LDS at all, so a one-lane
-// workgroup is two independent waves (128 chunks), every SIMD it lands on issues only
-// VALU work, and the launch needs the ring only for its quad / pair workgroups (34 KiB:
-// four workgroups per CU).  ~1,410 VALU per block on one SIMD against 896 + ~580 on two.
-// A chain runs ~1.6x longer per round than on the consumer/producer pair, which is why
-// latency-bound launches keep the pair.
-// ---------------------------------------------------------------------------
-#define SHA_RNDK(a, b, c, d, e, f, g, h, wt, kt)                                \
-    {                                                                           \
-        const uint32_t t1 = add3(add3(h, (wt), (kt)), ch(e, f, g), SHA_S1(e)); \
-        d += t1;                                                                \
-        h = add3(t1, SHA_S0(a), maj(a, b, c));                                  \
-    }
-// schedule word t (t >= 16) into w[t & 15]
-#define SHA_WNEXT(t) \
-    w[(t) & 15] = add3(w[(t) & 15], SHA_s0(w[((t) - 15) & 15]), w[((t) - 7) & 15]) + SHA_s1(w[((t) - 2) & 15])
-#define SHA_F8(i)                                                                       \
-    {                                                                                   \
-        if ((i) >= 16) {                                                                \
-            SHA_WNEXT((i) + 0);                                                         \
-        }                                                                               \
-        SHA_RNDK(a, b, c, d, e, f, g, h, w[((i) + 0) & 15], SHA_K[(i) + 0]);            \
-        if ((i) >= 16) SHA_WNEXT((i) + 1);                                              \
-        SHA_RNDK(h, a, b, c, d, e, f, g, w[((i) + 1) & 15], SHA_K[(i) + 1]);            \
-        if ((i) >= 16) SHA_WNEXT((i) + 2);                                              \
-        SHA_RNDK(g, h, a, b, c, d, e, f, w[((i) + 2) & 15], SHA_K[(i) + 2]);            \
-        if ((i) >= 16) SHA_WNEXT((i) + 3);                                              \
-        SHA_RNDK(f, g, h, a, b, c, d, e, w[((i) + 3) & 15], SHA_K[(i) + 3]);            \
-        if ((i) >= 16) SHA_WNEXT((i) + 4);                                              \
-        SHA_RNDK(e, f, g, h, a, b, c, d, w[((i) + 4) & 15], SHA_K[(i) + 4]);            \
-        if ((i) >= 16) SHA_WNEXT((i) + 5);                                              \
-        SHA_RNDK(d, e, f, g, h, a, b, c, w[((i) + 5) & 15], SHA_K[(i) + 5]);            \
-        if ((i) >= 16) SHA_WNEXT((i) + 6);                                              \
-        SHA_RNDK(c, d, e, f, g, h, a, b, w[((i) + 6) & 15], SHA_K[(i) + 6]);            \
-        if ((i) >= 16) SHA_WNEXT((i) + 7);                                              \
-        SHA_RNDK(b, c, d, e, f, g, h, a, w[((i) + 7) & 15], SHA_K[(i) + 7]);            \
-    }
-
-// The chunk of `len` bytes at p on this lane (nbt blocks with padding; NB = the wave's
-// most): lanes past their last block compute on stale words and keep their state by
-// select, so the rounds always run under a full exec mask.
-__device__ __forceinline__ void sha_fused(const uint8_t *p, uint64_t len, uint32_t nbt, uint32_t NB, uint32_t st[8]) {
-    const uint64_t nb = len >> 6;
-    const uint32_t shift = (uint32_t)((uintptr_t)p & 3u);
-    const uint32_t *base = reinterpret_cast<const uint32_t *>(p - shift);
-    const uint32_t sel = perm_sel(shift);
-    uint32_t dw[17];
-    auto load_full = [&](uint64_t k) {
-        const uint32_t *q = base + 16 * k;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) dw[i] = q[i];
-        dw[16] = q[shift ? 16 : 15];  // (shift == 0: re-read in the block; the realign ignores it)
-    };
-    if (nb > 0) load_full(0);
-    uint32_t w[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) w[i] = 0u;
-    for (uint32_t k = 0; k < NB; ++k) {
-        if (k < nb) {
-#pragma unroll
-            for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_perm(dw[i + 1], dw[i], sel);
-            // block k + 1's bytes are requested now and land under this block's rounds
-            __builtin_amdgcn_sched_barrier(0);
-            load_full(k + 1 < nb ? k + 1 : k);
-        } else if (k < nbt) {
-            sha_pad_words(w, p, base, sel, len, k);
-        }
-        uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
-        SHA_F8(0)
-        SHA_F8(8)
-        SHA_F8(16)
-        SHA_F8(24)
-        SHA_F8(32)
-        SHA_F8(40)
-        SHA_F8(48)
-        SHA_F8(56)
-        const bool active = k < nbt;
-        st[0] = active ? st[0] + a : st[0];
-        st[1] = active ? st[1] + b : st[1];
-        st[2] = active ? st[2] + c : st[2];
-        st[3] = active ? st[3] + d : st[3];
-        st[4] = active ? st[4] + e : st[4];
-        st[5] = active ? st[5] + f : st[5];
-        st[6] = active ? st[6] + g : st[6];
-        st[7] = active ? st[7] + h : st[7];
-    }
-}
-
+// Any change to this kernel's source -- even code on a path config 2 never takes -- moves
+// the register allocation and scheduling of the pinned round code: measure config 2's
+// merged launch against the previous build on the same box (round 6: a fused one-lane
+// tier for GPU-filling launches made config 2's launches 69.4 -> 79-94 ms and lost on
+// config 4 too; removed).
 // Workgroup kinds, longest chunks first (the length order): [0, nquad) take 8 chunks
 // on 8 lanes each, [nquad, nquad + npair) 32 chunks on lane pairs, the rest 64
 // chunks on one lane each.  The quad and pair kinds share the pair producer.
@@ -835,7 +744,7 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
                                                unsigned long long *__restrict__ diag, uint32_t mode,
                                                uint32_t nquad, uint32_t npair, uint32_t spin_limit,
                                                uint32_t *__restrict__ err, const uint32_t *__restrict__ need,
-                                               ShaNotify nt, uint32_t fused) {
+                                               ShaNotify nt) {
     unsigned long long t_start = diag ? __builtin_amdgcn_s_memtime() : 0ull, t_spin = 0;
     const unsigned long long rt_start = diag ? __builtin_amdgcn_s_memrealtime() : 0ull;
     if (need) {  // latency tiers (k_len_base): no more lanes per chunk than its length needs
@@ -845,8 +754,7 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
         const uint32_t np = (rest + 31u) / 32u;
         if (np < npair) npair = np;
     }
-    // the ring is dynamic LDS: PC_LDS_WORDS, or only the split tiers' slots in a fused launch
-    extern __shared__ __attribute__((aligned(16))) uint32_t sLDS[];
+    __shared__ __attribute__((aligned(16))) uint32_t sLDS[PC_LDS_WORDS];
     uint32_t(*sW)[ONE_SLOT] = reinterpret_cast<uint32_t(*)[ONE_SLOT]>(sLDS);     // one-lane view
     uint32_t(*sWs)[SPL_SLOT] = reinterpret_cast<uint32_t(*)[SPL_SLOT]>(sLDS);    // split view
     // hand-off words (SY_*): blocks filled by the producer / consumed by the consumer,
@@ -858,17 +766,15 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
     const uint32_t b = blockIdx.x;
     const bool quad = b < nquad;
     const bool split = b < nquad + npair;  // quad or pair
-    const bool fu = fused && !split;       // fused one-lane workgroup: two waves of 64 chunks
     const uint64_t wg_base = quad    ? 8ull * b
                              : split ? 8ull * nquad + 32ull * (b - nquad)
-                                     : 8ull * nquad + 32ull * npair + (fu ? 128ull : 64ull) * (b - nquad - npair);
-    const uint32_t wg_chunks = quad ? 8u : split ? 32u : fu ? 128u : 64u;
+                                     : 8ull * nquad + 32ull * npair + 64ull * (b - nquad - npair);
+    const uint32_t wg_chunks = quad ? 8u : split ? 32u : 64u;
     const bool hi = split && ((lane >> 2) & 1u);
     // the producer of a quad or pair workgroup pairs lanes as split_slot does (a quad
     // workgroup uses its first 16 lanes); a quad consumer gives chunk j lanes
     // 16r + 8h + 0..7 with j = 2r + h
-    const uint32_t slot = fu ? (uint32_t)threadIdx.x
-                          : !split ? lane
+    const uint32_t slot = !split ? lane
                           : (quad && !producer) ? (((lane >> 4) << 1) | ((lane >> 3) & 1u))
                                                 : split_slot(lane);
     const uint32_t row = split ? split_row(slot) : lane;
@@ -896,19 +802,7 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
     // blocks every valid lane's chunk has (the consumers' select-free main loop)
     const uint32_t NBmin = __builtin_amdgcn_readfirstlane(~wave_max_u32(valid ? ~nbt : 0u));
 
-    if (fu) {
-        uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
-                          0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
-        sha_fused(data + (valid ? abs[ci] : 0), len, nbt, NB, st);
-        if (valid) {
-            uint4 *o = reinterpret_cast<uint4 *>(nt.dst ? reinterpret_cast<uint8_t *>(nt.dst[ci]) : hash_base + ci * stride);
-            o[0] = make_uint4(__builtin_bswap32(st[0]), __builtin_bswap32(st[1]), __builtin_bswap32(st[2]),
-                              __builtin_bswap32(st[3]));
-            o[1] = make_uint4(__builtin_bswap32(st[4]), __builtin_bswap32(st[5]), __builtin_bswap32(st[6]),
-                              __builtin_bswap32(st[7]));
-            if (nt.remain) __threadfence();  // visible device-wide before the member is counted down
-        }
-    } else if (producer) {
+    if (producer) {
         const uint8_t *p = data + (valid ? abs[ci] : 0);
         if (mode == 1) {  // diag: no producer work, consumer rounds on stale schedules
             if (lane == 0) lds_store_release(&s_ready, 0xffffffffu);
@@ -989,7 +883,7 @@ __global__ __launch_bounds__(128) void k_sha256(const uint8_t *__restrict__ data
     // own lane, a split chunk's hi lane that stored H0..H3 -- counts its member down once
     // every digest of this workgroup is stored and fenced; the last one out raises the
     // member's host-mapped completion word (system scope, vector store)
-    if (nt.remain && (fu || !producer) && valid && (!split || (hi && (!quad || (lane & 3u) == 0)))) {
+    if (nt.remain && !producer && valid && (!split || (hi && (!quad || (lane & 3u) == 0)))) {
         const uint32_t m = nt.member[ci];
         if (timed_out) __hip_atomic_fetch_or(&nt.merr[m], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (__hip_atomic_fetch_sub(&nt.remain[m], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == 1u) {
@@ -1156,12 +1050,8 @@ uint32_t g_sha_spin_limit = 1u << 26;
 // LDS for 8 chunks, so up to 256 quads are used only when the one-lane tier left
 // behind them fits in one round of workgroups (<= 256 x 64 chunks); on a batch that
 // fills the GPU (config 4) only g_sha_quad_fill of them, for the longest chunks.
-// GPU-filling launches run their one-lane tier fused (sha_fused, 128 chunks per
-// workgroup): test hook cg_test_sha_fused (0 = the producer/consumer pair everywhere).
-uint32_t g_sha_fused = 1;
-
 uint32_t sha256_grid(uint64_t max_chunks, uint64_t expected, uint32_t *nquad_out, uint32_t *npair_out,
-                     bool *fill_out, bool *fused_out = nullptr) {
+                     bool *fill_out) {
     auto tiers = [&](uint64_t qmax, uint64_t pmax, uint64_t &nq, uint64_t &np) {
         nq = (max_chunks + 7) / 8;
         if (nq > qmax) nq = qmax;
@@ -1177,20 +1067,17 @@ uint32_t sha256_grid(uint64_t max_chunks, uint64_t expected, uint32_t *nquad_out
         tiers(std::min<uint64_t>(g_sha_quad_max, g_sha_quad_fill), std::min<uint64_t>(g_sha_split_max, g_sha_pair_fill),
               nq, np);
     const uint64_t rest = max_chunks > 8 * nq + 32 * np ? max_chunks - 8 * nq - 32 * np : 0;
-    const bool fused = fill && g_sha_fused;
     if (nquad_out) *nquad_out = (uint32_t)nq;
     if (npair_out) *npair_out = (uint32_t)np;
-    if (fused_out) *fused_out = fused;
-    const uint64_t per = fused ? 128 : 64;
-    return (uint32_t)(nq + np + (rest + per - 1) / per);
+    return (uint32_t)(nq + np + (rest + 63) / 64);
 }
 
 // Workgroups per CU of a launch with more workgroups than CUs: [0] latency-bound (the
 // chip mostly idle but for the chains: merged pipeline groups), [1] GPU-filling (config 4 /
-// 5 shapes).  Two: the 4-slot ring (68 KiB) admits no more, and a fused fill launch (34 KiB
-// ring) measured slower at 3 / 4 (config 4 714 -> 625 / 589 GiB/s, profiles/r06_v10_*):
-// its quad and pair chains then share their SIMDs.  CHUNKER_AMD_SHA_OCC="latency,fill"
-// (read once; A/B) or cg_test_sha_occupancy.
+// 5 shapes).  Two: the 4-slot ring (68 KiB) admits no more; a 2- or 3-slot ring at 3-4
+// per CU measured equal on config 4 and slower on configs 2 / 5 (DESIGN.md §4 round 6,
+// profiles/r06_v8_ring_occupancy.txt).  CHUNKER_AMD_SHA_OCC="latency,fill" (read once;
+// A/B) or cg_test_sha_occupancy.
 uint32_t g_sha_occ[2] = {0, 0};
 static uint32_t sha_wgs_per_cu(bool fill) {
     static const bool init = [] {
@@ -1204,10 +1091,10 @@ static uint32_t sha_wgs_per_cu(bool fill) {
     return g_sha_occ[fill ? 1 : 0];
 }
 // Dynamic LDS that holds a CU to `n` workgroups: past 160 KiB / (n + 1) in all.
-static size_t lds_pad_for(uint32_t n, size_t ring) {
-    const size_t used = ring + 64;  // (+ the hand-off words)
+static size_t lds_pad_for(uint32_t n) {
+    constexpr size_t ring_bytes = PC_LDS_WORDS * 4 + 64;  // (+ the hand-off words)
     const size_t want = 163840 / (n + 1) + 1024;
-    return want > used ? want - used : 0;
+    return want > ring_bytes ? want - ring_bytes : 0;
 }
 
 // Shape of this thread's last digest launch (cg_last_sha_tiers): quad, pair and
@@ -1220,8 +1107,8 @@ void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
                    bool latency_tiers, const ShaNotify *notify) {
     if (max_chunks == 0) return;
     uint32_t nquad = 0, npair = 0;
-    bool fill = false, fused = false;
-    const uint32_t nwg = sha256_grid(max_chunks, expected, &nquad, &npair, &fill, &fused);
+    bool fill = false;
+    const uint32_t nwg = sha256_grid(max_chunks, expected, &nquad, &npair, &fill);
     // one workgroup has nothing to balance
     // latency tiers: k_len_base counts the chunks that need a quad / a pair into the two
     // words after the order (sha256_order_tmp_elems' slack)
@@ -1236,17 +1123,15 @@ void launch_sha256(const uint8_t *d_data, const uint64_t *d_abs, const void *d_d
     // launches: at most sha_wgs_per_cu(fill) workgroups per CU (the ring's 34 KiB alone
     // lets four in: two waves per SIMD).
     const uint32_t per_cu = nwg <= 256 ? 1u : sha_wgs_per_cu(fill);
-    // (a fused launch's ring serves its quad / pair workgroups only)
-    const size_t ring = fused ? (size_t)PC_RING * SPL_SLOT * 4 : (size_t)PC_LDS_WORDS * 4;
-    const size_t pad = lds_pad_for(per_cu, ring);
+    const size_t pad = lds_pad_for(per_cu);
     t_sha_tiers[0] = nquad;
     t_sha_tiers[1] = npair;
     t_sha_tiers[2] = nwg - nquad - npair;
     t_sha_tiers[3] = (uint32_t)pad;
-    hipLaunchKernelGGL(k_sha256, dim3(nwg), dim3(128), ring + pad, st, d_data, d_abs,
+    hipLaunchKernelGGL(k_sha256, dim3(nwg), dim3(128), pad, st, d_data, d_abs,
                        (const DescRaw *)d_desc, d_total, max_chunks, order, d_hash_base, hash_stride, g_sha_diag,
                        g_sha_mode, nquad, npair, g_sha_spin_limit, d_err, order ? need : nullptr,
-                       notify ? *notify : ShaNotify{}, fused ? 1u : 0u);
+                       notify ? *notify : ShaNotify{});
 }
 
 // ---------------------------------------------------------------------------
@@ -1542,14 +1427,6 @@ static uint32_t set_sha_tiers(int k, uint32_t quad_pm, uint32_t pair_pm) {
 extern "C" uint32_t cg_test_sha_tiers(uint32_t quad_pm, uint32_t pair_pm) { return set_sha_tiers(0, quad_pm, pair_pm); }
 extern "C" uint32_t cg_test_sha_tiers_fill(uint32_t quad_pm, uint32_t pair_pm) {
     return set_sha_tiers(1, quad_pm, pair_pm);
-}
-
-// Test hook: the fused one-lane tier of GPU-filling launches on (1) / off (0); returns the
-// previous setting.
-extern "C" uint32_t cg_test_sha_fused(uint32_t v) {
-    const uint32_t old = cg::g_sha_fused;
-    cg::g_sha_fused = v ? 1u : 0u;
-    return old;
 }
 
 // Test hook: workgroups per CU of latency-bound (which = 0) / GPU-filling (1) launches with

@@ -434,14 +434,13 @@ def test_digest_spans_all_lengths(ca, O):
             assert bytes(dig[k]) == want, (algo, n, a)
 
 
-@pytest.mark.parametrize("fused,occ", [(1, 2), (1, 4), (0, 2), (1, 1)], ids=["fused_2cu", "fused_4cu", "pair_2cu",
-                                                                          "fused_1cu"])
-def test_sha_fill_launch_fused_tier(ca, fused, occ):
-    """A GPU-filling SHA-256 launch (40,000 spans: sha256_grid's fill tiers) with its
-    one-lane tier fused (sha_fused: one wave per 64 chunks, schedule in registers, no LDS)
-    or on the producer/consumer pair, at 1-4 workgroups per CU: every digest equals
-    hashlib's, for span lengths 0..5,000 at random unaligned offsets plus the padding
-    boundaries; the launch's one-lane workgroups hold 128 chunks when fused."""
+@pytest.mark.parametrize("occ", [1, 2, 4])
+def test_sha_fill_launch_occupancy(ca, occ):
+    """A GPU-filling SHA-256 launch (40,000 spans: sha256_grid's fill tiers) at 1-4
+    workgroups per CU (cg_test_sha_occupancy; the LDS pad that enforces it): every digest
+    equals hashlib's, for span lengths 0..5,000 at random unaligned offsets plus the
+    padding boundaries; the launch's one-lane workgroups cover the chunks the quad and pair
+    tiers leave, 64 each."""
     import torch
 
     rng = np.random.default_rng(77)
@@ -454,7 +453,6 @@ def test_sha_fill_launch_fused_tier(ca, fused, occ):
     d = torch.from_numpy(data).cuda()
     o = torch.from_numpy(offs).cuda()
     ln = torch.from_numpy(lens.astype(np.int64)).cuda()
-    old_f = ca.lib.cg_test_sha_fused(fused)
     old_o = ca.lib.cg_test_sha_occupancy(1, occ)
     try:
         dig = torch.zeros(n * 32, dtype=torch.uint8, device="cuda")
@@ -462,10 +460,9 @@ def test_sha_fill_launch_fused_tier(ca, fused, occ):
         tiers = (ctypes.c_uint32 * 4)()
         ca.lib.cg_last_sha_tiers(tiers)
     finally:
-        ca.lib.cg_test_sha_fused(old_f)
         ca.lib.cg_test_sha_occupancy(1, old_o)
     nq, npair, nlane = int(tiers[0]), int(tiers[1]), int(tiers[2])
-    assert nlane * (128 if fused else 64) >= n - 8 * nq - 32 * npair > nlane * (128 if fused else 64) - (128 if fused else 64)
+    assert nlane * 64 >= n - 8 * nq - 32 * npair > nlane * 64 - 64
     dig = dig.cpu().numpy().reshape(-1, 32)
     bad = [k for k in range(n) if bytes(dig[k]) != hashlib.sha256(data[offs[k]:offs[k] + lens[k]].tobytes()).digest()]
     assert not bad, (len(bad), bad[:8], [int(lens[k]) for k in bad[:8]])
