@@ -324,6 +324,93 @@ __device__ __forceinline__ void b3_leaf(const uint8_t *p, uint32_t n, uint64_t c
     }
 }
 
+#ifndef CG_B3_LDS_REALIGN
+#define CG_B3_LDS_REALIGN 0
+#endif
+#if CG_B3_LDS_REALIGN
+// Leaf with every load a whole 64-byte-aligned segment (A/B, round 6).
+// b3_leaf reads each block pair from the leaf's own (unaligned) address, so a 128-byte line
+// is read twice -- by the pair that ends in it and the next one, and the leaf's last line by
+// the right neighbour's first pair ~16 compressions earlier -- and by then L2 has often
+// dropped it (1.40x the batch's bytes, profiles/r05_v10_pmc_c3.json).  Here segment k of the
+// leaf's aligned span is loaded once, two blocks ahead, into a per-lane LDS ring of 48 dwords
+// (segments j and j + 1 at 0 / 16 for even j, 16 / 32 for odd j: the even slot is mirrored at
+// 32 so a block's 17 dwords never wrap), and block j is read back at the lane's dword offset
+// with constant-offset LDS reads, then realigned by byte as before.
+#define B3_RING 52u  // dwords per lane: 48 + 4 pad (8 consecutive lanes' b128 stores on distinct banks)
+__device__ __forceinline__ void b3_leaf_lds(const uint8_t *p, uint32_t n, uint64_t ctr, bool root, uint32_t cv[8],
+                                            uint32_t *ring) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) cv[i] = B3_IV[i];
+    const uint32_t off = (uint32_t)((uintptr_t)p & 63u);
+    const uint32_t shift = off & 3u;
+    const uint4 *seg0 = reinterpret_cast<const uint4 *>(p - off);
+    const uint32_t nblk = n ? (n + 63) / 64 : 1;
+    const uint32_t nfull = n / 64;
+    const uint32_t last_seg = (off + (n ? n : 1u) - 1u) >> 6;  // the last segment holding leaf bytes
+    uint32_t *rl = ring + (off >> 2);                           // this lane's block reads start here
+    uint4 r0, r1, r2, r3;  // the segment in flight (four named registers: an array went to scratch)
+    auto load_seg = [&](uint32_t k) {  // past the leaf: re-read its last segment (never read)
+        const uint4 *q = seg0 + 4 * (k < last_seg ? k : last_seg);
+        r0 = q[0];
+        r1 = q[1];
+        r2 = q[2];
+        r3 = q[3];
+    };
+    auto store_seg = [&](uint32_t at) {
+        uint4 *d = reinterpret_cast<uint4 *>(ring + at);
+        d[0] = r0;
+        d[1] = r1;
+        d[2] = r2;
+        d[3] = r3;
+    };
+    auto flags_of = [&](uint32_t j) {
+        const bool last = j + 1 == nblk;
+        return (j == 0 ? B3_CHUNK_START : 0u) | (last ? B3_CHUNK_END : 0u) | (root && last ? B3_ROOT : 0u);
+    };
+    load_seg(0);
+    store_seg(0);
+    store_seg(32);
+    load_seg(1);
+    store_seg(16);
+    load_seg(2);
+    // one block: its 17 dwords from the ring at `base` (0: even j, 16: odd j); segment j's
+    // slot then takes segment j + 2 (already in r) and segment j + 3 is requested
+    auto block = [&](uint32_t j, uint32_t base, bool full) {
+        uint32_t dw[17], m[16];
+#pragma unroll
+        for (int i = 0; i < 17; ++i) dw[i] = rl[base + i];
+        const uint32_t blen = full ? 64u : n - 64 * j;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t v = __builtin_amdgcn_alignbyte(dw[i + 1], dw[i], shift);
+            if (full) {
+                m[i] = v;
+            } else {
+                const int rr = (int)blen - 4 * i;
+                m[i] = rr >= 4 ? v : (rr <= 0 ? 0u : (v & (0xffffffffu >> (32 - 8 * rr))));
+            }
+        }
+        store_seg(base);
+        if (base == 0) store_seg(32);
+        load_seg(j + 3);
+        __builtin_amdgcn_sched_barrier(0);  // the next segment's load is issued before the compression
+        b3_compress(cv, m, ctr, blen, flags_of(j));
+    };
+    uint32_t j = 0;
+#pragma unroll 1
+    for (; j + 1 < nfull; j += 2) {
+        block(j, 0, true);
+        block(j + 1, 16, true);
+    }
+    if (j < nfull) {
+        block(j, 0, true);
+        ++j;
+    }
+    if (j < nblk) block(j, (j & 1u) ? 16u : 0u, false);  // the partial last block (or n == 0)
+}
+#endif
+
 // Leaves per lane in k_b3_groups: a lane hashes B3_LPL consecutive leaves and folds
 // them itself (full exec mask), so a wave covers a 64 x B3_LPL-leaf subtree and its
 // shuffle fold (6 levels, one wave-wide compression each, mostly idle lanes) is paid
@@ -571,7 +658,12 @@ __global__ __launch_bounds__(64 * B3_WAVES) void k_b3_leaves(const uint8_t *__re
     const uint64_t off = l * 1024;
     const uint32_t n = len ? (uint32_t)((len - off) < 1024 ? (len - off) : 1024) : 0u;
     uint32_t cv[8];
+#if CG_B3_LDS_REALIGN
+    __shared__ __attribute__((aligned(16))) uint32_t s_ring[B3_WAVES * 64 * B3_RING];
+    b3_leaf_lds(data + abs[c] + off, n, l, leaves == 1, cv, s_ring + (threadIdx.x * B3_RING));
+#else
     b3_leaf<false>(data + abs[c] + off, n, l, leaves == 1, cv);
+#endif
     if (leaves == 1) {
         store_digest(hash_base + c * stride, cv);
     } else {

@@ -166,8 +166,9 @@ pub fn available() -> bool {
 pub const BLAKE3: i32 = 0;
 pub const SHA256: i32 = 1;
 
-/// Dispatch rule (measured by bench.py's drop_in leg): BLAKE3 pays on the
-/// GPU from one 10 MiB call on (29 vs 2.9 GiB/s); a SHA-256 call lasts its longest chunk's
+/// Dispatch rule for single synchronous calls (measured by bench.py's
+/// drop_in leg): BLAKE3 pays on the GPU from one 10 MiB call on (24-29 vs 2.0-2.9 GiB/s); a
+/// SHA-256 call lasts its longest chunk's
 /// serial chain (~30-90 ms), so it pays only for large inputs (1 GiB: 11.3 vs 4.9 GiB/s;
 /// 256 MiB: even).  Smaller SHA-256 calls stay on the reference's CPU path.
 pub const SHA256_SINGLE_CALL_MIN: usize = 512 << 20;
@@ -283,9 +284,11 @@ impl Drop for BatchInFlight {
 /// SHA-256 digests of `group` consecutive batches merged into one launch on one of `lanes`
 /// digest streams, each batch handed back when its own chunks are digested.  Replaces,
 /// across the worker's consecutive chunk_descriptors_with_hash calls, the collect-then-hash
-/// sequence of src/chunking.rs:334-368.  Measured: config 2 (1 GiB batches
-/// of 256 x 4 MiB NARs) at group 24, 2 lanes, 72 in flight: 665 GiB/s at HIP's default 4
-/// hardware queues.  `group` 0 / `lanes` 0 = the engine's defaults (16 / 2).
+/// sequence of src/chunking.rs:334-368.  Measured (DESIGN.md §7 "The digest pipeline"):
+/// config 2 (1 GiB batches of 256 x 4 MiB NARs) at group 20-24, 2 lanes, 60-72 in flight:
+/// 580-666 GiB/s at HIP's default 4 hardware queues on the faster boxes, 453-525 on the
+/// slower ones.  Keep (lanes + 1) x group batches in flight.  `group` 0 / `lanes` 0 = the
+/// engine's defaults (16 / 2).
 pub struct Pipeline(NonNull<CgPipeline>);
 unsafe impl Send for Pipeline {}
 impl Pipeline {
