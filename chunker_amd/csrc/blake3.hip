@@ -325,10 +325,11 @@ __device__ __forceinline__ void b3_leaf(const uint8_t *p, uint32_t n, uint64_t c
 }
 
 #ifndef CG_B3_LDS_REALIGN
-#define CG_B3_LDS_REALIGN 0
+#define CG_B3_LDS_REALIGN 1
 #endif
 #if CG_B3_LDS_REALIGN
-// Leaf with every load a whole 64-byte-aligned segment (A/B, round 6).
+// Leaf with every load a whole 64-byte-aligned segment (k_b3_leaves, the product since round
+// 6; CG_B3_LDS_REALIGN=0 builds the round-5 b3_leaf loads there).
 // b3_leaf reads each block pair from the leaf's own (unaligned) address, so a 128-byte line
 // is read twice -- by the pair that ends in it and the next one, and the leaf's last line by
 // the right neighbour's first pair ~16 compressions earlier -- and by then L2 has often
@@ -336,7 +337,11 @@ __device__ __forceinline__ void b3_leaf(const uint8_t *p, uint32_t n, uint64_t c
 // leaf's aligned span is loaded once, two blocks ahead, into a per-lane LDS ring of 48 dwords
 // (segments j and j + 1 at 0 / 16 for even j, 16 / 32 for odd j: the even slot is mirrored at
 // 32 so a block's 17 dwords never wrap), and block j is read back at the lane's dword offset
-// with constant-offset LDS reads, then realigned by byte as before.
+// with constant-offset LDS reads, then realigned by byte as before.  Measured on config 3
+// (profiles/r06_v18_b3_lds_realign_ab.txt): fetched 1.41x -> 1.22x the batch (what is left:
+// the leaf's last 128-byte line, which the right neighbour's lane read ~16 compressions
+// earlier), kernel time equal (0.406 / 0.410 ms): the kernel is VALU-issue bound.  53 KiB
+// of LDS per 4-wave workgroup: 3 waves per SIMD instead of 4, no loss at this issue rate.
 #define B3_RING 52u  // dwords per lane: 48 + 4 pad (8 consecutive lanes' b128 stores on distinct banks)
 __device__ __forceinline__ void b3_leaf_lds(const uint8_t *p, uint32_t n, uint64_t ctr, bool root, uint32_t cv[8],
                                             uint32_t *ring) {
