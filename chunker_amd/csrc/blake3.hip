@@ -327,6 +327,9 @@ __device__ __forceinline__ void b3_leaf(const uint8_t *p, uint32_t n, uint64_t c
 #ifndef CG_B3_LDS_REALIGN
 #define CG_B3_LDS_REALIGN 1
 #endif
+#ifndef CG_B3_HOLD_TAIL
+#define CG_B3_HOLD_TAIL 1
+#endif
 #if CG_B3_LDS_REALIGN
 // Leaf with every load a whole 64-byte-aligned segment (k_b3_leaves, the product since round
 // 6; CG_B3_LDS_REALIGN=0 builds the round-5 b3_leaf loads there).
@@ -342,6 +345,9 @@ __device__ __forceinline__ void b3_leaf(const uint8_t *p, uint32_t n, uint64_t c
 // the leaf's last 128-byte line, which the right neighbour's lane read ~16 compressions
 // earlier), kernel time equal (0.406 / 0.410 ms): the kernel is VALU-issue bound.  53 KiB
 // of LDS per 4-wave workgroup: 3 waves per SIMD instead of 4, no loss at this issue rate.
+// With that last line loaded at the start, beside the neighbour's request for it, and held
+// in registers (CG_B3_HOLD_TAIL, 32 VGPRs): 1.09x, 0.405 -> 0.412 ms, config 3 equal
+// (profiles/r06_v20_b3_hold_tail_ab.txt).
 #define B3_RING 52u  // dwords per lane: 48 + 4 pad (8 consecutive lanes' b128 stores on distinct banks)
 __device__ __forceinline__ void b3_leaf_lds(const uint8_t *p, uint32_t n, uint64_t ctr, bool root, uint32_t cv[8],
                                             uint32_t *ring) {
@@ -355,6 +361,35 @@ __device__ __forceinline__ void b3_leaf_lds(const uint8_t *p, uint32_t n, uint64
     const uint32_t last_seg = (off + (n ? n : 1u) - 1u) >> 6;  // the last segment holding leaf bytes
     uint32_t *rl = ring + (off >> 2);                           // this lane's block reads start here
     uint4 r0, r1, r2, r3;  // the segment in flight (four named registers: an array went to scratch)
+#if CG_B3_HOLD_TAIL
+    // The leaf's last 128-byte line (its last segment, and the one before when both share the
+    // line) is the right neighbour lane's first: loaded now, at the same time as the
+    // neighbour's, and held in registers until the last blocks need it.
+    const uint32_t hold_from =
+        (last_seg > 0 && (((uintptr_t)(seg0 + 4 * last_seg)) & 64u)) ? last_seg - 1 : last_seg;
+    const uint4 *qa = seg0 + 4 * hold_from, *qb = seg0 + 4 * last_seg;
+    const uint4 ha0 = qa[0], ha1 = qa[1], ha2 = qa[2], ha3 = qa[3];
+    const uint4 hb0 = qb[0], hb1 = qb[1], hb2 = qb[2], hb3 = qb[3];
+    auto load_seg = [&](uint32_t k) {  // past the leaf: its last segment again (never read)
+        if (k < hold_from) {
+            const uint4 *q = seg0 + 4 * k;
+            r0 = q[0];
+            r1 = q[1];
+            r2 = q[2];
+            r3 = q[3];
+        } else if (k == hold_from) {
+            r0 = ha0;
+            r1 = ha1;
+            r2 = ha2;
+            r3 = ha3;
+        } else {
+            r0 = hb0;
+            r1 = hb1;
+            r2 = hb2;
+            r3 = hb3;
+        }
+    };
+#else
     auto load_seg = [&](uint32_t k) {  // past the leaf: re-read its last segment (never read)
         const uint4 *q = seg0 + 4 * (k < last_seg ? k : last_seg);
         r0 = q[0];
@@ -362,6 +397,7 @@ __device__ __forceinline__ void b3_leaf_lds(const uint8_t *p, uint32_t n, uint64
         r2 = q[2];
         r3 = q[3];
     };
+#endif
     auto store_seg = [&](uint32_t at) {
         uint4 *d = reinterpret_cast<uint4 *>(ring + at);
         d[0] = r0;
