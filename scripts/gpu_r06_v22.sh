@@ -28,3 +28,8 @@ for r in rows:
     q = r.get('Queue_Id'); gap = s - last.get(q, s); last[q] = e
     print(round(s, 1), round(e, 1), 'dur', round(e - s, 1), 'queue', q, 'stream', r.get('Stream_Id'), 'gap_on_queue', round(gap, 1))
 PY
+# PMC passes of the merged 16 GiB-batch launches (configs 4 / 5: two batches per launch)
+for c in c4 c5; do
+  CFG=$c TAG=r06_v22_pmc_$c bash scripts/gpu_pmc.sh || exit $?
+  python3 scripts/pmc_summary.py gpurun_out r06_v22_pmc_$c > gpurun_out/r06_v22_pmc_$c.json
+done
