@@ -92,25 +92,27 @@ struct cg_pipeline {
 namespace cgrt {
 
 // Stream kind of the pipeline's streams (CHUNKER_AMD_PIPE_STREAMS, read once): "high"
-// (default) = non-blocking, high priority (HIP's high-priority queue pool); "cumask" = a CU
-// mask over every CU (a queue of its own, but a blocking stream); "plain" = ordinary
-// non-blocking streams (the shared pool; A/B only).
+// (default) = non-blocking, high priority (HIP's high-priority queue pool); "split" = the
+// boundary stream high priority, the digest lanes low priority (HIP's low-priority pool);
+// "cumask" = a CU mask over every CU (a queue of its own, but a blocking stream); "plain" =
+// ordinary non-blocking streams (the shared pool; A/B only).
 static int pipe_stream_kind() {
     static const int k = [] {
         const char *e = getenv("CHUNKER_AMD_PIPE_STREAMS");
         if (e && !strcmp(e, "plain")) return 0;
         if (e && !strcmp(e, "cumask")) return 2;
+        if (e && !strcmp(e, "split")) return 3;
         return 1;
     }();
     return k;
 }
 
-static int make_stream(hipStream_t *s) {
+static int make_stream(hipStream_t *s, bool boundary) {
     const int kind = pipe_stream_kind();
-    if (kind == 1) {
+    if (kind == 1 || kind == 3) {
         int lo = 0, hi = 0;
         HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        HIP_TRY(hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi));
+        HIP_TRY(hipStreamCreateWithPriority(s, hipStreamNonBlocking, (kind == 3 && !boundary) ? lo : hi));
     } else if (kind == 2) {
         int dev = 0;
         HIP_TRY(hipGetDevice(&dev));
@@ -287,9 +289,9 @@ int cg_pipeline_create(int device, uint32_t group_batches, uint32_t lanes, cg_pi
     p->group_max = group_batches ? group_batches : 16;
     p->nlanes = lanes ? lanes : 2;
     p->lanes.resize(p->nlanes);
-    if ((rc = make_stream(&p->bstream))) return rc;
+    if ((rc = make_stream(&p->bstream, true))) return rc;
     for (auto &L : p->lanes)
-        if ((rc = make_stream(&L.st))) return rc;
+        if ((rc = make_stream(&L.st, false))) return rc;
     *out = p.release();
     return CG_OK;
 }

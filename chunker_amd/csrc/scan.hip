@@ -232,13 +232,13 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan(const uint8_t *__restrict__ da
 #define F32_RPS (CG_SEG / F32_ROW)  // rows per segment
 static_assert(CG_SEG % F32_ROW == 0 && F32_RPS == 2, "two 2 KiB rows per segment");
 
-template <uint32_t RING, bool NT>
+template <uint32_t RING, bool NT, uint32_t GC = GEAR_COPIES>
 __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data, uint64_t n,
                                                           const uint64_t *__restrict__ gear_g, uint64_t mask_s,
                                                           uint64_t mask_l, uint32_t cap,
                                                           uint32_t *__restrict__ seg_count,
                                                           uint32_t *__restrict__ seg_cand, uint64_t nseg, uint32_t spw) {
-    __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * GEAR_COPIES];
+    __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * GC];
     __shared__ uint32_t s_slots[SCAN2_T / 64][64];  // the open segment's candidate slots, per wave
     const uint32_t lane = threadIdx.x & 63u;
     // the wave index through readfirstlane: the run's base, bounds and buffer resource
@@ -271,7 +271,7 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
         v[0] = uint4{x0.x, x0.y, x0.z, x0.w};
         v[1] = uint4{x1.x, x1.y, x1.z, x1.w};
     };
-    static_assert(SCAN2_T == 2 * 256 && GEAR_COPIES == 32, "two threads per Gear entry, 16 copies each");
+    static_assert(SCAN2_T == 2 * 256, "two threads per Gear entry");
     const uint32_t ge = threadIdx.x >> 1;
     const uint64_t gv = gear_g[ge] << SCAN_SHIFT;
     uint4 ring[RING][2];
@@ -290,13 +290,12 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
         }
     }
     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (uint32_t j = 0; j < 16; ++j) s_gear[ge * GEAR_COPIES + (((threadIdx.x & 1u) * 16u + j + ge) & 31u)] = gv;
+    gear_fill<GC>(s_gear, gv, ge, threadIdx.x);
     __syncthreads();
     if (!active) return;
     const char *gbase = reinterpret_cast<const char *>(s_gear);
     uint32_t *slots = s_slots[wv];
-    const uint32_t lo8 = (threadIdx.x & 31u) * 8u;
+    const uint32_t lo8 = (threadIdx.x & (GC - 1)) * 8u;
     uint32_t ad[2][4];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -312,14 +311,14 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
 
     // q[k][b]: split partials of the lane's 8 dwords (k), byte b
     auto partials = [&](const uint4 (&v)[2], uint64_t (&q)[8][4]) {
-        lookup4(gbase, ad[0], v[0].x, q[0]);
-        lookup4(gbase, ad[0], v[0].y, q[1]);
-        lookup4(gbase, ad[0], v[0].z, q[2]);
-        lookup4(gbase, ad[0], v[0].w, q[3]);
-        lookup4(gbase, ad[0], v[1].x, q[4]);
-        lookup4(gbase, ad[0], v[1].y, q[5]);
-        lookup4(gbase, ad[0], v[1].z, q[6]);
-        lookup4(gbase, ad[0], v[1].w, q[7]);
+        gear_look<GC>(gbase, ad[0], lo8, v[0].x, q[0]);
+        gear_look<GC>(gbase, ad[0], lo8, v[0].y, q[1]);
+        gear_look<GC>(gbase, ad[0], lo8, v[0].z, q[2]);
+        gear_look<GC>(gbase, ad[0], lo8, v[0].w, q[3]);
+        gear_look<GC>(gbase, ad[0], lo8, v[1].x, q[4]);
+        gear_look<GC>(gbase, ad[0], lo8, v[1].y, q[5]);
+        gear_look<GC>(gbase, ad[0], lo8, v[1].z, q[6]);
+        gear_look<GC>(gbase, ad[0], lo8, v[1].w, q[7]);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             q[k][1] = shl1_add(q[k][0], q[k][1]);
@@ -502,14 +501,14 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
 #endif
 static_assert(sizeof(ScanQueue) == 9 * 64, "one 64-B line per counter");
 
-template <uint32_t SPU>
+template <uint32_t SPU, uint32_t GC = GEAR_COPIES>
 __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data, uint64_t n,
                                                            const uint64_t *__restrict__ gear_g, uint64_t mask_s,
                                                            uint64_t mask_l, uint32_t cap,
                                                            uint32_t *__restrict__ seg_count,
                                                            uint32_t *__restrict__ seg_cand, uint64_t nseg,
                                                            ScanQueue *queue, uint32_t nunits) {
-    __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * GEAR_COPIES];
+    __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * GC];
     __shared__ uint32_t s_slots[SCAN2_T / 64][64];  // the open segment's candidate slots, per wave
     constexpr uint32_t R = SPU * F32_RPS;           // rows per unit
     constexpr uint32_t UNIT = SPU * CG_SEG;
@@ -591,7 +590,7 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
         return nunits;
     };
 
-    static_assert(SCAN2_T == 2 * 256 && GEAR_COPIES == 32, "two threads per Gear entry, 16 copies each");
+    static_assert(SCAN2_T == 2 * 256, "two threads per Gear entry");
     const uint32_t ge = threadIdx.x >> 1;
     const uint64_t gv = gear_g[ge] << SCAN_SHIFT;
     dq_issue();
@@ -604,12 +603,11 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
     blk(ur.rs, 0, ring[0], halo_off);
     blk(ur.rs, ur.hoff, ring[1], lane_off);
     __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (uint32_t j = 0; j < 16; ++j) s_gear[ge * GEAR_COPIES + (((threadIdx.x & 1u) * 16u + j + ge) & 31u)] = gv;
+    gear_fill<GC>(s_gear, gv, ge, threadIdx.x);
     __syncthreads();
     const char *gbase = reinterpret_cast<const char *>(s_gear);
     uint32_t *slots = s_slots[wv];
-    const uint32_t lo8 = (threadIdx.x & 31u) * 8u;
+    const uint32_t lo8 = (threadIdx.x & (GC - 1)) * 8u;
     uint32_t ad[2][4];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -623,14 +621,14 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
     const uint32_t ms_lo = (uint32_t)ms, ms_hi = (uint32_t)(ms >> 32), ml_lo = (uint32_t)ml, ml_hi = (uint32_t)(ml >> 32);
 
     auto partials = [&](const uint4 (&v)[2], uint64_t (&q)[8][4]) {
-        lookup4(gbase, ad[0], v[0].x, q[0]);
-        lookup4(gbase, ad[0], v[0].y, q[1]);
-        lookup4(gbase, ad[0], v[0].z, q[2]);
-        lookup4(gbase, ad[0], v[0].w, q[3]);
-        lookup4(gbase, ad[0], v[1].x, q[4]);
-        lookup4(gbase, ad[0], v[1].y, q[5]);
-        lookup4(gbase, ad[0], v[1].z, q[6]);
-        lookup4(gbase, ad[0], v[1].w, q[7]);
+        gear_look<GC>(gbase, ad[0], lo8, v[0].x, q[0]);
+        gear_look<GC>(gbase, ad[0], lo8, v[0].y, q[1]);
+        gear_look<GC>(gbase, ad[0], lo8, v[0].z, q[2]);
+        gear_look<GC>(gbase, ad[0], lo8, v[0].w, q[3]);
+        gear_look<GC>(gbase, ad[0], lo8, v[1].x, q[4]);
+        gear_look<GC>(gbase, ad[0], lo8, v[1].y, q[5]);
+        gear_look<GC>(gbase, ad[0], lo8, v[1].z, q[6]);
+        gear_look<GC>(gbase, ad[0], lo8, v[1].w, q[7]);
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             q[k][1] = shl1_add(q[k][0], q[k][1]);
@@ -871,10 +869,21 @@ uint32_t g_scan_kernel = 0;
 // test hook (cg_test_scan_grid): workgroups of the persistent scan (0 = the resident count)
 uint64_t g_scan_grid = 0;
 
+// Lean Gear table for the flat scans (GEAR_COPIES_LEAN, scan_common.h): CHUNKER_AMD_SCAN_LEAN=1
+// (read once; A/B) takes it for every flat scan.
+static bool scan_lean() {
+    static const bool lean = [] {
+        const char *e = getenv("CHUNKER_AMD_SCAN_LEAN");
+        return e && e[0] == '1';
+    }();
+    return lean;
+}
+
 void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint64_t mask_s, uint64_t mask_l,
                  uint32_t cap, uint32_t *d_seg_count, uint32_t *d_seg_cand, uint64_t nseg, hipStream_t st,
                  ScanQueue *d_queue) {
     if (nseg == 0) return;
+    const bool lean = scan_lean();
     const uint64_t blocks = (nseg + SCAN2_T - 1) / SCAN2_T;
     // prefilter when the bits of mask_s & mask_l it tests leave hits rarer than ~1 per 16 KiB
     // (averages >= 64 KiB with the v2020 masks)
@@ -929,11 +938,12 @@ void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint
         const uint64_t want = (nunits + SCAN2_T / 64 - 1) / (SCAN2_T / 64);  // >= one unit per wave
         uint64_t grid = std::max<uint64_t>(1, std::min(want, resident));
         if (g_scan_grid) grid = g_scan_grid;
-        hipLaunchKernelGGL(k_scan_flat32p<CG_SCAN_SPU>, dim3((uint32_t)grid), dim3(SCAN2_T), 0, st, d_data, n, d_gear,
-                           mask_s, mask_l, cap, d_seg_count, d_seg_cand, nseg, d_queue, (uint32_t)nunits);
+        auto kp = lean ? k_scan_flat32p<CG_SCAN_SPU, GEAR_COPIES_LEAN> : k_scan_flat32p<CG_SCAN_SPU>;
+        hipLaunchKernelGGL(kp, dim3((uint32_t)grid), dim3(SCAN2_T), 0, st, d_data, n, d_gear, mask_s, mask_l, cap,
+                           d_seg_count, d_seg_cand, nseg, d_queue, (uint32_t)nunits);
         return;
     }
-    auto k = k_scan_flat32<2, true>;
+    auto k = lean ? k_scan_flat32<2, true, GEAR_COPIES_LEAN> : k_scan_flat32<2, true>;
 #ifdef CG_DIAG
     if (diag_variant) k = scan_flat_diag_kernel(k);
 #endif

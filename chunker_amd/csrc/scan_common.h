@@ -64,6 +64,34 @@ __device__ __forceinline__ void lookup4(const char *gbase, uint32_t (&a)[4], uin
     for (int b = 0; b < 4; ++b) g[b] = lds_gear(gbase, a[b]);
 }
 
+// Lean table (round 6): 8 copies at a 64-byte entry stride -- 16 KiB, 18 KiB with the
+// candidate slots -- so a scan workgroup fits on a CU beside two SHA-256 digest workgroups
+// (2 x 69.7 KiB) of the digest pipeline's merged launches.  The byte no longer lands on a
+// byte boundary of the address, so an address takes two VALU (extract, shift-or) instead of
+// the SDWA mov's one, and the 4 lanes sharing a copy (of 32 per ds_read_b64 group) meet on a
+// bank pair when their bytes agree mod 4.
+#define GEAR_COPIES_LEAN 8u
+__device__ __forceinline__ void lookup4_lean(const char *gbase, uint32_t lo, uint32_t w, uint64_t (&g)[4]) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) g[b] = lds_gear(gbase, (__builtin_amdgcn_ubfe(w, 8 * b, 8) << 6) | lo);
+}
+// The table fill of a 512-thread workgroup: two threads per entry, each storing half its copies
+// (rotated by the entry so a store group spreads over the banks).
+template <uint32_t GC>
+__device__ __forceinline__ void gear_fill(uint64_t *s_gear, uint64_t gv, uint32_t ge, uint32_t tid) {
+    static_assert(GC == 32 || GC == GEAR_COPIES_LEAN, "32 or 8 copies");
+#pragma unroll
+    for (uint32_t j = 0; j < GC / 2; ++j) s_gear[ge * GC + (((tid & 1u) * (GC / 2) + j + ge) & (GC - 1))] = gv;
+}
+template <uint32_t GC>
+__device__ __forceinline__ void gear_look(const char *gbase, uint32_t (&a)[4], uint32_t lo, uint32_t w,
+                                          uint64_t (&g)[4]) {
+    if constexpr (GC == 32)
+        lookup4(gbase, a, w, g);
+    else
+        lookup4_lean(gbase, lo, w, g);
+}
+
 __device__ __forceinline__ uint32_t gear_flags64(uint64_t h, uint64_t ms, uint64_t ml) {
     return ((h & ms) == 0 ? CG_FLAG_S : 0u) | ((h & ml) == 0 ? CG_FLAG_L : 0u);
 }
