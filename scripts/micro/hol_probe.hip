@@ -35,6 +35,28 @@ __global__ __launch_bounds__(512) void k_spin_scan(unsigned long long ticks, uns
     if (x == 0x12345678u) out[threadIdx.x] = x + s[0];
 }
 
+// variants of the scan's shape: 256 threads at 128 VGPRs, 512 threads at 112 VGPRs
+__global__ __launch_bounds__(256) void k_spin_scan256(unsigned long long ticks, unsigned *out) {
+    extern __shared__ unsigned s[];
+    asm volatile("" ::: "v127");
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned x = threadIdx.x;
+    if (threadIdx.x == 0) s[0] = x;
+    __syncthreads();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) x = x * 1664525u + 1013904223u;
+    if (x == 0x12345678u) out[threadIdx.x] = x + s[0];
+}
+__global__ __launch_bounds__(512) void k_spin_scan112(unsigned long long ticks, unsigned *out) {
+    extern __shared__ unsigned s[];
+    asm volatile("" ::: "v111");
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned x = threadIdx.x;
+    if (threadIdx.x == 0) s[0] = x;
+    __syncthreads();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) x = x * 1664525u + 1013904223u;
+    if (x == 0x12345678u) out[threadIdx.x] = x + s[0];
+}
+
 __global__ void k_spin(unsigned long long ticks, unsigned *out) {
     extern __shared__ unsigned s[];
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -59,7 +81,7 @@ int main(int argc, char **argv) {
     const int a_wgs = atoi(argv[1]), a_lds = atoi(argv[2]), b_lds = atoi(argv[4]), hi = atoi(argv[5]);
     const int real = argc > 6 ? atoi(argv[6]) : 0;  // 1: the real kernels' footprints (k_spin_sha / k_spin_scan)
     const double a_ms = atof(argv[3]);
-    if (a_wgs < 1 || a_wgs > 4096 || a_lds < 4 || a_lds > 160 * 1024 || b_lds < 4 || b_lds > 64 * 1024 || a_ms > 100)
+    if (a_wgs < 1 || a_wgs > 4096 || a_lds < 4 || a_lds > 160 * 1024 || b_lds < 4 || b_lds > 96 * 1024 || a_ms > 100)
         return 2;
     unsigned *d = nullptr;
     CK(hipMalloc(&d, 4096));
@@ -81,7 +103,11 @@ int main(int argc, char **argv) {
         while (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count() < 2.0) {
         }
         const auto t0 = std::chrono::steady_clock::now();
-        if (real)
+        if (real == 2)
+            hipLaunchKernelGGL(k_spin_scan256, dim3(2048), dim3(256), b_lds, sb, 10000ull, d);
+        else if (real == 3)
+            hipLaunchKernelGGL(k_spin_scan112, dim3(1024), dim3(512), b_lds, sb, 10000ull, d);
+        else if (real)
             hipLaunchKernelGGL(k_spin_scan, dim3(1024), dim3(512), b_lds, sb, 10000ull, d);
         else
             hipLaunchKernelGGL(k_spin, dim3(256), dim3(256), b_lds, sb, 20000ull, d);
