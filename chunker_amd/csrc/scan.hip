@@ -232,19 +232,19 @@ __global__ __launch_bounds__(SCAN2_T) void k_scan(const uint8_t *__restrict__ da
 #define F32_RPS (CG_SEG / F32_ROW)  // rows per segment
 static_assert(CG_SEG % F32_ROW == 0 && F32_RPS == 2, "two 2 KiB rows per segment");
 
-template <uint32_t RING, bool NT, uint32_t GC = GEAR_COPIES>
-__global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data, uint64_t n,
+template <uint32_t RING, bool NT, uint32_t GC = GEAR_COPIES, uint32_t T = SCAN2_T>
+__global__ __launch_bounds__(T, 4) void k_scan_flat32(const uint8_t *data, uint64_t n,
                                                           const uint64_t *__restrict__ gear_g, uint64_t mask_s,
                                                           uint64_t mask_l, uint32_t cap,
                                                           uint32_t *__restrict__ seg_count,
                                                           uint32_t *__restrict__ seg_cand, uint64_t nseg, uint32_t spw) {
     __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * GC];
-    __shared__ uint32_t s_slots[SCAN2_T / 64][64];  // the open segment's candidate slots, per wave
+    __shared__ uint32_t s_slots[T / 64][64];  // the open segment's candidate slots, per wave
     const uint32_t lane = threadIdx.x & 63u;
     // the wave index through readfirstlane: the run's base, bounds and buffer resource
     // are then scalar (SGPRs), not per-lane copies
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t seg0 = ((uint64_t)blockIdx.x * (SCAN2_T / 64) + wv) * spw;
+    const uint64_t seg0 = ((uint64_t)blockIdx.x * (T / 64) + wv) * spw;
     const bool active = seg0 < nseg;  // whole wave (uniform)
     const uint64_t r0 = seg0 * CG_SEG;
     const uint64_t nrow = (uint64_t)spw * F32_RPS;  // a multiple of RING (spw a multiple of 4)
@@ -271,8 +271,8 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
         v[0] = uint4{x0.x, x0.y, x0.z, x0.w};
         v[1] = uint4{x1.x, x1.y, x1.z, x1.w};
     };
-    static_assert(SCAN2_T == 2 * 256, "two threads per Gear entry");
-    const uint32_t ge = threadIdx.x >> 1;
+    static_assert(T == 2 * 256 || (T == 256 && GC == GEAR_COPIES_LEAN), "two threads per Gear entry, or one (lean)");
+    const uint32_t ge = T == 256 ? threadIdx.x : threadIdx.x >> 1;
     const uint64_t gv = gear_g[ge] << SCAN_SHIFT;
     uint4 ring[RING][2];
 #pragma unroll
@@ -290,7 +290,12 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32(const uint8_t *data,
         }
     }
     __builtin_amdgcn_sched_barrier(0);
-    gear_fill<GC>(s_gear, gv, ge, threadIdx.x);
+    if constexpr (T == 256) {
+#pragma unroll
+        for (uint32_t j = 0; j < GC; ++j) s_gear[ge * GC + ((j + ge) & (GC - 1))] = gv;
+    } else {
+        gear_fill<GC>(s_gear, gv, ge, threadIdx.x);
+    }
     __syncthreads();
     if (!active) return;
     const char *gbase = reinterpret_cast<const char *>(s_gear);
@@ -938,12 +943,18 @@ void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint
         const uint64_t want = (nunits + SCAN2_T / 64 - 1) / (SCAN2_T / 64);  // >= one unit per wave
         uint64_t grid = std::max<uint64_t>(1, std::min(want, resident));
         if (g_scan_grid) grid = g_scan_grid;
-        auto kp = lean ? k_scan_flat32p<CG_SCAN_SPU, GEAR_COPIES_LEAN> : k_scan_flat32p<CG_SCAN_SPU>;
+        auto kp = k_scan_flat32p<CG_SCAN_SPU>;
         hipLaunchKernelGGL(kp, dim3((uint32_t)grid), dim3(SCAN2_T), 0, st, d_data, n, d_gear, mask_s, mask_l, cap,
                            d_seg_count, d_seg_cand, nseg, d_queue, (uint32_t)nunits);
         return;
     }
-    auto k = lean ? k_scan_flat32<2, true, GEAR_COPIES_LEAN> : k_scan_flat32<2, true>;
+    if (lean) {  // 256-thread workgroups, 18 KiB: beside two digest workgroups per CU
+        auto kl = k_scan_flat32<2, true, GEAR_COPIES_LEAN, 256>;
+        hipLaunchKernelGGL(kl, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, st, d_data, n, d_gear, mask_s, mask_l,
+                           cap, d_seg_count, d_seg_cand, nseg, (uint32_t)spw);
+        return;
+    }
+    auto k = k_scan_flat32<2, true>;
 #ifdef CG_DIAG
     if (diag_variant) k = scan_flat_diag_kernel(k);
 #endif
