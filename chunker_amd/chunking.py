@@ -436,7 +436,7 @@ def pipeline_destroy(p: int) -> None:
 
 
 PIPE_GROUP_BYTES = 24 << 30  # bytes of batches one merged SHA-256 digest launch takes (default_group)
-PIPE_LANES = 2               # merged digests in flight (cg_pipeline_create lanes)
+PIPE_LANES = 3               # merged digests in flight (cg_pipeline_create lanes)
 
 
 def default_group(hash: HashAlgorithm, batch_bytes: int) -> int:

@@ -60,6 +60,8 @@ struct ScanQueue {
 };
 
 // d_queue: a zeroed ScanQueue owned by the caller's workspace (nullptr: the one-shot kernel)
+// the calling thread asks launch_scan for the lean one-shot scan (scan.hip; the digest pipeline)
+extern thread_local bool t_scan_lean;
 void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint64_t mask_s, uint64_t mask_l,
                  uint32_t cap, uint32_t *d_seg_count, uint32_t *d_seg_cand, uint64_t nseg, hipStream_t st,
                  ScanQueue *d_queue = nullptr);

@@ -287,7 +287,7 @@ int cg_pipeline_create(int device, uint32_t group_batches, uint32_t lanes, cg_pi
     std::unique_ptr<cg_pipeline> p(new cg_pipeline());
     p->device = device;
     p->group_max = group_batches ? group_batches : 16;
-    p->nlanes = lanes ? lanes : 2;
+    p->nlanes = lanes ? lanes : 3;
     p->lanes.resize(p->nlanes);
     if ((rc = make_stream(&p->bstream, true))) return rc;
     for (auto &L : p->lanes)
@@ -331,9 +331,13 @@ int cg_pipeline_submit(cg_pipeline *p, const uint8_t *d_data, const uint64_t *na
     }
     if ((rc = ws->done_flag.ensure(64, /*mapped=*/true))) return undo(rc);
     __atomic_store_n(ws->done_flag.as<uint32_t>(), 0u, __ATOMIC_RELEASE);
-    if ((rc = launch_batch(ws, d_data, nar_offsets, n_nars, o, algo, d_out, out_cap, p->bstream, nullptr, nullptr,
-                           /*digest=*/false, &bl)))
-        return undo(rc);
+    // the boundary stages run beside the merged digests, which hold two workgroups on every
+    // CU: the lean scan fits there (scan.hip, t_scan_lean)
+    cg::t_scan_lean = true;
+    rc = launch_batch(ws, d_data, nar_offsets, n_nars, o, algo, d_out, out_cap, p->bstream, nullptr, nullptr,
+                      /*digest=*/false, &bl);
+    cg::t_scan_lean = false;
+    if (rc) return undo(rc);
     // the digest's sizes, as launch_batch's own digest would take them
     uint64_t total_cap = 0;
     for (size_t i = 0; i < n_nars; ++i) total_cap += capacity_of(nar_offsets[i + 1] - nar_offsets[i], o.min);

@@ -874,14 +874,24 @@ uint32_t g_scan_kernel = 0;
 // test hook (cg_test_scan_grid): workgroups of the persistent scan (0 = the resident count)
 uint64_t g_scan_grid = 0;
 
-// Lean Gear table for the flat scans (GEAR_COPIES_LEAN, scan_common.h): CHUNKER_AMD_SCAN_LEAN=1
-// (read once; A/B) takes it for every flat scan.
+// Lean one-shot scan (256-thread workgroups, GEAR_COPIES_LEAN table, 17 KiB of LDS): the
+// digest pipeline's boundary stream asks for it (t_scan_lean, pipeline.hip), because there
+// every CU already holds two k_sha256 workgroups of the merged launches, and a 512-thread,
+// 128-VGPR scan workgroup does not fit beside them (the per-SIMD register file: two digest
+// waves of 136 VGPRs leave room for one 128-VGPR wave on that SIMD, and the SPI gives a
+// 512-thread workgroup two per SIMD; profiles/r06_v28_hol_probe.txt).  So the boundary stages
+// of the next group waited 0.5-26 ms per scan for a digest workgroup to end
+// (profiles/r06_v22_*), and the lanes starved.  The lean scan alone is ~10 % slower (0.23 vs
+// 0.21 ms per GiB cold: two VALU per lookup address, 2-way bank conflicts), but runs beside the
+// digests (1.0-1.3 ms under load, against 0.5-26).  CHUNKER_AMD_SCAN_LEAN=0/1 (read once)
+// forces it off / on for every one-shot scan (A/B).
+thread_local bool t_scan_lean = false;
 static bool scan_lean() {
-    static const bool lean = [] {
+    static const int forced = [] {
         const char *e = getenv("CHUNKER_AMD_SCAN_LEAN");
-        return e && e[0] == '1';
+        return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
     }();
-    return lean;
+    return forced >= 0 ? forced == 1 : t_scan_lean;
 }
 
 void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint64_t mask_s, uint64_t mask_l,
