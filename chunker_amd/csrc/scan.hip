@@ -506,15 +506,15 @@ __global__ __launch_bounds__(T, 4) void k_scan_flat32(const uint8_t *data, uint6
 #endif
 static_assert(sizeof(ScanQueue) == 9 * 64, "one 64-B line per counter");
 
-template <uint32_t SPU, uint32_t GC = GEAR_COPIES>
-__global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data, uint64_t n,
+template <uint32_t SPU, uint32_t GC = GEAR_COPIES, uint32_t T = SCAN2_T>
+__global__ __launch_bounds__(T, 4) void k_scan_flat32p(const uint8_t *data, uint64_t n,
                                                            const uint64_t *__restrict__ gear_g, uint64_t mask_s,
                                                            uint64_t mask_l, uint32_t cap,
                                                            uint32_t *__restrict__ seg_count,
                                                            uint32_t *__restrict__ seg_cand, uint64_t nseg,
                                                            ScanQueue *queue, uint32_t nunits) {
     __shared__ __attribute__((aligned(16))) uint64_t s_gear[256 * GC];
-    __shared__ uint32_t s_slots[SCAN2_T / 64][64];  // the open segment's candidate slots, per wave
+    __shared__ uint32_t s_slots[T / 64][64];  // the open segment's candidate slots, per wave
     constexpr uint32_t R = SPU * F32_RPS;           // rows per unit
     constexpr uint32_t UNIT = SPU * CG_SEG;
     const uint32_t lane = threadIdx.x & 63u;
@@ -561,8 +561,8 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
     uint32_t tick = 0;
 #if CG_SCAN_STATIC
     // (A/B form: no queue; wave g of the grid takes units g, g + W, g + 2W, ...)
-    uint32_t snext = blockIdx.x * (SCAN2_T / 64) + wv;
-    const uint32_t sstride = gridDim.x * (SCAN2_T / 64);
+    uint32_t snext = blockIdx.x * (T / 64) + wv;
+    const uint32_t sstride = gridDim.x * (T / 64);
     auto dq_issue = [&]() {};
 #else
     auto dq_issue = [&]() {
@@ -595,8 +595,8 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
         return nunits;
     };
 
-    static_assert(SCAN2_T == 2 * 256, "two threads per Gear entry");
-    const uint32_t ge = threadIdx.x >> 1;
+    static_assert(T == 2 * 256 || (T == 256 && GC == GEAR_COPIES_LEAN), "two threads per Gear entry, or one (lean)");
+    const uint32_t ge = T == 256 ? threadIdx.x : threadIdx.x >> 1;
     const uint64_t gv = gear_g[ge] << SCAN_SHIFT;
     dq_issue();
     uint32_t u = dq_resolve(0u);
@@ -608,7 +608,12 @@ __global__ __launch_bounds__(SCAN2_T, 4) void k_scan_flat32p(const uint8_t *data
     blk(ur.rs, 0, ring[0], halo_off);
     blk(ur.rs, ur.hoff, ring[1], lane_off);
     __builtin_amdgcn_sched_barrier(0);
-    gear_fill<GC>(s_gear, gv, ge, threadIdx.x);
+    if constexpr (T == 256) {
+#pragma unroll
+        for (uint32_t j = 0; j < GC; ++j) s_gear[ge * GC + ((j + ge) & (GC - 1))] = gv;
+    } else {
+        gear_fill<GC>(s_gear, gv, ge, threadIdx.x);
+    }
     __syncthreads();
     const char *gbase = reinterpret_cast<const char *>(s_gear);
     uint32_t *slots = s_slots[wv];
@@ -949,12 +954,14 @@ void launch_scan(const uint8_t *d_data, uint64_t n, const uint64_t *d_gear, uint
     const bool persistent = g_scan_kernel == 2 || (g_scan_kernel == 0 && nseg >= (1ull << 20));
     if (d_queue && persistent && !diag_variant) {
         const uint64_t nunits = (nseg + CG_SCAN_SPU - 1) / CG_SCAN_SPU;
-        const uint64_t resident = scan_resident_wgs();
-        const uint64_t want = (nunits + SCAN2_T / 64 - 1) / (SCAN2_T / 64);  // >= one unit per wave
+        // the lean form: 256-thread workgroups (4 waves), twice as many for the same waves
+        const uint32_t t = lean ? 256u : SCAN2_T;
+        const uint64_t resident = scan_resident_wgs() * (lean ? 2 : 1);
+        const uint64_t want = (nunits + t / 64 - 1) / (t / 64);  // >= one unit per wave
         uint64_t grid = std::max<uint64_t>(1, std::min(want, resident));
         if (g_scan_grid) grid = g_scan_grid;
-        auto kp = k_scan_flat32p<CG_SCAN_SPU>;
-        hipLaunchKernelGGL(kp, dim3((uint32_t)grid), dim3(SCAN2_T), 0, st, d_data, n, d_gear, mask_s, mask_l, cap,
+        auto kp = lean ? k_scan_flat32p<CG_SCAN_SPU, GEAR_COPIES_LEAN, 256> : k_scan_flat32p<CG_SCAN_SPU>;
+        hipLaunchKernelGGL(kp, dim3((uint32_t)grid), dim3(t), 0, st, d_data, n, d_gear, mask_s, mask_l, cap,
                            d_seg_count, d_seg_cand, nseg, d_queue, (uint32_t)nunits);
         return;
     }
