@@ -843,7 +843,7 @@ __global__ __launch_bounds__(T, 4) void k_scan_flat32p(const uint8_t *data, uint
     // count made every wave write back and invalidate its XCD's L2 on the way out --
     // buffer_wbl2 / buffer_inv sc1 -- dropping the lines the running waves had fetched.)
     if (lane == 0) {
-        const uint32_t waves = gridDim.x * (SCAN2_T / 64);
+        const uint32_t waves = gridDim.x * (T / 64);
         const uint32_t old = __hip_atomic_fetch_add(&queue->done[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (old == waves - 1) {
 #pragma unroll
