@@ -18,7 +18,7 @@
 //     member's host-mapped completion word when its last chunk is stored (ShaNotify), so a
 //     batch completes when ITS longest chunk does, not when the merged launch ends, and a
 //     cg_batch_wait returns as soon as its own digests are in HBM.
-// The pipeline holds 1 + L streams however many batches are in flight.  They are
+// The pipeline holds 1 + L streams (L = 3 by default) however many batches are in flight.  They are
 // non-blocking high-priority streams (CHUNKER_AMD_PIPE_STREAMS, below): HIP keeps a pool
 // of hardware queues per priority, so they do not share a queue with the process's
 // ordinary streams however many of those are busy (scripts/micro/queue_probe.hip,

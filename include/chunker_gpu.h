@@ -137,7 +137,7 @@ int cg_chunk_batch_device_async_after(const uint8_t *d_data, const uint64_t *nar
  * run on the pipeline's boundary stream, each after its own `inputs_ready` event (a
  * hipEvent_t recorded after the last write to d_data and the last use of d_out; NULL = no
  * wait); the SHA-256 digests of up to `group_batches` consecutive batches (0 = 16, at most
- * 64) are then computed by ONE merged launch on one of `lanes` digest streams (0 = 2, at
+ * 64) are then computed by ONE merged launch on one of `lanes` digest streams (0 = 3, at
  * most 8), so the next group's boundary stages and digest run beside it.  A group is
  * launched when it is full, when one of its batches is waited for (cg_batch_wait,
  * cg_batch_event) or by cg_pipeline_flush.  Each batch completes as soon as its own chunks
@@ -145,7 +145,9 @@ int cg_chunk_batch_device_async_after(const uint8_t *d_data, const uint64_t *nar
  * batches run whole on the boundary stream, in submission order.  The pipeline uses
  * 1 + lanes non-blocking high-priority streams on `device` (-1 = the current device; the
  * caller's current device is left unchanged by every pipeline call), which HIP keeps off
- * the hardware queues of the process's ordinary streams whatever GPU_MAX_HW_QUEUES is.
+ * the hardware queues of the process's ordinary streams whatever GPU_MAX_HW_QUEUES is (its
+ * high-priority pool holds four queues: up to 3 lanes get one each).  The boundary stream's
+ * scans use a lean form that fits on a CU beside two digest workgroups.
  * A batch is waited for with cg_batch_wait exactly once, as for
  * cg_chunk_batch_device_async; results, errors and nar_first are the same as those of
  * cg_chunk_batch_device on the same inputs.  A pipeline is single-owner; its batches may
