@@ -371,6 +371,9 @@ def test_async_batches_from_threads(ca, O):
         try:
             s = torch.cuda.Stream()
             outs = [torch.zeros(cap * 48, dtype=torch.uint8, device="cuda") for _ in range(2)]
+            # the zero fills run on torch's current stream, the batches on `s` (non-blocking):
+            # without this the fill could land after a batch's descriptors
+            torch.cuda.current_stream().synchronize()
             algo = t % 2
             pending = ca.chunk_batch_device_async(d.data_ptr(), offs, outs[0].data_ptr(), cap, *params, hash=algo,
                                                   stream=s.cuda_stream)
