@@ -1287,13 +1287,6 @@ void launch_sha256_pipe(const PipeTable &t, uint64_t bound_sum, uint64_t expecte
     const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((bound_sum + 255) / 256, 1024));
     hipLaunchKernelGGL(k_pipe_merge, dim3(grid), dim3(256), 0, st, t, b);
     if (start) (void)hipEventRecord(start, st);
-    // A/B only (CHUNKER_AMD_PIPE_TIGHT=1): size the digest grid from 1.4x the expected chunk
-    // count instead of the members' capacity -- unsafe for inputs with more chunks than that
-    static const bool tight = [] {
-        const char *e = getenv("CHUNKER_AMD_PIPE_TIGHT");
-        return e && e[0] == '1';
-    }();
-    if (tight && expected) bound_sum = std::min<uint64_t>(bound_sum, expected + expected * 2 / 5);
     if (bound_sum) {
         ShaNotify nt;
         nt.dst = b.mdst;
