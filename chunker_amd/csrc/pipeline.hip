@@ -52,9 +52,11 @@ struct PipeMember {
     uint32_t *flag_dev = nullptr;
 };
 
+constexpr uint32_t PIPE_MAX_BSTREAMS = 4;
+
 struct PipeGroup {
     std::vector<PipeMember> members;
-    hipEvent_t bdone = nullptr, done = nullptr, t0 = nullptr, t1 = nullptr;
+    hipEvent_t bdone[PIPE_MAX_BSTREAMS] = {}, done = nullptr, t0 = nullptr, t1 = nullptr;
     bool launched = false, timed = false;
     int rc = CG_OK;
     std::string err;
@@ -62,7 +64,9 @@ struct PipeGroup {
     uint64_t bytes = 0;
     cg_pipeline *owner = nullptr;  // while the group is open (a wait flushes it)
     ~PipeGroup() {
-        for (hipEvent_t e : {bdone, done, t0, t1})
+        for (hipEvent_t e : bdone)
+            if (e) (void)hipEventDestroy(e);
+        for (hipEvent_t e : {done, t0, t1})
             if (e) (void)hipEventDestroy(e);
     }
 };
@@ -78,7 +82,9 @@ struct PipeLane {
 struct cg_pipeline {
     int device = -1;
     uint32_t group_max = 0, nlanes = 0;
-    hipStream_t bstream = nullptr;
+    // boundary streams: a submitted batch's stages run on bstream[k % nb] (batch k)
+    hipStream_t bstream[cgrt::PIPE_MAX_BSTREAMS] = {};
+    uint32_t nb = 1, next_b = 0;
     std::vector<cgrt::PipeLane> lanes;
     uint32_t next_lane = 0;
     std::shared_ptr<cgrt::PipeGroup> open;
@@ -144,8 +150,10 @@ static int flush_locked(cg_pipeline *p) {
     PipeLane &L = p->lanes[p->next_lane];
     p->next_lane = (p->next_lane + 1) % p->nlanes;
     auto launch = [&]() -> int {
-        HIP_TRY(hipEventRecord(g->bdone, p->bstream));
-        HIP_TRY(hipStreamWaitEvent(L.st, g->bdone, 0));
+        for (uint32_t i = 0; i < p->nb; ++i) {
+            HIP_TRY(hipEventRecord(g->bdone[i], p->bstream[i]));
+            HIP_TRY(hipStreamWaitEvent(L.st, g->bdone[i], 0));
+        }
         cg::PipeTable t{};
         t.n = (uint32_t)g->members.size();
         uint64_t bound = 0, expected = 0, max_len = 0;
@@ -192,7 +200,7 @@ static int flush_locked(cg_pipeline *p) {
         // whatever was queued may still read the members' buffers: drain before their
         // waits release the workspaces
         (void)hipStreamSynchronize(L.st);
-        (void)hipStreamSynchronize(p->bstream);
+        for (uint32_t i = 0; i < p->nb; ++i) (void)hipStreamSynchronize(p->bstream[i]);
         return group_fail(*g, rc);
     }
     L.last = g;
@@ -289,7 +297,10 @@ int cg_pipeline_create(int device, uint32_t group_batches, uint32_t lanes, cg_pi
     p->group_max = group_batches ? group_batches : 16;
     p->nlanes = lanes ? lanes : 3;
     p->lanes.resize(p->nlanes);
-    if ((rc = make_stream(&p->bstream, true))) return rc;
+    // CHUNKER_AMD_PIPE_BSTREAMS (1..4, read per pipeline): boundary streams (A/B)
+    if (const char *e = getenv("CHUNKER_AMD_PIPE_BSTREAMS")) p->nb = std::min<uint32_t>(std::max(atoi(e), 1), PIPE_MAX_BSTREAMS);
+    for (uint32_t i = 0; i < p->nb; ++i)
+        if ((rc = make_stream(&p->bstream[i], true))) return rc;
     for (auto &L : p->lanes)
         if ((rc = make_stream(&L.st, false))) return rc;
     *out = p.release();
@@ -314,19 +325,21 @@ int cg_pipeline_submit(cg_pipeline *p, const uint8_t *d_data, const uint64_t *na
     Workspace *ws = nullptr;
     if ((rc = acquire(&ws))) return rc;
     std::lock_guard<std::mutex> lk(p->mu);
+    hipStream_t bs = p->bstream[p->next_b];
+    p->next_b = (p->next_b + 1) % p->nb;
     auto undo = [&](int code) {
-        (void)hipStreamSynchronize(p->bstream);
+        (void)hipStreamSynchronize(bs);
         release(ws);
         return code;
     };
-    if (inputs_ready && hipStreamWaitEvent(p->bstream, static_cast<hipEvent_t>(inputs_ready), 0) != hipSuccess)
+    if (inputs_ready && hipStreamWaitEvent(bs, static_cast<hipEvent_t>(inputs_ready), 0) != hipSuccess)
         return undo(fail(CG_E_IO, "hipStreamWaitEvent(inputs_ready) failed"));
     BatchLaunch bl;
     if (algo == CG_BLAKE3) {  // the whole batch on the boundary stream, in submission order
-        if ((rc = launch_batch(ws, d_data, nar_offsets, n_nars, o, algo, d_out, out_cap, p->bstream, nullptr,
-                               nullptr, true, &bl)))
+        if ((rc = launch_batch(ws, d_data, nar_offsets, n_nars, o, algo, d_out, out_cap, bs, nullptr, nullptr, true,
+                               &bl)))
             return undo(rc);
-        *batch = new cg_batch{ws, p->bstream, bl, nullptr, 0, p->device};
+        *batch = new cg_batch{ws, bs, bl, nullptr, 0, p->device};
         return CG_OK;
     }
     if ((rc = ws->done_flag.ensure(64, /*mapped=*/true))) return undo(rc);
@@ -334,7 +347,7 @@ int cg_pipeline_submit(cg_pipeline *p, const uint8_t *d_data, const uint64_t *na
     // the boundary stages run beside the merged digests, which hold two workgroups on every
     // CU: the lean scan fits there (scan.hip, t_scan_lean)
     cg::t_scan_lean = true;
-    rc = launch_batch(ws, d_data, nar_offsets, n_nars, o, algo, d_out, out_cap, p->bstream, nullptr, nullptr,
+    rc = launch_batch(ws, d_data, nar_offsets, n_nars, o, algo, d_out, out_cap, bs, nullptr, nullptr,
                       /*digest=*/false, &bl);
     cg::t_scan_lean = false;
     if (rc) return undo(rc);
@@ -357,8 +370,10 @@ int cg_pipeline_submit(cg_pipeline *p, const uint8_t *d_data, const uint64_t *na
     if (!p->open) {
         auto g = std::make_shared<PipeGroup>();
         g->timed = g_profiling.load() != 0;
-        if (hipEventCreateWithFlags(&g->bdone, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&g->done, hipEventDisableTiming) != hipSuccess ||
+        for (uint32_t i = 0; i < p->nb; ++i)
+            if (hipEventCreateWithFlags(&g->bdone[i], hipEventDisableTiming) != hipSuccess)
+                return undo(fail(CG_E_IO, "hipEventCreate failed"));
+        if (hipEventCreateWithFlags(&g->done, hipEventDisableTiming) != hipSuccess ||
             (g->timed && (hipEventCreate(&g->t0) != hipSuccess || hipEventCreate(&g->t1) != hipSuccess)))
             return undo(fail(CG_E_IO, "hipEventCreate failed"));
         g->owner = p;
@@ -367,7 +382,7 @@ int cg_pipeline_submit(cg_pipeline *p, const uint8_t *d_data, const uint64_t *na
     std::shared_ptr<PipeGroup> g = p->open;
     g->members.push_back(m);
     g->bytes += total_len;
-    *batch = new cg_batch{ws, p->bstream, bl, g, (uint32_t)(g->members.size() - 1), p->device};
+    *batch = new cg_batch{ws, bs, bl, g, (uint32_t)(g->members.size() - 1), p->device};
     if (g->members.size() >= p->group_max) flush_locked(p);  // a failure reaches every member's wait
     return CG_OK;
 }
@@ -427,7 +442,8 @@ void cg_pipeline_destroy(cg_pipeline *p) {
         (void)flush_locked(p);  // a batch still in the open group gets its digest
         for (auto &L : p->lanes)
             if (L.st) (void)hipStreamSynchronize(L.st);
-        if (p->bstream) (void)hipStreamSynchronize(p->bstream);
+        for (hipStream_t b : p->bstream)
+            if (b) (void)hipStreamSynchronize(b);
         p->timing.clear();
         for (auto &L : p->lanes) {
             L.last.reset();
@@ -436,7 +452,8 @@ void cg_pipeline_destroy(cg_pipeline *p) {
                 d->release();
             if (L.st) (void)hipStreamDestroy(L.st);
         }
-        if (p->bstream) (void)hipStreamDestroy(p->bstream);
+        for (hipStream_t b : p->bstream)
+            if (b) (void)hipStreamDestroy(b);
     }
     delete p;
 }
