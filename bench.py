@@ -90,7 +90,7 @@ def parse_args():
                          "chunker_amd.default_group; 0: the round-5 per-batch-stream path, "
                          "cg_chunk_batch_device_async_after)")
     ap.add_argument("--lanes", type=int, default=0, choices=range(0, 9), metavar="0..8",
-                    help="merged digests in flight (cg_pipeline_create lanes; 0: chunker_amd.PIPE_LANES)")
+                    help="merged digests in flight (cg_pipeline_create lanes; 0: chunking.default_lanes)")
     ap.add_argument("--sha-occ", default="",
                     help="SHA-256 workgroups per CU 'LATENCY,FILL' for launches with more workgroups than CUs "
                          "(cg_test_sha_occupancy; '' = the library's)")
@@ -232,7 +232,7 @@ def main():
     # members finish, so the default group is the divisor of --steps nearest the library's
     # default -- 20 for the driver's 20 steps)
     group = args.group if args.group >= 0 else timed_group(ca.chunking.default_group(algo, batch_bytes), args.steps)
-    lanes = args.lanes or ca.chunking.PIPE_LANES
+    lanes = args.lanes or ca.chunking.default_lanes(algo, batch_bytes)
     depth = args.depth or ((lanes + 1) * group if group else default_depth(algo, batch_bytes))
     # Distinct inputs: every in-flight slot owns its own batch of NARs (global NAR indices
     # slot * n_per * world + this rank's shard, the reference's per-NAR seeds,
@@ -764,7 +764,7 @@ def e2e_one_caller(ca, torch, bufs, offs, nbytes, cap, params, algo, want, args)
     reps x batch bytes / wall time, fill and drain included, reps = 3 x depth."""
     host = bufs[0][0]
     group = args.group if args.group >= 0 else ca.chunking.default_group(algo, nbytes)
-    lanes = args.lanes or ca.chunking.PIPE_LANES
+    lanes = args.lanes or ca.chunking.default_lanes(algo, nbytes)
     depth = args.depth or ((lanes + 1) * group if group else default_depth(algo, nbytes))
     reps = 3 * depth
     dins = [torch.empty(nbytes + 256, dtype=torch.uint8, device="cuda") for _ in range(depth)]

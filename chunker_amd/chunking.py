@@ -436,7 +436,17 @@ def pipeline_destroy(p: int) -> None:
 
 
 PIPE_GROUP_BYTES = 24 << 30  # bytes of batches one merged SHA-256 digest launch takes (default_group)
-PIPE_LANES = 3               # merged digests in flight (cg_pipeline_create lanes)
+PIPE_LANES = 3               # merged digests in flight (cg_pipeline_create lanes; default_lanes)
+
+
+def default_lanes(hash: HashAlgorithm, batch_bytes: int) -> int:
+    """Merged digest launches in flight: four for SHA-256 batches under 4 GiB (the library
+    then runs their boundary stages on two streams, and the lanes in HIP's low-priority
+    queue pool: config 2 at 20 x 4 861-903 GiB/s against 791-808 at 20 x 3,
+    profiles/r06_v35_summary.txt), three otherwise."""
+    if HashAlgorithm(hash) == HashAlgorithm.Sha256 and int(batch_bytes) < (4 << 30):
+        return 4
+    return PIPE_LANES
 
 
 def default_group(hash: HashAlgorithm, batch_bytes: int) -> int:
@@ -478,6 +488,7 @@ class BatchPipeline:
         self.hash = HashAlgorithm(hash)
         self.stream = stream
         self.group = group
+        self._lanes = lanes
         self.lanes = lanes or PIPE_LANES
         self.device = device
         self._p = None
@@ -488,6 +499,8 @@ class BatchPipeline:
         self._opened = True
         if self.group is None:
             self.group = default_group(self.hash, batch_bytes)
+        if not self._lanes:
+            self.lanes = default_lanes(self.hash, batch_bytes)
         if self.group:
             self._p = pipeline_create(self.device, self.group, self.lanes)
             if self.depth is None:

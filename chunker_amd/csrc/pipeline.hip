@@ -84,7 +84,7 @@ struct cg_pipeline {
     uint32_t group_max = 0, nlanes = 0;
     // boundary streams: a submitted batch's stages run on bstream[k % nb] (batch k)
     hipStream_t bstream[cgrt::PIPE_MAX_BSTREAMS] = {};
-    uint32_t nb = 1, next_b = 0;
+    uint32_t nb = 0, next_b = 0;  // nb 0: no batch yet (start_streams)
     std::vector<cgrt::PipeLane> lanes;
     uint32_t next_lane = 0;
     std::shared_ptr<cgrt::PipeGroup> open;
@@ -97,28 +97,30 @@ struct cg_pipeline {
 
 namespace cgrt {
 
-// Stream kind of the pipeline's streams (CHUNKER_AMD_PIPE_STREAMS, read once): "high"
-// (default) = non-blocking, high priority (HIP's high-priority queue pool); "split" = the
-// boundary stream high priority, the digest lanes low priority (HIP's low-priority pool);
+// Stream kind of the pipeline's streams (CHUNKER_AMD_PIPE_STREAMS, read once): default =
+// non-blocking, priority streams: the boundary streams high priority (HIP's high-priority
+// queue pool, four queues), the digest lanes too while they all fit there, else low priority
+// (the low-priority pool, four more queues); "high" / "split" = lanes always high / low;
 // "cumask" = a CU mask over every CU (a queue of its own, but a blocking stream); "plain" =
-// ordinary non-blocking streams (the shared pool; A/B only).
+// ordinary non-blocking streams (the shared pool).  The last three are A/B only.
 static int pipe_stream_kind() {
     static const int k = [] {
         const char *e = getenv("CHUNKER_AMD_PIPE_STREAMS");
         if (e && !strcmp(e, "plain")) return 0;
         if (e && !strcmp(e, "cumask")) return 2;
         if (e && !strcmp(e, "split")) return 3;
+        if (e && !strcmp(e, "high")) return 4;
         return 1;
     }();
     return k;
 }
 
-static int make_stream(hipStream_t *s, bool boundary) {
+static int make_stream(hipStream_t *s, bool low) {
     const int kind = pipe_stream_kind();
-    if (kind == 1 || kind == 3) {
+    if (kind == 1 || kind == 3 || kind == 4) {
         int lo = 0, hi = 0;
         HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        HIP_TRY(hipStreamCreateWithPriority(s, hipStreamNonBlocking, (kind == 3 && !boundary) ? lo : hi));
+        HIP_TRY(hipStreamCreateWithPriority(s, hipStreamNonBlocking, low ? lo : hi));
     } else if (kind == 2) {
         int dev = 0;
         HIP_TRY(hipGetDevice(&dev));
@@ -297,13 +299,35 @@ int cg_pipeline_create(int device, uint32_t group_batches, uint32_t lanes, cg_pi
     p->group_max = group_batches ? group_batches : 16;
     p->nlanes = lanes ? lanes : 3;
     p->lanes.resize(p->nlanes);
-    // CHUNKER_AMD_PIPE_BSTREAMS (1..4, read per pipeline): boundary streams (A/B)
-    if (const char *e = getenv("CHUNKER_AMD_PIPE_BSTREAMS")) p->nb = std::min<uint32_t>(std::max(atoi(e), 1), PIPE_MAX_BSTREAMS);
-    for (uint32_t i = 0; i < p->nb; ++i)
-        if ((rc = make_stream(&p->bstream[i], true))) return rc;
-    for (auto &L : p->lanes)
-        if ((rc = make_stream(&L.st, false))) return rc;
-    *out = p.release();
+    *out = p.release();  // the streams come with the first batch (start_streams)
+    return CG_OK;
+}
+
+// The pipeline's streams, made at its first batch (pipeline lock held).  Boundary streams:
+// two for batches under 4 GiB -- beside the merged digests the lean scan takes ~1.1 ms per
+// GiB, so one stream forms a group of twenty 1 GiB batches in ~23 ms, about the rate three
+// lanes digest them -- one from 4 GiB on (the persistent scan; a second measured slower on
+// config 4); one for a pipeline that starts with a BLAKE3 batch (run whole in
+// order).  CHUNKER_AMD_PIPE_BSTREAMS=1..4 (A/B) overrides.
+static int start_streams(cg_pipeline *p, uint64_t batch_bytes, int algo) {
+    if (p->nb) return CG_OK;
+    uint32_t nb = algo == CG_SHA256 && batch_bytes < (4ull << 30) ? 2u : 1u;
+    if (const char *e = getenv("CHUNKER_AMD_PIPE_BSTREAMS")) nb = std::min<uint32_t>(std::max(atoi(e), 1), PIPE_MAX_BSTREAMS);
+    const int kind = pipe_stream_kind();
+    const bool low = kind == 3 || (kind == 1 && nb + p->nlanes > 4);
+    std::vector<hipStream_t> made;
+    int rc = CG_OK;
+    for (uint32_t i = 0; i < nb + p->nlanes && !rc; ++i) {
+        hipStream_t st = nullptr;
+        if (!(rc = make_stream(&st, i >= nb && low))) made.push_back(st);
+    }
+    if (rc) {  // nothing is kept: the next batch tries again
+        for (hipStream_t st : made) (void)hipStreamDestroy(st);
+        return rc;
+    }
+    for (uint32_t i = 0; i < nb; ++i) p->bstream[i] = made[i];
+    for (uint32_t i = 0; i < p->nlanes; ++i) p->lanes[i].st = made[nb + i];
+    p->nb = nb;
     return CG_OK;
 }
 
@@ -325,6 +349,10 @@ int cg_pipeline_submit(cg_pipeline *p, const uint8_t *d_data, const uint64_t *na
     Workspace *ws = nullptr;
     if ((rc = acquire(&ws))) return rc;
     std::lock_guard<std::mutex> lk(p->mu);
+    if ((rc = start_streams(p, n_nars ? nar_offsets[n_nars] : 0, algo))) {
+        release(ws);
+        return rc;
+    }
     hipStream_t bs = p->bstream[p->next_b];
     p->next_b = (p->next_b + 1) % p->nb;
     auto undo = [&](int code) {

@@ -108,7 +108,7 @@ def test_default_depth_and_group():
     4 from 4 GiB, 2 for BLAKE3, never more than the hardware queues less 2 (each batch in
     flight holds a stream of its own); the queue count defaults to what the library saw at
     load (cg_hw_queues), not the environment's current value.  Digest pipeline: 16 GiB of
-    batches per merged SHA-256 launch (1 GiB -> 16, 16 GiB -> 1), BLAKE3 unmerged."""
+    batches per merged SHA-256 launch (1 GiB -> 24, 16 GiB -> 2), BLAKE3 unmerged."""
     G = 1 << 30
     dd = chunking.default_depth
     assert dd(1, G, 22) == 20 and dd(1, G, 32) == 20 and dd(1, G, 16) == 14
@@ -119,6 +119,9 @@ def test_default_depth_and_group():
     assert dg(1, G) == 24 and dg(1, 4 * G) == 6 and dg(1, 16 * G) == 2 and dg(1, 64 << 20) == 64
     assert dg(1, 32 * G) == 1
     assert dg(0, G) == 1
+    # lanes: four for SHA-256 batches under 4 GiB (two boundary streams in the library), else three
+    dl = chunking.default_lanes
+    assert dl(1, G) == 4 and dl(1, 4 * G - 1) == 4 and dl(1, 4 * G) == 3 and dl(1, 16 * G) == 3 and dl(0, G) == 3
 
 
 def test_batch_pipeline_order_depth_and_drain(monkeypatch):
