@@ -77,6 +77,42 @@ struct PipeLane {
     std::shared_ptr<PipeGroup> last;
 };
 
+// Lane staggering (device side).  Lanes whose groups form faster than they digest start
+// their launches together -- the fill submits (lanes + 1) groups at once -- and stay in
+// phase: completions then come in bursts of `lanes` groups, and any window of one group's
+// completions reads anywhere from 0.7x to 1.4x the steady rate (profiles/r06_v36_*).  So each
+// lane's launch first waits (k_pipe_stagger, one wave) until `ema / lanes` after the latest
+// launch on any lane, ema = the lanes' recent launch durations (k_pipe_end after each merged
+// digest).  Times are s_memrealtime ticks (100 MHz); a wait never exceeds 50 ms.
+struct PipeClock {
+    unsigned long long last_start, ema, start[8];
+};
+
+__global__ void k_pipe_stagger(PipeClock *c, uint32_t lane, uint32_t nlanes) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long last = __hip_atomic_load(&c->last_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long ema = __hip_atomic_load(&c->ema, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long target = last + ema / nlanes;
+    unsigned long long now = t0;
+    while (last && ema && now < target && now - t0 < 5000000ull) {
+        __builtin_amdgcn_s_sleep(32);
+        now = __builtin_amdgcn_s_memrealtime();
+    }
+    __hip_atomic_store(&c->start[lane], now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&c->last_start, now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ void k_pipe_end(PipeClock *c, uint32_t lane) {
+    if (threadIdx.x != 0) return;
+    const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long st = __hip_atomic_load(&c->start[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long ema = __hip_atomic_load(&c->ema, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!st || now <= st) return;
+    const unsigned long long d = now - st;
+    __hip_atomic_store(&c->ema, ema ? (3 * ema + d) / 4 : d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace cgrt
 
 struct cg_pipeline {
@@ -87,6 +123,7 @@ struct cg_pipeline {
     uint32_t nb = 0, next_b = 0;  // nb 0: no batch yet (start_streams)
     std::vector<cgrt::PipeLane> lanes;
     uint32_t next_lane = 0;
+    cgrt::DevBuf clock;  // PipeClock (lane staggering)
     std::shared_ptr<cgrt::PipeGroup> open;
     std::mutex mu;
     // counters (cg_pipeline_stats)
@@ -113,6 +150,15 @@ static int pipe_stream_kind() {
         return 1;
     }();
     return k;
+}
+
+// Lane staggering on (default) / off (CHUNKER_AMD_PIPE_STAGGER=0, read once; A/B).
+static bool pipe_stagger() {
+    static const bool on = [] {
+        const char *e = getenv("CHUNKER_AMD_PIPE_STAGGER");
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 
 static int make_stream(hipStream_t *s, bool low) {
@@ -191,8 +237,12 @@ static int flush_locked(cg_pipeline *p) {
                         L.mmember.as<uint32_t>(), L.mtotal.as<uint64_t>(), L.morder.as<uint32_t>(),
                         L.remain.as<uint32_t>(), L.merr.as<uint32_t>(),  L.mflag.as<uint32_t *>(),
                         L.err.as<uint32_t>()};
+        const uint32_t lane = (uint32_t)(&L - p->lanes.data());
+        PipeClock *clk = p->clock.as<PipeClock>();
+        if (clk && pipe_stagger()) hipLaunchKernelGGL(k_pipe_stagger, dim3(1), dim3(64), 0, L.st, clk, lane, p->nlanes);
         cg::launch_sha256_pipe(t, bound, expected, max_len, pb, L.st, g->timed ? g->t0 : nullptr,
                                g->timed ? g->t1 : nullptr);
+        if (clk && pipe_stagger()) hipLaunchKernelGGL(k_pipe_end, dim3(1), dim3(64), 0, L.st, clk, lane);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(g->done, L.st));
         return CG_OK;
@@ -322,6 +372,11 @@ static int start_streams(cg_pipeline *p, uint64_t batch_bytes, int algo) {
         if (!(rc = make_stream(&st, i >= nb && low))) made.push_back(st);
     }
     if (rc) {  // nothing is kept: the next batch tries again
+        for (hipStream_t st : made) (void)hipStreamDestroy(st);
+        return rc;
+    }
+    if ((rc = p->clock.ensure(sizeof(PipeClock), "pipeline clock")) ||
+        (rc = hipMemset(p->clock.p, 0, sizeof(PipeClock)) == hipSuccess ? CG_OK : fail(CG_E_IO, "hipMemset failed"))) {
         for (hipStream_t st : made) (void)hipStreamDestroy(st);
         return rc;
     }
@@ -482,6 +537,7 @@ void cg_pipeline_destroy(cg_pipeline *p) {
         }
         for (hipStream_t b : p->bstream)
             if (b) (void)hipStreamDestroy(b);
+        p->clock.release();
     }
     delete p;
 }
