@@ -366,7 +366,7 @@ def main():
     if multi:
         dist.barrier()
     # Fill (untimed): depth - 1 steps queued, the pipeline's groups forming and launching;
-    # then settle (untimed): at least `depth` more steps submitted and completed one for one,
+    # then settle (untimed): at least `depth` (and 4 x lanes groups) more steps submitted and completed one for one,
     # as in every step of a long run, ending at the completion of a whole group.  The timed
     # region then counts completions in steady state, from one group's
     # end to another's.
@@ -381,7 +381,10 @@ def main():
     def count(kk, waited):
         settled[0] += 1
 
-    while settled[0] < depth or (group and (last["k"] + 1) % group):
+    # (settle >= 4 x lanes groups: with four lanes the lanes' phases take a few cycles to even
+    # out, profiles/r06_v37_summary.txt)
+    n_settle = max(depth, 4 * lanes * group) if group else depth
+    while settled[0] < n_settle or (group and (last["k"] + 1) % group):
         submit_next(count)
     settle_ms = (time.perf_counter() - t_settle) * 1e3
     # t0: the caller's own streams are idle (torch's current stream and the gather's), the
