@@ -440,12 +440,10 @@ PIPE_LANES = 3               # merged digests in flight (cg_pipeline_create lane
 
 
 def default_lanes(hash: HashAlgorithm, batch_bytes: int) -> int:
-    """Merged digest launches in flight: four for SHA-256 batches under 4 GiB (the library
-    then runs their boundary stages on two streams, and the lanes in HIP's low-priority
-    queue pool: config 2 at 20 x 4 861-903 GiB/s against 791-808 at 20 x 3,
-    profiles/r06_v35_summary.txt), three otherwise."""
-    if HashAlgorithm(hash) == HashAlgorithm.Sha256 and int(batch_bytes) < (4 << 30):
-        return 4
+    """Merged digest launches in flight: three.  (Four with two boundary streams raise config
+    2's steady rate ~7 %, but their phases drift and a 20-batch window reads 0.7-1.1x of it,
+    profiles/r06_v38_summary.txt; lanes= and CHUNKER_AMD_PIPE_BSTREAMS select that form.)"""
+    del hash, batch_bytes
     return PIPE_LANES
 
 

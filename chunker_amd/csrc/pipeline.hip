@@ -353,15 +353,15 @@ int cg_pipeline_create(int device, uint32_t group_batches, uint32_t lanes, cg_pi
     return CG_OK;
 }
 
-// The pipeline's streams, made at its first batch (pipeline lock held).  Boundary streams:
-// two for batches under 4 GiB -- beside the merged digests the lean scan takes ~1.1 ms per
-// GiB, so one stream forms a group of twenty 1 GiB batches in ~23 ms, about the rate three
-// lanes digest them -- one from 4 GiB on (the persistent scan; a second measured slower on
-// config 4); one for a pipeline that starts with a BLAKE3 batch (run whole in
-// order).  CHUNKER_AMD_PIPE_BSTREAMS=1..4 (A/B) overrides.
+// The pipeline's streams, made at its first batch (pipeline lock held): one boundary stream
+// (CHUNKER_AMD_PIPE_BSTREAMS=1..4, A/B: two boundary streams and four lanes raise config 2's
+// steady rate ~7 % but leave the lanes' phases loose, so a 20-batch window reads 0.7-1.1x of
+// it), then the lanes.
 static int start_streams(cg_pipeline *p, uint64_t batch_bytes, int algo) {
     if (p->nb) return CG_OK;
-    uint32_t nb = algo == CG_SHA256 && batch_bytes < (4ull << 30) ? 2u : 1u;
+    (void)batch_bytes;
+    (void)algo;
+    uint32_t nb = 1;
     if (const char *e = getenv("CHUNKER_AMD_PIPE_BSTREAMS")) nb = std::min<uint32_t>(std::max(atoi(e), 1), PIPE_MAX_BSTREAMS);
     const int kind = pipe_stream_kind();
     const bool low = kind == 3 || (kind == 1 && nb + p->nlanes > 4);

@@ -274,7 +274,7 @@ def test_pipeline_device_argument(ca):
 @pytest.mark.slow
 def test_pipeline_bench_shape_distinct_c2(ca, O):
     """The shape bench.py times: BASELINE config 2 batches (256 x 4 MiB NARs, 256K/1M/4M)
-    through the default BatchPipeline (group 24, 4 lanes, depth 120) over depth + 4 DISTINCT
+    through the default BatchPipeline (group 24, 3 lanes, depth 96) over depth + 4 DISTINCT
     batches, each in its own input and output array, at this process's hardware queues
     (HIP's default 4: the pipeline needs no more).  Every batch equals the per-batch entry
     on the same input, and one sampled NAR of every batch equals the oracle."""

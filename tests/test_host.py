@@ -119,9 +119,9 @@ def test_default_depth_and_group():
     assert dg(1, G) == 24 and dg(1, 4 * G) == 6 and dg(1, 16 * G) == 2 and dg(1, 64 << 20) == 64
     assert dg(1, 32 * G) == 1
     assert dg(0, G) == 1
-    # lanes: four for SHA-256 batches under 4 GiB (two boundary streams in the library), else three
+    # lanes: three (four with two boundary streams only as an A/B)
     dl = chunking.default_lanes
-    assert dl(1, G) == 4 and dl(1, 4 * G - 1) == 4 and dl(1, 4 * G) == 3 and dl(1, 16 * G) == 3 and dl(0, G) == 3
+    assert dl(1, G) == 3 and dl(1, 16 * G) == 3 and dl(0, G) == 3
 
 
 def test_batch_pipeline_order_depth_and_drain(monkeypatch):
