@@ -152,11 +152,13 @@ static int pipe_stream_kind() {
     return k;
 }
 
-// Lane staggering on (default) / off (CHUNKER_AMD_PIPE_STAGGER=0, read once; A/B).
+// Lane staggering off (default) / on (CHUNKER_AMD_PIPE_STAGGER=1, read once; A/B): at three
+// lanes the boundary stream spaces the launches by itself; the wait measured neutral on
+// config 2 and cost configs 4 / 5 their 20-step lines (profiles/r06_v40_summary.txt).
 static bool pipe_stagger() {
     static const bool on = [] {
         const char *e = getenv("CHUNKER_AMD_PIPE_STAGGER");
-        return !(e && e[0] == '0');
+        return e && e[0] == '1';
     }();
     return on;
 }
