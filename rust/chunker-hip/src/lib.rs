@@ -286,7 +286,7 @@ impl Drop for BatchInFlight {
 /// across the worker's consecutive chunk_descriptors_with_hash calls, the collect-then-hash
 /// sequence of src/chunking.rs:334-368.  Measured (DESIGN.md §7 "The digest pipeline"):
 /// config 2 (1 GiB batches of 256 x 4 MiB NARs) at group 20, 3 lanes, 80 in flight:
-/// 800-850 GiB/s at HIP's default 4 hardware queues.  Keep (lanes + 1) x group batches in
+/// 736-864 GiB/s at HIP's default 4 hardware queues.  Keep (lanes + 1) x group batches in
 /// flight.  `group` 0 / `lanes` 0 = the engine's defaults (16 / 3).
 pub struct Pipeline(NonNull<CgPipeline>);
 unsafe impl Send for Pipeline {}
