@@ -233,7 +233,7 @@ def main():
     # default -- 20 for the driver's 20 steps)
     group = args.group if args.group >= 0 else timed_group(ca.chunking.default_group(algo, batch_bytes), args.steps)
     lanes = args.lanes or ca.chunking.default_lanes(algo, batch_bytes)
-    depth = args.depth or ((lanes + 1) * group if group else default_depth(algo, batch_bytes))
+    depth = args.depth or (ca.chunking.pipeline_depth(algo, group, lanes) if group else default_depth(algo, batch_bytes))
     # Distinct inputs: every in-flight slot owns its own batch of NARs (global NAR indices
     # slot * n_per * world + this rank's shard, the reference's per-NAR seeds,
     # crates/node/src/lib.rs:191-203) and output array.  Slot k % depth is reused by step k
@@ -768,7 +768,7 @@ def e2e_one_caller(ca, torch, bufs, offs, nbytes, cap, params, algo, want, args)
     host = bufs[0][0]
     group = args.group if args.group >= 0 else ca.chunking.default_group(algo, nbytes)
     lanes = args.lanes or ca.chunking.default_lanes(algo, nbytes)
-    depth = args.depth or ((lanes + 1) * group if group else default_depth(algo, nbytes))
+    depth = args.depth or (ca.chunking.pipeline_depth(algo, group, lanes) if group else default_depth(algo, nbytes))
     reps = 3 * depth
     dins = [torch.empty(nbytes + 256, dtype=torch.uint8, device="cuda") for _ in range(depth)]
     douts = [torch.empty(cap * 48, dtype=torch.uint8, device="cuda") for _ in range(depth)]

@@ -439,6 +439,15 @@ PIPE_GROUP_BYTES = 24 << 30  # bytes of batches one merged SHA-256 digest launch
 PIPE_LANES = 3               # merged digests in flight (cg_pipeline_create lanes; default_lanes)
 
 
+def pipeline_depth(hash: HashAlgorithm, group: int, lanes: int) -> int:
+    """Batches in flight for the digest pipeline: (lanes + 1) x group for SHA-256 (every lane
+    busy while the next group forms); 8 for BLAKE3, whose batches run whole on the
+    pipeline's three boundary streams (profiles/r06_v42_summary.txt)."""
+    if HashAlgorithm(hash) != HashAlgorithm.Sha256:
+        return 8
+    return (lanes + 1) * group
+
+
 def default_lanes(hash: HashAlgorithm, batch_bytes: int) -> int:
     """Merged digest launches in flight: three.  (Four with two boundary streams raise config
     2's steady rate ~7 %, but their phases drift and a 20-batch window reads 0.7-1.1x of it,
@@ -502,7 +511,7 @@ class BatchPipeline:
         if self.group:
             self._p = pipeline_create(self.device, self.group, self.lanes)
             if self.depth is None:
-                self.depth = (self.lanes + 1) * self.group
+                self.depth = pipeline_depth(self.hash, self.group, self.lanes)
         elif self.depth is None:
             self.depth = default_depth(self.hash, batch_bytes)
 

@@ -356,14 +356,16 @@ int cg_pipeline_create(int device, uint32_t group_batches, uint32_t lanes, cg_pi
 }
 
 // The pipeline's streams, made at its first batch (pipeline lock held): one boundary stream
-// (CHUNKER_AMD_PIPE_BSTREAMS=1..4, A/B: two boundary streams and four lanes raise config 2's
-// steady rate ~7 % but leave the lanes' phases loose, so a 20-batch window reads 0.7-1.1x of
-// it), then the lanes.
+// for SHA-256 (CHUNKER_AMD_PIPE_BSTREAMS=1..4, A/B: two boundary streams and four lanes raise
+// config 2's steady rate ~7 % but leave the lanes' phases loose, so a 20-batch window reads
+// 0.7-1.1x of it), three for a pipeline that starts with a BLAKE3 batch -- its
+// digest runs whole on the boundary stream, so consecutive batches on three streams overlap
+// one's scan with another's digest (config 3: 1498-1516 -> 1566-1572 GiB/s, steady window
+// 1549-1558 -> 1698-1708, profiles/r06_v42_summary.txt) -- then the lanes.
 static int start_streams(cg_pipeline *p, uint64_t batch_bytes, int algo) {
     if (p->nb) return CG_OK;
     (void)batch_bytes;
-    (void)algo;
-    uint32_t nb = 1;
+    uint32_t nb = algo == CG_BLAKE3 ? 3u : 1u;
     if (const char *e = getenv("CHUNKER_AMD_PIPE_BSTREAMS")) nb = std::min<uint32_t>(std::max(atoi(e), 1), PIPE_MAX_BSTREAMS);
     const int kind = pipe_stream_kind();
     const bool low = kind == 3 || (kind == 1 && nb + p->nlanes > 4);
