@@ -26,8 +26,8 @@
 // beside 16 busy ordinary streams at GPU_MAX_HW_QUEUES=4, where three ordinary streams took
 // 5x as long).  A full-CU-mask stream also gets a queue of its own, but HIP creates it as a
 // blocking stream (it then synchronises with the legacy null stream, which torch and other
-// callers use).  BLAKE3 batches (a digest that fills the chip by itself) run whole on the
-// boundary stream, in submission order.
+// callers use).  BLAKE3 batches (a digest that fills the chip by itself) run whole on a
+// boundary stream (three when the pipeline starts with one: start_streams).
 // Replaces, across a caller's consecutive chunk_descriptors_with_hash calls, the
 // collect-then-hash sequence of src/chunking.rs:334-368.
 #include <chrono>
@@ -422,7 +422,7 @@ int cg_pipeline_submit(cg_pipeline *p, const uint8_t *d_data, const uint64_t *na
     if (inputs_ready && hipStreamWaitEvent(bs, static_cast<hipEvent_t>(inputs_ready), 0) != hipSuccess)
         return undo(fail(CG_E_IO, "hipStreamWaitEvent(inputs_ready) failed"));
     BatchLaunch bl;
-    if (algo == CG_BLAKE3) {  // the whole batch on the boundary stream, in submission order
+    if (algo == CG_BLAKE3) {  // the whole batch on its boundary stream
         if ((rc = launch_batch(ws, d_data, nar_offsets, n_nars, o, algo, d_out, out_cap, bs, nullptr, nullptr, true,
                                &bl)))
             return undo(rc);

@@ -142,7 +142,8 @@ int cg_chunk_batch_device_async_after(const uint8_t *d_data, const uint64_t *nar
  * launched when it is full, when one of its batches is waited for (cg_batch_wait,
  * cg_batch_event) or by cg_pipeline_flush.  Each batch completes as soon as its own chunks
  * are digested (the digest kernel signals it), not when its whole group does.  BLAKE3
- * batches run whole on the boundary stream, in submission order.  The pipeline uses
+ * batches run whole on a boundary stream (a pipeline whose first batch is BLAKE3 has three,
+ * used in turn, so consecutive batches overlap).  The pipeline uses
  * 1 + lanes non-blocking high-priority streams on `device` (-1 = the current device; the
  * caller's current device is left unchanged by every pipeline call), which HIP keeps off
  * the hardware queues of the process's ordinary streams whatever GPU_MAX_HW_QUEUES is (its
